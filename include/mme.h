@@ -1,0 +1,173 @@
+/*
+ * mme.h — C ABI of libmme, the MI355X (gfx950) hot path of the
+ * multimodal-embedding retrieval engine.
+ *
+ * Drop-in boundary: the reference (sariekr/multimodal-embedding,
+ * main.py) has no native code; its hot path is the duck-typed HF model /
+ * processor pair consumed by
+ *   encode_data               main.py:386-438
+ *   compute_similarity_scores main.py:440-475
+ *   compute_metrics_detailed  main.py:305-383
+ * Every entry point below replaces one arithmetic step those functions reach
+ * through PyTorch / HF / PIL / colpali_engine; the step is cited per function.
+ *
+ * Conventions
+ *   - all tensor pointers are DEVICE pointers owned by the caller; libmme never
+ *     allocates or frees caller memory. Scratch comes from a caller workspace.
+ *   - `stream` is a hipStream_t passed as void* (0 = legacy default stream).
+ *   - bf16 tensors are IEEE bfloat16 bit patterns (uint16), row-major, with an
+ *     explicit leading dimension (`ld*`, in elements).
+ *   - return value: MME_OK (0) or an error code; mme_last_error() gives text
+ *     (thread-local). Kernels are only launched after all argument checks pass.
+ */
+#ifndef MME_H_
+#define MME_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MME_OK 0
+#define MME_ERR_ARG 1         /* bad shape / pointer / alignment           */
+#define MME_ERR_HIP 2         /* HIP runtime error at launch               */
+#define MME_ERR_UNSUPPORTED 3 /* valid request this build does not handle  */
+
+#define MME_ABI_VERSION 1
+
+/* activation codes for mme_gemm (HF config.hidden_act) */
+#define MME_ACT_NONE 0
+#define MME_ACT_GELU_TANH 1  /* "gelu_pytorch_tanh" (SigLIP)        */
+#define MME_ACT_QUICK_GELU 2 /* "quick_gelu" (OpenAI CLIP, DFN5B)   */
+#define MME_ACT_GELU_ERF 3   /* "gelu" (LAION ViT-H/14)             */
+
+/* output kinds for mme_preprocess_u8 */
+#define MME_PIX_F32_NCHW 0 /* pixel_values fp32 [n,3,S,S] (HF processor output)   */
+#define MME_PIX_PATCHES 1  /* bf16 im2col patches [n*(S/p)^2, kpad] (fused path)  */
+
+const char* mme_last_error(void);
+int mme_abi_version(void);
+
+/* ---------------------------------------------------------------- a2 ----
+ * PIL-exact bicubic resize of u8 RGB images + rescale(1/255) + normalise.
+ * Replaces processor(images=...) main.py:407 -> HF PIL backend
+ * (image_processing_backends.py PilBackend._preprocess: resize, center_crop,
+ * rescale, normalize) -> PIL Image.resize(BICUBIC) (libImaging/Resample.c).
+ * imgs  : u8 [n, H, W, 3] (NHWC, as PIL's RGB raster)
+ * (rh, rw) resized size, then a crop of S x S at (top, left) (CLIP center crop;
+ *          SigLIP: rh = rw = S, top = left = 0).
+ * out   : MME_PIX_F32_NCHW -> float [n,3,S,S]
+ *         MME_PIX_PATCHES  -> bf16 [n*(S/patch)^2, kpad], column c*p*p+ky*p+kx
+ *                             (Conv2d weight flattening), zero for col >= 3*p*p.
+ * mean3/std3: HOST float[3] (per-channel, copied into the kernel arguments).
+ * workspace: >= mme_preprocess_workspace_bytes(n, H, W, rh, rw) bytes. */
+size_t mme_preprocess_workspace_bytes(int n, int H, int W, int rh, int rw);
+int mme_preprocess_u8(const uint8_t* imgs, int n, int H, int W, int rh, int rw, int top, int left,
+                      int S, const float* mean3, const float* std3, int out_kind, int patch, int kpad,
+                      void* out, void* workspace, size_t ws_bytes, void* stream);
+
+/* im2col of fp32 / bf16 pixel_values [n,3,S,S] -> bf16 patches [n*(S/p)^2, kpad].
+ * Replaces the Conv2d(k=s=patch) input side of SiglipVisionEmbeddings /
+ * CLIPVisionEmbeddings (TF:models/siglip/modeling_siglip.py:175-186). in_is_f32:1/0 */
+int mme_im2col(const void* pixels, int in_is_f32, int n, int S, int patch, int kpad, void* out,
+               void* stream);
+
+/* ---------------------------------------------------------------- a4/a5 ----
+ * C[M,N] = act(A[M,K] . B[N,K]^T + bias[N]) + residual[r(row), N]
+ * r(row) = row if res_period == 0 else row % res_period (position-table add).
+ * Replaces nn.Linear / Conv2d GEMMs of the SigLIP / CLIP towers
+ * (TF:models/siglip/modeling_siglip.py:268-322, TF:models/clip/modeling_clip.py).
+ * bf16 in, fp32 accumulate (MFMA 16x16x32), bf16 out (or fp32 if out_f32).
+ * Requires K % 64 == 0, N % 8 == 0, lda/ldb/ldc/ldr % 8 == 0, 16-B aligned rows. */
+int mme_gemm(const void* A, int lda, const void* B, int ldb, void* C, int ldc, int M, int N, int K,
+             const void* bias, const void* residual, int ldr, int res_period, int act, int out_f32,
+             void* stream);
+
+/* LayerNorm over the last dim (fp32 statistics), bf16 in/out.
+ * y[r] = (x[r]-mean)*rsqrt(var+eps)*gamma + beta. Replaces nn.LayerNorm
+ * (TF:models/siglip/modeling_siglip.py:329-331). If `rows_idx` is non-null,
+ * output row r reads input row rows_idx[r] (fused gather for pooling). */
+int mme_layernorm(const void* x, int ldx, const void* gamma, const void* beta, void* y, int ldy, int rows,
+                  int d, float eps, const int32_t* rows_idx, void* stream);
+
+/* Multi-head attention softmax(Q K^T * scale + mask) V over packed QKV rows.
+ * qkv: bf16 [B*T, ld_qkv], Q at column 0, K at H*hd, V at 2*H*hd; head h at h*hd.
+ * out: bf16 [B*T, ld_out], head h at column h*hd.
+ * seq_lens (int32[B], nullable): key padding (keys >= len masked).
+ * causal: keys > query masked (CLIP text, TF:models/clip/modeling_clip.py:543-555).
+ * hd in {64, 72, 80}. Replaces eager/SDPA attention (TF:…siglip.py:228-247). */
+int mme_attention(const void* qkv, int ld_qkv, void* out, int ld_out, int B, int T, int H, int hd,
+                  const int32_t* seq_lens, int causal, float scale, void* stream);
+
+/* SigLIP MAP pooling-head attention: one probe query per head against the
+ * T keys/values of each image. q: bf16 [H*hd] (already projected);
+ * kv: bf16 [B*T, ld_kv], K at col 0, V at col H*hd. out: bf16 [B, ld_out].
+ * Replaces nn.MultiheadAttention in SiglipMultiheadAttentionPoolingHead
+ * (TF:models/siglip/modeling_siglip.py:622-644). */
+int mme_probe_attention(const void* q, const void* kv, int ld_kv, void* out, int ld_out, int B, int T, int H,
+                        int hd, float scale, void* stream);
+
+/* out[b*L + t, :] = tok[ids[b,t]] + pos[t] (bf16). Replaces SiglipTextEmbeddings /
+ * CLIPTextEmbeddings (TF:models/siglip/modeling_siglip.py:189-224). */
+int mme_token_embed(const int64_t* ids, int B, int L, const void* tok, const void* pos, int d, void* out,
+                    int ld_out, void* stream);
+
+/* CLIP vision embedding assembly + pre_layrnorm (fused):
+ * x[b,0] = cls + pos[0]; x[b,1+p] = patch[b*P+p] + pos[1+p]; y = LN(x).
+ * Replaces CLIPVisionEmbeddings.forward + pre_layrnorm (TF:…clip.py:203-218,642). */
+int mme_clip_embed_ln(const void* patch, int ld_patch, const void* cls, const void* pos, const void* gamma,
+                      const void* beta, float eps, void* out, int ld_out, int B, int P, int d, void* stream);
+
+/* Pooling positions for text towers: pos[b] = first t with ids[b,t]==eos_id
+ * (mode 0), argmax_t ids[b,t] (mode 1, legacy eos_token_id==2 configs), or
+ * L-1 (mode 2, SigLIP last position TF:…siglip.py:539). Output is the ROW
+ * index b*L + pos. Replaces TF:models/clip/modeling_clip.py:561-581. */
+int mme_text_pool_rows(const int64_t* ids, int B, int L, int64_t eos_id, int mode, int32_t* rows_out,
+                       void* stream);
+
+/* ---------------------------------------------------------------- a6 ----
+ * y = bf16( x / bf16( sqrt( sum_fp32 x^2 ) ) ) per row — the exact semantics of
+ * `out / out.norm(dim=-1, keepdim=True)` on a bf16 tensor (main.py:414,434). */
+int mme_l2norm(const void* x, int ldx, void* y, int ldy, int rows, int d, void* stream);
+
+/* ---------------------------------------------------------------- a7/a9 ----
+ * Fused similarity + row top-k:
+ *   S = Q[nq,D] . Db[nd,D]^T (fp32 acc), keep the k best columns per row,
+ *   ordered (score desc, column asc).  k <= 16, D % 64 == 0.
+ * Replaces torch.matmul at main.py:473 + torch.topk at main.py:335,365,375.
+ * workspace >= mme_sim_topk_workspace_bytes(nq, nd, k). */
+size_t mme_sim_topk_workspace_bytes(int nq, int nd, int k);
+int mme_sim_topk(const void* Q, int ldq, const void* Db, int ldd, int nq, int nd, int D, int k, int col_offset,
+                 int32_t* out_idx, float* out_score, void* workspace, size_t ws_bytes, void* stream);
+
+/* Merge `parts` sorted top-k lists per row (e.g. per-rank partial results):
+ * in_idx/in_score [rows, parts*k] -> out [rows, k], order (score desc, idx asc). */
+int mme_topk_merge(const int32_t* in_idx, const float* in_score, int rows, int parts, int k, int32_t* out_idx,
+                   float* out_score, void* stream);
+
+/* Recall hit counts. For row r the targets are columns
+ *   [tgt_start[r], tgt_start[r] + tgt_count)   (tgt_start nullable -> r*tgt_count)
+ * hits[j] += #rows whose first kk[j] indices contain a target, j < nk.
+ * Replaces the counting loops of compute_metrics_detailed (main.py:331-378). */
+int mme_recall_hits(const int32_t* topk_idx, int rows, int k, const int32_t* tgt_start, int tgt_count,
+                    int row_offset, const int32_t* kk, int nk, int64_t* hits, void* stream);
+
+/* ---------------------------------------------------------------- a8 ----
+ * ColPali late-interaction MaxSim (colpali_engine processor.score,
+ * main.py:467; in-container port TF:models/colpali/processing_colpali.py:256-270):
+ *   score[q,d] = bf16( sum_{i<q_len} bf16( max_{j<d_len} <Q[q,i], D[d,j]> ) )
+ * Q: bf16 [nq, Lq, dim], D: bf16 [nd, Ld, dim] (rows beyond the lengths ignored),
+ * d_zero (u8[nd], nullable): 1 -> the doc was zero-padded in the reference's
+ * chunk, so 0 joins its max (pad_sequence semantics). dim == 128, Ld % 16 == 0.
+ * out: fp32 [nq, nd]. workspace >= mme_maxsim_workspace_bytes(nq, Lq, nd). */
+size_t mme_maxsim_workspace_bytes(int nq, int Lq, int nd);
+int mme_maxsim(const void* Q, const int32_t* q_lens, int nq, int Lq, const void* D, const int32_t* d_lens,
+               const uint8_t* d_zero, int nd, int Ld, int dim, float* out, void* workspace, size_t ws_bytes,
+               void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MME_H_ */

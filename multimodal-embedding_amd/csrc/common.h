@@ -1,0 +1,82 @@
+// Shared device helpers for libmme (gfx950 / CDNA4 only).
+//
+// Everything here is written for 64-lane wavefronts and the gfx950 MFMA /
+// LDS-DMA builtins; there is no other target.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stddef.h>
+
+#include "../../include/mme.h"
+
+typedef __bf16 bf16;
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef unsigned short u16x8 __attribute__((ext_vector_type(8)));
+
+#define LDS_AS __attribute__((address_space(3)))
+#define GLB_AS __attribute__((address_space(1)))
+
+// ---------------------------------------------------------------------------
+// host-side error plumbing (defined in capi.cpp)
+// ---------------------------------------------------------------------------
+int mme_set_error(int code, const char* fmt, ...);
+int mme_check_launch(const char* what);
+
+#define MME_REQUIRE(cond, ...)                                  \
+    do {                                                        \
+        if (!(cond)) return mme_set_error(MME_ERR_ARG, __VA_ARGS__); \
+    } while (0)
+
+static inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
+static inline int cdiv(long a, long b) { return (int)((a + b - 1) / b); }
+
+// ---------------------------------------------------------------------------
+// device helpers
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ float bf2f(bf16 x) { return (float)x; }
+__device__ __forceinline__ bf16 f2bf(float x) { return (bf16)x; }  // RNE (v_cvt_pk_bf16_f32)
+
+__device__ __forceinline__ float bits2f(unsigned short u) {
+    return __uint_as_float(((unsigned)u) << 16);
+}
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+    return v;
+}
+
+// async global -> LDS copy of 16 bytes per lane; LDS destination is the
+// wave-uniform `lds_base` + lane*16 (gfx950 global_load_lds_dwordx4).
+__device__ __forceinline__ void glds16(const void* gsrc, void* lds_base) {
+    __builtin_amdgcn_global_load_lds((const GLB_AS void*)gsrc, (LDS_AS void*)lds_base, 16, 0, 0);
+}
+
+__device__ __forceinline__ void wait_vmcnt0() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+
+// Activation codes shared by the GEMM epilogue and the host (mme.h MME_ACT_*).
+__device__ __forceinline__ float apply_act(float x, int act) {
+    switch (act) {
+        case MME_ACT_GELU_TANH: {  // gelu_pytorch_tanh
+            const float k0 = 0.7978845608028654f, k1 = 0.044715f;
+            float u = k0 * (x + k1 * x * x * x);
+            return 0.5f * x * (1.0f + tanhf(u));
+        }
+        case MME_ACT_QUICK_GELU:  // x * sigmoid(1.702 x)
+            return x / (1.0f + __expf(-1.702f * x));
+        case MME_ACT_GELU_ERF:
+            return 0.5f * x * (1.0f + erff(x * 0.7071067811865476f));
+        default:
+            return x;
+    }
+}

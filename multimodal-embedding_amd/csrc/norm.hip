@@ -1,0 +1,124 @@
+// Row normalisations: LayerNorm (encoder) and the bf16 L2-normalise of the
+// pooled embeddings. HBM-bound wavefront reductions: one 64-lane wave owns a
+// row, 16-byte (8 x bf16) vector loads/stores, statistics in fp32 registers.
+#include "common.h"
+
+namespace {
+
+constexpr int ROWS_PER_BLOCK = 4;  // 4 waves, one row each
+constexpr int MAXC = 4;            // 16-B chunks per lane: d <= 8*64*4 = 2048
+
+__device__ __forceinline__ void load_row(const bf16* xr, int nch, int lane, float (&v)[MAXC][8]) {
+#pragma unroll
+    for (int c = 0; c < MAXC; ++c) {
+        const int ch = lane + c * 64;
+        if (ch < nch) {
+            const u16x8 u = *reinterpret_cast<const u16x8*>(xr + ch * 8);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) v[c][e] = bits2f(u[e]);
+        } else {
+#pragma unroll
+            for (int e = 0; e < 8; ++e) v[c][e] = 0.f;
+        }
+    }
+}
+
+// nn.LayerNorm on a bf16 row (TF:models/siglip/modeling_siglip.py:329-331):
+// fp32 mean / biased variance, y = (x - mean) * rsqrt(var + eps) * gamma + beta.
+__global__ __launch_bounds__(256) void layernorm_kernel(const bf16* __restrict__ x, int ldx,
+                                                        const bf16* __restrict__ g, const bf16* __restrict__ b,
+                                                        bf16* __restrict__ y, int ldy, int rows, int d, float eps,
+                                                        const int32_t* __restrict__ idx) {
+    const int row = blockIdx.x * ROWS_PER_BLOCK + (threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    if (row >= rows) return;
+    const long src = idx ? idx[row] : row;
+    const int nch = d >> 3;
+    float v[MAXC][8];
+    load_row(x + src * ldx, nch, lane, v);
+    float s = 0.f;
+#pragma unroll
+    for (int c = 0; c < MAXC; ++c)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) s += v[c][e];
+    const float mean = wave_sum(s) / d;
+    float s2 = 0.f;
+#pragma unroll
+    for (int c = 0; c < MAXC; ++c) {
+        if (lane + c * 64 < nch) {
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+                const float t = v[c][e] - mean;
+                s2 += t * t;
+            }
+        }
+    }
+    const float rstd = rsqrtf(wave_sum(s2) / d + eps);
+    bf16* yr = y + (long)row * ldy;
+#pragma unroll
+    for (int c = 0; c < MAXC; ++c) {
+        const int ch = lane + c * 64;
+        if (ch < nch) {
+            const u16x8 gu = *reinterpret_cast<const u16x8*>(g + ch * 8);
+            const u16x8 bu = *reinterpret_cast<const u16x8*>(b + ch * 8);
+            bf16x8 o;
+#pragma unroll
+            for (int e = 0; e < 8; ++e) o[e] = f2bf((v[c][e] - mean) * rstd * bits2f(gu[e]) + bits2f(bu[e]));
+            *reinterpret_cast<bf16x8*>(yr + ch * 8) = o;
+        }
+    }
+}
+
+// out / out.norm(dim=-1, keepdim=True) on a bf16 tensor (main.py:414,434):
+// torch reduces the norm in fp32, rounds it to bf16, then divides in fp32 and
+// rounds the quotient: y = bf16(x / float(bf16(sqrt(sum x^2)))).
+__global__ __launch_bounds__(256) void l2norm_kernel(const bf16* __restrict__ x, int ldx, bf16* __restrict__ y,
+                                                     int ldy, int rows, int d) {
+    const int row = blockIdx.x * ROWS_PER_BLOCK + (threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    if (row >= rows) return;
+    const int nch = d >> 3;
+    float v[MAXC][8];
+    load_row(x + (long)row * ldx, nch, lane, v);
+    float s = 0.f;
+#pragma unroll
+    for (int c = 0; c < MAXC; ++c)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) s += v[c][e] * v[c][e];
+    const float nrm = bf2f(f2bf(sqrtf(wave_sum(s))));
+    bf16* yr = y + (long)row * ldy;
+#pragma unroll
+    for (int c = 0; c < MAXC; ++c) {
+        const int ch = lane + c * 64;
+        if (ch < nch) {
+            bf16x8 o;
+#pragma unroll
+            for (int e = 0; e < 8; ++e) o[e] = f2bf(v[c][e] / nrm);
+            *reinterpret_cast<bf16x8*>(yr + ch * 8) = o;
+        }
+    }
+}
+
+}  // namespace
+
+extern "C" int mme_layernorm(const void* x, int ldx, const void* gamma, const void* beta, void* y, int ldy, int rows,
+                             int d, float eps, const int32_t* rows_idx, void* stream) {
+    MME_REQUIRE(x && gamma && beta && y, "mme_layernorm: null pointer");
+    MME_REQUIRE(rows >= 0 && d > 0 && d % 8 == 0 && d <= 8 * 64 * MAXC, "mme_layernorm: d=%d unsupported", d);
+    MME_REQUIRE(ldx % 8 == 0 && ldy % 8 == 0 && ldx >= d && ldy >= d, "mme_layernorm: bad leading dims");
+    if (rows == 0) return MME_OK;
+    hipLaunchKernelGGL(layernorm_kernel, dim3(cdiv(rows, ROWS_PER_BLOCK)), dim3(256), 0, as_stream(stream),
+                       (const bf16*)x, ldx, (const bf16*)gamma, (const bf16*)beta, (bf16*)y, ldy, rows, d, eps,
+                       rows_idx);
+    return mme_check_launch("mme_layernorm");
+}
+
+extern "C" int mme_l2norm(const void* x, int ldx, void* y, int ldy, int rows, int d, void* stream) {
+    MME_REQUIRE(x && y, "mme_l2norm: null pointer");
+    MME_REQUIRE(rows >= 0 && d > 0 && d % 8 == 0 && d <= 8 * 64 * MAXC, "mme_l2norm: d=%d unsupported", d);
+    MME_REQUIRE(ldx % 8 == 0 && ldy % 8 == 0 && ldx >= d && ldy >= d, "mme_l2norm: bad leading dims");
+    if (rows == 0) return MME_OK;
+    hipLaunchKernelGGL(l2norm_kernel, dim3(cdiv(rows, ROWS_PER_BLOCK)), dim3(256), 0, as_stream(stream),
+                       (const bf16*)x, ldx, (bf16*)y, ldy, rows, d);
+    return mme_check_launch("mme_l2norm");
+}

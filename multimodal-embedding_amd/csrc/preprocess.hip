@@ -1,0 +1,258 @@
+// Image preprocessing on the device: PIL-exact BICUBIC resize of u8 RGB
+// images, center crop, rescale(1/255) and normalise — what
+// processor(images=batch) does on the host in the reference (main.py:407 ->
+// HF PilBackend._preprocess -> PIL Image.resize(BICUBIC)).
+//
+// PIL's algorithm (libImaging/Resample.c, restated; no PIL source is used):
+//   * per output coordinate xx: scale = in/out, filterscale = max(scale, 1),
+//     support = 2 * filterscale, center = (xx + 0.5) * scale,
+//     xmin = max((int)(center - support + 0.5), 0),
+//     xmax = min((int)(center + support + 0.5), in) - xmin,
+//     w_x = bicubic((x + xmin - center + 0.5) / filterscale), normalised by
+//     their sum, then converted to 22-bit fixed point
+//     (int)(w * 2^22 +- 0.5) — all in IEEE double, no FMA contraction;
+//   * horizontal pass first, then vertical; each pass accumulates
+//     int32 sum = 2^21 + sum(u8 * coeff) and clips (sum >> 22) to [0, 255];
+//   * HF then computes float32(float64(u8) * (1/255)) and (x - mean) / std in
+//     float32 (transformers image_transforms.rescale / normalize).
+// Every step is integer or correctly-rounded IEEE, so the device result is
+// bit-identical to PIL + HF (pinned by tests/golden/preprocess.npz).
+#include "common.h"
+
+namespace {
+
+constexpr int PREC = 22;
+
+#pragma clang fp contract(off)
+__device__ double bicubic(double x) {
+    const double a = -0.5;
+    if (x < 0.0) x = -x;
+    if (x < 1.0) return ((a + 2.0) * x - (a + 3.0)) * x * x + 1;
+    if (x < 2.0) return (((x - 5) * x + 8) * x - 4) * a;
+    return 0.0;
+}
+
+__host__ __device__ inline int ksize_for(int in, int out) {
+    double scale = (double)in / out;
+    double fs = scale < 1.0 ? 1.0 : scale;
+    double support = 2.0 * fs;
+    return (int)ceil(support) * 2 + 1;
+}
+
+// One thread per output coordinate: bounds[2*xx] = xmin, bounds[2*xx+1] = count,
+// kk[xx*ksize + i] = fixed-point coefficient.
+__global__ void coeffs_kernel(int in, int out, int ksize, int* __restrict__ bounds, int* __restrict__ kk) {
+#pragma clang fp contract(off)
+    const int xx = blockIdx.x * blockDim.x + threadIdx.x;
+    if (xx >= out) return;
+    const double scale = (double)in / out;
+    const double fs = scale < 1.0 ? 1.0 : scale;
+    const double support = 2.0 * fs;
+    const double center = (xx + 0.5) * scale;
+    const double ss = 1.0 / fs;
+    int xmin = (int)(center - support + 0.5);
+    if (xmin < 0) xmin = 0;
+    int xmax = (int)(center + support + 0.5);
+    if (xmax > in) xmax = in;
+    xmax -= xmin;
+    double w[64];
+    double ww = 0.0;
+    for (int x = 0; x < xmax; ++x) {
+        const double v = bicubic((x + xmin - center + 0.5) * ss);
+        w[x] = v;
+        ww += v;
+    }
+    for (int x = 0; x < ksize; ++x) {
+        double k = 0.0;
+        if (x < xmax) k = (ww != 0.0) ? w[x] / ww : w[x];
+        kk[xx * ksize + x] = k < 0 ? (int)(-0.5 + k * (1 << PREC)) : (int)(0.5 + k * (1 << PREC));
+    }
+    bounds[2 * xx] = xmin;
+    bounds[2 * xx + 1] = xmax;
+}
+
+__device__ __forceinline__ int clip8(int v) {
+    v >>= PREC;
+    return v < 0 ? 0 : (v > 255 ? 255 : v);
+}
+
+// Horizontal pass for the cropped columns only: tmp[n][y][xc][3], xc < S.
+__global__ void resample_h_kernel(const uint8_t* __restrict__ img, int n, int H, int W, int S, int left, int ksize,
+                                  const int* __restrict__ bounds, const int* __restrict__ kk,
+                                  uint8_t* __restrict__ tmp) {
+    const long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    const long total = (long)n * H * S;
+    if (t >= total) return;
+    const int xc = t % S;
+    const long ny = t / S;  // n*H + y
+    const int xx = xc + left;
+    const int xmin = bounds[2 * xx], cnt = bounds[2 * xx + 1];
+    const int* k = kk + xx * ksize;
+    const uint8_t* src = img + ny * W * 3;
+    int s0 = 1 << (PREC - 1), s1 = s0, s2 = s0;
+    for (int x = 0; x < cnt; ++x) {
+        const uint8_t* p = src + (xmin + x) * 3;
+        s0 += p[0] * k[x];
+        s1 += p[1] * k[x];
+        s2 += p[2] * k[x];
+    }
+    uint8_t* d = tmp + t * 3;
+    d[0] = (uint8_t)clip8(s0);
+    d[1] = (uint8_t)clip8(s1);
+    d[2] = (uint8_t)clip8(s2);
+}
+
+__device__ __forceinline__ float normalize(int u8, float mean, float stdv) {
+    const float r = (float)((double)u8 * (1.0 / 255.0));
+    return (r - mean) / stdv;
+}
+
+// Vertical pass + rescale/normalise; thread = one output element of the
+// requested layout (coalesced writes).
+struct NormArgs {
+    float mean[3], stdv[3];
+};
+
+__device__ __forceinline__ int vpass(const uint8_t* tmp_img, int S, int yy, int xc, int c, int ksize,
+                                     const int* bounds, const int* kk) {
+    const int ymin = bounds[2 * yy], cnt = bounds[2 * yy + 1];
+    const int* k = kk + yy * ksize;
+    int s = 1 << (PREC - 1);
+    for (int y = 0; y < cnt; ++y) s += tmp_img[((long)(ymin + y) * S + xc) * 3 + c] * k[y];
+    return clip8(s);
+}
+
+__global__ void resample_v_nchw_kernel(const uint8_t* __restrict__ tmp, int n, int H, int S, int top, int ksize,
+                                       const int* __restrict__ bounds, const int* __restrict__ kk, NormArgs na,
+                                       float* __restrict__ out) {
+    const long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    const long total = (long)n * 3 * S * S;
+    if (t >= total) return;
+    const int xc = t % S;
+    const int yc = (t / S) % S;
+    const int c = (t / ((long)S * S)) % 3;
+    const long b = t / (3L * S * S);
+    const int u = vpass(tmp + b * H * S * 3, S, yc + top, xc, c, ksize, bounds, kk);
+    out[t] = normalize(u, na.mean[c], na.stdv[c]);
+}
+
+// patches[row = b*G*G + py*G + px][col = c*p*p + ky*p + kx] (G = S/p), bf16,
+// zero for col >= 3*p*p: the im2col image of Conv2d(k=s=p) fed straight to
+// the patch-embedding GEMM.
+__global__ void resample_v_patch_kernel(const uint8_t* __restrict__ tmp, int n, int H, int S, int top, int ksize,
+                                        const int* __restrict__ bounds, const int* __restrict__ kk, NormArgs na,
+                                        int p, int kpad, bf16* __restrict__ out) {
+    const long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    const int G = S / p;
+    const long total = (long)n * G * G * kpad;
+    if (t >= total) return;
+    const int col = t % kpad;
+    const long row = t / kpad;
+    if (col >= 3 * p * p) {
+        out[t] = f2bf(0.f);
+        return;
+    }
+    const int c = col / (p * p), ky = (col / p) % p, kx = col % p;
+    const int px = row % G, py = (row / G) % G;
+    const long b = row / ((long)G * G);
+    const int u = vpass(tmp + b * H * S * 3, S, py * p + ky + top, px * p + kx, c, ksize, bounds, kk);
+    out[t] = f2bf(normalize(u, na.mean[c], na.stdv[c]));
+}
+
+// Plain im2col of pixel_values (the HF-API path: get_image_features(pixel_values)).
+template <typename T>
+__global__ void im2col_kernel(const T* __restrict__ pix, int n, int S, int p, int kpad, bf16* __restrict__ out) {
+    const long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    const int G = S / p;
+    const long total = (long)n * G * G * kpad;
+    if (t >= total) return;
+    const int col = t % kpad;
+    const long row = t / kpad;
+    if (col >= 3 * p * p) {
+        out[t] = f2bf(0.f);
+        return;
+    }
+    const int c = col / (p * p), ky = (col / p) % p, kx = col % p;
+    const int px = row % G, py = (row / G) % G;
+    const long b = row / ((long)G * G);
+    const float v = (float)pix[((b * 3 + c) * S + py * p + ky) * (long)S + px * p + kx];
+    out[t] = f2bf(v);
+}
+
+size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
+
+}  // namespace
+
+extern "C" size_t mme_preprocess_workspace_bytes(int n, int H, int W, int rh, int rw) {
+    const size_t kx = ksize_for(W, rw), ky = ksize_for(H, rh);
+    return align256((size_t)rw * 2 * 4) + align256((size_t)rw * kx * 4) + align256((size_t)rh * 2 * 4) +
+           align256((size_t)rh * ky * 4) + align256((size_t)n * H * (size_t)rw * 3);
+}
+
+extern "C" int mme_preprocess_u8(const uint8_t* imgs, int n, int H, int W, int rh, int rw, int top, int left, int S,
+                                 const float* mean3, const float* std3, int out_kind, int patch, int kpad, void* out,
+                                 void* workspace, size_t ws_bytes, void* stream) {
+    MME_REQUIRE(imgs && out && workspace && mean3 && std3, "mme_preprocess_u8: null pointer");
+    MME_REQUIRE(n >= 0 && H > 0 && W > 0 && rh > 0 && rw > 0 && S > 0, "mme_preprocess_u8: bad sizes");
+    MME_REQUIRE(top >= 0 && left >= 0 && top + S <= rh && left + S <= rw, "mme_preprocess_u8: crop outside image");
+    MME_REQUIRE(ksize_for(W, rw) <= 64 && ksize_for(H, rh) <= 64, "mme_preprocess_u8: downscale factor too large");
+    MME_REQUIRE(ws_bytes >= mme_preprocess_workspace_bytes(n, H, W, rh, rw),
+                "mme_preprocess_u8: workspace too small");
+    if (out_kind == MME_PIX_PATCHES)
+        MME_REQUIRE(patch > 0 && S % patch == 0 && kpad >= 3 * patch * patch && kpad % 8 == 0,
+                    "mme_preprocess_u8: bad patch/kpad");
+    else
+        MME_REQUIRE(out_kind == MME_PIX_F32_NCHW, "mme_preprocess_u8: bad out_kind %d", out_kind);
+    if (n == 0) return MME_OK;
+    hipStream_t s = as_stream(stream);
+    const int kx = ksize_for(W, rw), ky = ksize_for(H, rh);
+    char* ws = (char*)workspace;
+    int* xb = (int*)ws;
+    ws += align256((size_t)rw * 2 * 4);
+    int* xk = (int*)ws;
+    ws += align256((size_t)rw * kx * 4);
+    int* yb = (int*)ws;
+    ws += align256((size_t)rh * 2 * 4);
+    int* yk = (int*)ws;
+    ws += align256((size_t)rh * ky * 4);
+    uint8_t* tmp = (uint8_t*)ws;
+
+    hipLaunchKernelGGL(coeffs_kernel, dim3(cdiv(rw, 64)), dim3(64), 0, s, W, rw, kx, xb, xk);
+    hipLaunchKernelGGL(coeffs_kernel, dim3(cdiv(rh, 64)), dim3(64), 0, s, H, rh, ky, yb, yk);
+    const long th = (long)n * H * S;
+    hipLaunchKernelGGL(resample_h_kernel, dim3(cdiv(th, 256)), dim3(256), 0, s, imgs, n, H, W, S, left, kx, xb, xk,
+                       tmp);
+    NormArgs na;
+    for (int c = 0; c < 3; ++c) {
+        na.mean[c] = mean3[c];
+        na.stdv[c] = std3[c];
+    }
+    if (out_kind == MME_PIX_F32_NCHW) {
+        const long tv = (long)n * 3 * S * S;
+        hipLaunchKernelGGL(resample_v_nchw_kernel, dim3(cdiv(tv, 256)), dim3(256), 0, s, tmp, n, H, S, top, ky, yb,
+                           yk, na, (float*)out);
+    } else {
+        const int G = S / patch;
+        const long tv = (long)n * G * G * kpad;
+        hipLaunchKernelGGL(resample_v_patch_kernel, dim3(cdiv(tv, 256)), dim3(256), 0, s, tmp, n, H, S, top, ky, yb,
+                           yk, na, patch, kpad, (bf16*)out);
+    }
+    return mme_check_launch("mme_preprocess_u8");
+}
+
+extern "C" int mme_im2col(const void* pixels, int in_is_f32, int n, int S, int patch, int kpad, void* out,
+                          void* stream) {
+    MME_REQUIRE(pixels && out, "mme_im2col: null pointer");
+    MME_REQUIRE(n >= 0 && patch > 0 && S % patch == 0 && kpad >= 3 * patch * patch && kpad % 8 == 0,
+                "mme_im2col: bad shape");
+    if (n == 0) return MME_OK;
+    const int G = S / patch;
+    const long tv = (long)n * G * G * kpad;
+    if (in_is_f32)
+        hipLaunchKernelGGL(im2col_kernel<float>, dim3(cdiv(tv, 256)), dim3(256), 0, as_stream(stream),
+                           (const float*)pixels, n, S, patch, kpad, (bf16*)out);
+    else
+        hipLaunchKernelGGL(im2col_kernel<bf16>, dim3(cdiv(tv, 256)), dim3(256), 0, as_stream(stream),
+                           (const bf16*)pixels, n, S, patch, kpad, (bf16*)out);
+    return mme_check_launch("mme_im2col");
+}

@@ -1,0 +1,238 @@
+// Retrieval: fused similarity GEMM + row top-k, top-k merge, recall counting.
+//
+// Reference path: scores = torch.matmul(txt.float(), img.float().t()) on the
+// CPU (main.py:473, 100 MB / 500 MB fp32 matrices), then one torch.topk per
+// row in a Python loop (main.py:331-378). Here the bf16 x bf16 -> fp32 MFMA
+// GEMM of gemm_core.h feeds a top-k epilogue: each 128 x 128 score tile is
+// spilled to LDS once and scanned by 2 threads per row that keep a sorted
+// (score desc, column asc) list in registers. The score matrix never reaches
+// HBM; per (row, column-split, half) candidate lists go to the workspace and a
+// one-wave-per-row merge produces the final top-k.
+#include "gemm_core.h"
+
+namespace {
+using namespace gemmcore;
+
+constexpr int KMAX = 16;
+using SimCfg = Cfg<128, 128, 2, 2>;
+constexpr int TILE_LD = 128 + 4;  // fp32 score tile row stride in LDS
+constexpr int SIM_LDS = (SimCfg::LDS > 128 * TILE_LD * 4) ? SimCfg::LDS : 128 * TILE_LD * 4;
+
+// Insert (v, idx) into a sorted-desc list; strictly-greater keeps the earlier
+// column first on ties (columns are scanned in increasing order).
+__device__ __forceinline__ void topk_insert(float (&ts)[KMAX], int (&ti)[KMAX], float v, int idx) {
+    if (!(v > ts[KMAX - 1])) return;
+    ts[KMAX - 1] = v;
+    ti[KMAX - 1] = idx;
+#pragma unroll
+    for (int j = KMAX - 1; j > 0; --j) {
+        if (ts[j] > ts[j - 1]) {
+            const float tv = ts[j];
+            ts[j] = ts[j - 1];
+            ts[j - 1] = tv;
+            const int tx = ti[j];
+            ti[j] = ti[j - 1];
+            ti[j - 1] = tx;
+        }
+    }
+}
+
+struct SimArgs {
+    const bf16* Q;
+    const bf16* Dm;
+    int ldq, ldd, nq, nd, D, k, col_offset;
+    int tiles_per_split, nsplit;
+    float* cand_s;  // [nq][nsplit*2][k]
+    int* cand_i;
+};
+
+__global__ __launch_bounds__(SimCfg::NT) void sim_topk_kernel(SimArgs p) {
+    __shared__ __attribute__((aligned(16))) char lds[SIM_LDS];
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wm = wave / SimCfg::WN, wn = wave % SimCfg::WN;
+    const int m0 = blockIdx.x * SimCfg::BM;
+    const int split = blockIdx.y;
+    const int ntiles = (p.nd + SimCfg::BN - 1) / SimCfg::BN;
+    const int t0 = split * p.tiles_per_split, t1 = min(ntiles, t0 + p.tiles_per_split);
+
+    float ts[KMAX];
+    int ti[KMAX];
+#pragma unroll
+    for (int j = 0; j < KMAX; ++j) {
+        ts[j] = -INFINITY;
+        ti[j] = 0x7fffffff;
+    }
+    const int myrow = tid >> 1, half = tid & 1;
+    float* tile = reinterpret_cast<float*>(lds);
+
+    for (int t = t0; t < t1; ++t) {
+        const int n0 = t * SimCfg::BN;
+        f32x4 acc[SimCfg::FM][SimCfg::FN];
+        mainloop<SimCfg>(p.Q, p.ldq, p.nq, m0, p.Dm, p.ldd, p.nd, n0, p.D, lds, acc, wave, lane);
+        __syncthreads();  // staging buffers are dead; reuse LDS for the score tile
+#pragma unroll
+        for (int i = 0; i < SimCfg::FM; ++i)
+#pragma unroll
+            for (int j = 0; j < SimCfg::FN; ++j)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int row = wm * SimCfg::TM + i * 16 + 4 * (lane >> 4) + r;
+                    const int col = wn * SimCfg::TN + j * 16 + (lane & 15);
+                    tile[row * TILE_LD + col] = (n0 + col < p.nd) ? acc[i][j][r] : -INFINITY;
+                }
+        __syncthreads();
+        const float* tr = tile + myrow * TILE_LD + half * 64;
+        const int cbase = n0 + half * 64;
+        for (int c = 0; c < 64; ++c) topk_insert(ts, ti, tr[c], cbase + c);
+        __syncthreads();
+    }
+    const int row = m0 + myrow;
+    if (row < p.nq) {
+        const long o = ((long)row * p.nsplit * 2 + split * 2 + half) * p.k;
+        for (int j = 0; j < p.k; ++j) {
+            p.cand_s[o + j] = ts[j];
+            p.cand_i[o + j] = ti[j] == 0x7fffffff ? -1 : ti[j] + p.col_offset;
+        }
+    }
+}
+
+// One wave per row: repeatedly extract the best (score desc, idx asc) candidate.
+__global__ __launch_bounds__(256) void topk_merge_kernel(const float* __restrict__ cs, const int* __restrict__ ci,
+                                                         int rows, int ncand, int k, int32_t* __restrict__ oi,
+                                                         float* __restrict__ os) {
+    const int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+    if (row >= rows) return;
+    const float* s = cs + (long)row * ncand;
+    const int* ix = ci + (long)row * ncand;
+    // each lane keeps its own best-first cursor over a strided slice
+    constexpr int PER = 16;
+    float vs[PER];
+    int vi[PER];
+#pragma unroll
+    for (int j = 0; j < PER; ++j) {
+        const int c = lane + j * 64;
+        const bool ok = c < ncand && ix[c] >= 0;
+        vs[j] = ok ? s[c] : -INFINITY;
+        vi[j] = ok ? ix[c] : 0x7fffffff;
+    }
+    for (int out = 0; out < k; ++out) {
+        // lane-local best
+        float bv = -INFINITY;
+        int bi = 0x7fffffff, bj = -1;
+#pragma unroll
+        for (int j = 0; j < PER; ++j) {
+            const bool better = vs[j] > bv || (vs[j] == bv && vi[j] < bi);
+            if (better) {
+                bv = vs[j];
+                bi = vi[j];
+                bj = j;
+            }
+        }
+        float wv = bv;
+        int wi = bi;
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) {
+            const float ov = __shfl_xor(wv, o, 64);
+            const int oi2 = __shfl_xor(wi, o, 64);
+            if (ov > wv || (ov == wv && oi2 < wi)) {
+                wv = ov;
+                wi = oi2;
+            }
+        }
+        if (lane == 0) {
+            oi[(long)row * k + out] = wi == 0x7fffffff ? -1 : wi;
+            os[(long)row * k + out] = wv;
+        }
+        if (bj >= 0 && bi == wi && bv == wv) {
+#pragma unroll
+            for (int j = 0; j < PER; ++j)
+                if (j == bj) {
+                    vs[j] = -INFINITY;
+                    vi[j] = 0x7fffffff;
+                }
+        }
+    }
+}
+
+__global__ void recall_kernel(const int32_t* __restrict__ idx, int rows, int k, const int32_t* __restrict__ tstart,
+                              int tcount, int row_offset, const int32_t* __restrict__ kk, int nk,
+                              unsigned long long* __restrict__ hits) {
+    const int r = blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= rows) return;
+    const int lo = tstart ? tstart[r] : (r + row_offset) * tcount;
+    const int hi = lo + tcount;
+    int first = k;  // first rank holding a target
+    for (int j = 0; j < k; ++j) {
+        const int c = idx[(long)r * k + j];
+        if (c >= lo && c < hi) {
+            first = j;
+            break;
+        }
+    }
+    for (int j = 0; j < nk; ++j)
+        if (first < min(kk[j], k)) atomicAdd(&hits[j], 1ull);
+}
+
+size_t sim_splits(int nq, int nd, int k, int* tiles_per_split) {
+    const int nqt = (nq + 127) / 128, ntiles = (nd + 127) / 128;
+    // aim for >= 1024 workgroups, >= 4 tiles per split, and a candidate list
+    // (nsplit * 2 halves * k) the one-wave merge can hold (<= 1024)
+    int nsplit = (1024 + nqt - 1) / nqt;
+    nsplit = min(nsplit, max(1, ntiles / 4));
+    nsplit = min(nsplit, 512 / k);
+    nsplit = max(1, min(nsplit, ntiles));
+    *tiles_per_split = (ntiles + nsplit - 1) / nsplit;
+    nsplit = (ntiles + *tiles_per_split - 1) / *tiles_per_split;
+    return (size_t)nsplit;
+}
+
+}  // namespace
+
+extern "C" size_t mme_sim_topk_workspace_bytes(int nq, int nd, int k) {
+    int tps;
+    const size_t nsplit = sim_splits(nq, nd, k, &tps);
+    return (size_t)nq * nsplit * 2 * k * (sizeof(float) + sizeof(int)) + 256;
+}
+
+extern "C" int mme_sim_topk(const void* Q, int ldq, const void* Db, int ldd, int nq, int nd, int D, int k,
+                            int col_offset, int32_t* out_idx, float* out_score, void* workspace, size_t ws_bytes,
+                            void* stream) {
+    MME_REQUIRE(Q && Db && out_idx && out_score && workspace, "mme_sim_topk: null pointer");
+    MME_REQUIRE(nq >= 0 && nd > 0 && D > 0 && D % 64 == 0, "mme_sim_topk: D=%d must be a multiple of 64", D);
+    MME_REQUIRE(k >= 1 && k <= KMAX && k <= nd, "mme_sim_topk: k=%d out of range (<= %d, <= nd)", k, KMAX);
+    MME_REQUIRE(ldq % 8 == 0 && ldd % 8 == 0 && ldq >= D && ldd >= D, "mme_sim_topk: bad leading dims");
+    MME_REQUIRE(ws_bytes >= mme_sim_topk_workspace_bytes(nq, nd, k), "mme_sim_topk: workspace too small");
+    if (nq == 0) return MME_OK;
+    int tps;
+    const int nsplit = (int)sim_splits(nq, nd, k, &tps);
+    float* cs = (float*)workspace;
+    int* ci = (int*)((char*)workspace + (size_t)nq * nsplit * 2 * k * sizeof(float));
+    SimArgs a{(const bf16*)Q, (const bf16*)Db, ldq, ldd, nq, nd, D, k, col_offset, tps, nsplit, cs, ci};
+    hipStream_t s = as_stream(stream);
+    hipLaunchKernelGGL(sim_topk_kernel, dim3((nq + 127) / 128, nsplit), dim3(SimCfg::NT), 0, s, a);
+    int rc = mme_check_launch("mme_sim_topk");
+    if (rc) return rc;
+    return mme_topk_merge(ci, cs, nq, nsplit * 2, k, out_idx, out_score, stream);
+}
+
+extern "C" int mme_topk_merge(const int32_t* in_idx, const float* in_score, int rows, int parts, int k,
+                              int32_t* out_idx, float* out_score, void* stream) {
+    MME_REQUIRE(in_idx && in_score && out_idx && out_score, "mme_topk_merge: null pointer");
+    MME_REQUIRE(rows >= 0 && parts >= 1 && k >= 1 && (long)parts * k <= 64 * 16,
+                "mme_topk_merge: parts*k=%d exceeds 1024", parts * k);
+    if (rows == 0) return MME_OK;
+    hipLaunchKernelGGL(topk_merge_kernel, dim3(cdiv(rows, 4)), dim3(256), 0, as_stream(stream), in_score, in_idx,
+                       rows, parts * k, k, out_idx, out_score);
+    return mme_check_launch("mme_topk_merge");
+}
+
+extern "C" int mme_recall_hits(const int32_t* topk_idx, int rows, int k, const int32_t* tgt_start, int tgt_count,
+                               int row_offset, const int32_t* kk, int nk, int64_t* hits, void* stream) {
+    MME_REQUIRE(topk_idx && kk && hits, "mme_recall_hits: null pointer");
+    MME_REQUIRE(rows >= 0 && k >= 1 && tgt_count >= 1 && nk >= 1, "mme_recall_hits: bad args");
+    if (rows == 0) return MME_OK;
+    hipLaunchKernelGGL(recall_kernel, dim3(cdiv(rows, 256)), dim3(256), 0, as_stream(stream), topk_idx, rows, k,
+                       tgt_start, tgt_count, row_offset, kk, nk, (unsigned long long*)hits);
+    return mme_check_launch("mme_recall_hits");
+}

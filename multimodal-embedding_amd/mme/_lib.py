@@ -1,0 +1,86 @@
+"""ctypes binding of libmme.so — the C ABI declared in include/mme.h.
+
+The library is built in-tree (``make -C multimodal-embedding_amd``) so it
+travels with the repository. There is deliberately NO fallback: if the
+library is missing or fails to load, every compute entry point raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from ctypes import c_float, c_int, c_int64, c_size_t, c_void_p
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("MME_LIB", os.path.join(_HERE, "libmme.so"))
+
+# MME_ACT_* / MME_PIX_* from include/mme.h
+ACT_NONE, ACT_GELU_TANH, ACT_QUICK_GELU, ACT_GELU_ERF = 0, 1, 2, 3
+PIX_F32_NCHW, PIX_PATCHES = 0, 1
+ABI_VERSION = 1
+
+# name -> (restype, argtypes)
+_P = c_void_p
+SIGNATURES = {
+    "mme_last_error": (ctypes.c_char_p, []),
+    "mme_abi_version": (c_int, []),
+    "mme_preprocess_workspace_bytes": (c_size_t, [c_int] * 5),
+    "mme_preprocess_u8": (c_int, [_P, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, _P, _P, c_int, c_int,
+                                  c_int, _P, _P, c_size_t, _P]),
+    "mme_im2col": (c_int, [_P, c_int, c_int, c_int, c_int, c_int, _P, _P]),
+    "mme_gemm": (c_int, [_P, c_int, _P, c_int, _P, c_int, c_int, c_int, c_int, _P, _P, c_int, c_int, c_int, c_int,
+                         _P]),
+    "mme_layernorm": (c_int, [_P, c_int, _P, _P, _P, c_int, c_int, c_int, c_float, _P, _P]),
+    "mme_attention": (c_int, [_P, c_int, _P, c_int, c_int, c_int, c_int, c_int, _P, c_int, c_float, _P]),
+    "mme_probe_attention": (c_int, [_P, _P, c_int, _P, c_int, c_int, c_int, c_int, c_int, c_float, _P]),
+    "mme_token_embed": (c_int, [_P, c_int, c_int, _P, _P, c_int, _P, c_int, _P]),
+    "mme_clip_embed_ln": (c_int, [_P, c_int, _P, _P, _P, _P, c_float, _P, c_int, c_int, c_int, c_int, _P]),
+    "mme_text_pool_rows": (c_int, [_P, c_int, c_int, c_int64, c_int, _P, _P]),
+    "mme_l2norm": (c_int, [_P, c_int, _P, c_int, c_int, c_int, _P]),
+    "mme_sim_topk_workspace_bytes": (c_size_t, [c_int, c_int, c_int]),
+    "mme_sim_topk": (c_int, [_P, c_int, _P, c_int, c_int, c_int, c_int, c_int, c_int, _P, _P, _P, c_size_t, _P]),
+    "mme_topk_merge": (c_int, [_P, _P, c_int, c_int, c_int, _P, _P, _P]),
+    "mme_recall_hits": (c_int, [_P, c_int, c_int, _P, c_int, c_int, _P, c_int, _P, _P]),
+    "mme_maxsim_workspace_bytes": (c_size_t, [c_int, c_int, c_int]),
+    "mme_maxsim": (c_int, [_P, _P, c_int, c_int, _P, _P, _P, c_int, c_int, c_int, _P, _P, c_size_t, _P]),
+}
+
+
+class MMEError(RuntimeError):
+    """A libmme call returned a non-zero status."""
+
+
+_lib = None
+
+
+def load() -> ctypes.CDLL:
+    """Load libmme.so once and bind every entry point; raise loudly on failure."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise MMEError(
+            f"libmme.so not found at {LIB_PATH}; build it with `make -C multimodal-embedding_amd` "
+            "(or __graft_entry__.build()). There is no CPU fallback.")
+    lib = ctypes.CDLL(LIB_PATH)
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    if lib.mme_abi_version() != ABI_VERSION:
+        raise MMEError(f"libmme ABI {lib.mme_abi_version()} != expected {ABI_VERSION}")
+    _lib = lib
+    return lib
+
+
+def call(name: str, *args) -> None:
+    """Invoke an int-returning entry point and raise MMEError on failure."""
+    lib = load()
+    rc = getattr(lib, name)(*args)
+    if rc != 0:
+        msg = lib.mme_last_error().decode(errors="replace")
+        raise MMEError(f"{name} failed (status {rc}): {msg}")
+
+
+def query(name: str, *args):
+    """Invoke a value-returning entry point (workspace sizes, versions)."""
+    return getattr(load(), name)(*args)

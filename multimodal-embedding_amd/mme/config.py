@@ -1,0 +1,182 @@
+"""Model registry: the dense dual encoders of the reference's model table.
+
+The reference loads these by hub id (main.py:127-142, 808-820); offline, the
+architecture constants below (public HF configs, confirmed by parameter count
+in SURVEY.md §6) are instantiated with seeded random weights or with a local
+safetensors / HF state dict (mme.weights).
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass, field, replace
+from typing import Dict, Optional, Tuple
+
+from ._lib import ACT_GELU_ERF, ACT_GELU_TANH, ACT_QUICK_GELU
+
+OPENAI_CLIP_MEAN = (0.48145466, 0.4578275, 0.40821073)
+OPENAI_CLIP_STD = (0.26862954, 0.26130258, 0.27577711)
+IMAGENET_STANDARD_MEAN = (0.5, 0.5, 0.5)
+IMAGENET_STANDARD_STD = (0.5, 0.5, 0.5)
+
+ACTS = {"gelu_pytorch_tanh": ACT_GELU_TANH, "quick_gelu": ACT_QUICK_GELU, "gelu": ACT_GELU_ERF}
+
+
+@dataclass(frozen=True)
+class TowerConfig:
+    hidden: int
+    intermediate: int
+    layers: int
+    heads: int
+    act: str
+    eps: float
+
+    @property
+    def head_dim(self) -> int:
+        return self.hidden // self.heads
+
+    @property
+    def inter_pad(self) -> int:
+        """Intermediate width padded to a multiple of 128 (zero rows/cols; gelu(0) = 0)."""
+        return (self.intermediate + 127) // 128 * 128
+
+
+@dataclass(frozen=True)
+class VisionConfig(TowerConfig):
+    image_size: int = 224
+    patch: int = 14
+
+    @property
+    def grid(self) -> int:
+        return self.image_size // self.patch
+
+    @property
+    def num_patches(self) -> int:
+        return self.grid ** 2
+
+    @property
+    def kpad(self) -> int:
+        """Patch-embedding GEMM K (3*p*p) padded to a multiple of 64."""
+        return (3 * self.patch * self.patch + 63) // 64 * 64
+
+
+@dataclass(frozen=True)
+class TextConfig(TowerConfig):
+    vocab: int = 49408
+    max_pos: int = 77
+    eos_id: int = 49407
+    bos_id: Optional[int] = 49406
+    pad_id: int = 49407
+    pool: str = "eos"  # "eos" (first eos), "argmax" (legacy eos_token_id == 2), "last" (SigLIP)
+    causal: bool = True
+
+
+@dataclass(frozen=True)
+class ImageProcConfig:
+    size: int                      # final (cropped) size S
+    mode: str                      # "square" (SigLIP: resize to S x S) | "shortest_edge" (CLIP: resize + center crop)
+    mean: Tuple[float, float, float]
+    std: Tuple[float, float, float]
+
+
+@dataclass(frozen=True)
+class ModelSpec:
+    name: str
+    hub_id: str
+    family: str                    # "siglip" | "clip"
+    vision: VisionConfig
+    text: TextConfig
+    proj_dim: int                  # joint embedding width D
+    image_proc: ImageProcConfig
+    batch_size: int = 32           # main.py:131-136 (ARGS.batch_size default 32, main.py:73)
+    extra: Dict[str, str] = field(default_factory=dict)
+
+    @property
+    def m_info(self) -> dict:
+        """The reference's m_info dict (main.py:130-136)."""
+        typ = "siglip" if self.family == "siglip" else "dense"
+        return {"name": self.name, "id": self.hub_id, "type": typ, "batch_size": self.batch_size}
+
+    def with_batch_size(self, bs: int) -> "ModelSpec":
+        return replace(self, batch_size=bs)
+
+
+def _siglip_400m() -> ModelSpec:
+    v = VisionConfig(hidden=1152, intermediate=4304, layers=27, heads=16, act="gelu_pytorch_tanh", eps=1e-6,
+                     image_size=384, patch=14)
+    t = TextConfig(hidden=1152, intermediate=4304, layers=27, heads=16, act="gelu_pytorch_tanh", eps=1e-6,
+                   vocab=32000, max_pos=64, eos_id=1, bos_id=None, pad_id=1, pool="last", causal=False)
+    return ModelSpec("SigLIP-400M", "google/siglip-so400m-patch14-384", "siglip", v, t, 1152,
+                     ImageProcConfig(384, "square", IMAGENET_STANDARD_MEAN, IMAGENET_STANDARD_STD))
+
+
+def _clip(name, hub, v_hidden, v_inter, v_layers, image_size, v_act, t_hidden, t_inter, t_layers, t_heads, t_act,
+          proj, pool="eos") -> ModelSpec:
+    v = VisionConfig(hidden=v_hidden, intermediate=v_inter, layers=v_layers, heads=16, act=v_act, eps=1e-5,
+                     image_size=image_size, patch=14)
+    t = TextConfig(hidden=t_hidden, intermediate=t_inter, layers=t_layers, heads=t_heads, act=t_act, eps=1e-5,
+                   pool=pool)
+    return ModelSpec(name, hub, "clip", v, t, proj,
+                     ImageProcConfig(image_size, "shortest_edge", OPENAI_CLIP_MEAN, OPENAI_CLIP_STD))
+
+
+REGISTRY: Dict[str, ModelSpec] = {
+    "SigLIP-400M": _siglip_400m(),
+    # openai config.json keeps the legacy text eos_token_id == 2 -> argmax pooling (TF:…clip.py:561-570)
+    "OpenAI-CLIP-L": _clip("OpenAI-CLIP-L", "openai/clip-vit-large-patch14-336", 1024, 4096, 24, 336, "quick_gelu",
+                           768, 3072, 12, 12, "quick_gelu", 768, pool="argmax"),
+    "LAION-CLIP-H": _clip("LAION-CLIP-H", "laion/CLIP-ViT-H-14-laion2B-s32B-b79K", 1280, 5120, 32, 224, "gelu",
+                          1024, 4096, 24, 16, "gelu", 1024),
+    "MetaCLIP-H14": _clip("MetaCLIP-H14", "facebook/metaclip-h14-fullcc2.5b", 1280, 5120, 32, 224, "quick_gelu",
+                          1024, 4096, 24, 16, "quick_gelu", 1024),
+    "Apple-DFN5B-H": _clip("Apple-DFN5B-H", "apple/DFN5B-CLIP-ViT-H-14-378", 1280, 5120, 32, 378, "quick_gelu",
+                           1024, 4096, 24, 16, "quick_gelu", 1024),
+}
+
+# Small configurations with the same code paths (head dims 72 / 80 / 64, ragged
+# token counts, padded intermediate widths) for parity tests.
+TINY: Dict[str, ModelSpec] = {
+    "tiny-siglip": ModelSpec(
+        "tiny-siglip", "-", "siglip",
+        VisionConfig(hidden=576, intermediate=600, layers=2, heads=8, act="gelu_pytorch_tanh", eps=1e-6,
+                     image_size=98, patch=14),
+        TextConfig(hidden=576, intermediate=600, layers=2, heads=8, act="gelu_pytorch_tanh", eps=1e-6, vocab=1000,
+                   max_pos=16, eos_id=1, bos_id=None, pad_id=1, pool="last", causal=False),
+        576, ImageProcConfig(98, "square", IMAGENET_STANDARD_MEAN, IMAGENET_STANDARD_STD), batch_size=4),
+    "tiny-clip": ModelSpec(
+        "tiny-clip", "-", "clip",
+        VisionConfig(hidden=320, intermediate=640, layers=2, heads=4, act="quick_gelu", eps=1e-5, image_size=56,
+                     patch=14),
+        TextConfig(hidden=256, intermediate=512, layers=2, heads=4, act="gelu", eps=1e-5, vocab=1000, max_pos=20,
+                   eos_id=999, bos_id=998, pad_id=999, pool="eos", causal=True),
+        256, ImageProcConfig(56, "shortest_edge", OPENAI_CLIP_MEAN, OPENAI_CLIP_STD), batch_size=4),
+}
+
+
+def get_spec(name: str) -> ModelSpec:
+    if name in REGISTRY:
+        return REGISTRY[name]
+    if name in TINY:
+        return TINY[name]
+    raise KeyError(f"unknown model {name!r}; known: {sorted(REGISTRY) + sorted(TINY)}")
+
+
+def image_flops(spec: ModelSpec) -> float:
+    """Algorithmic FLOPs of one image through the vision tower (GEMMs + attention, 2*M*N*K)."""
+    v = spec.vision
+    P = v.num_patches
+    T = P + (1 if spec.family == "clip" else 0)
+    d, I = v.hidden, v.intermediate
+    f = 2.0 * P * (3 * v.patch * v.patch) * d
+    f += v.layers * (2.0 * T * d * (3 * d + d + 2 * I) + 4.0 * T * T * d)
+    if spec.family == "siglip":  # MAP head: kv proj over T tokens + tiny per-image tail
+        f += 2.0 * T * d * 2 * d + 4.0 * T * d + 2.0 * d * (d + 2 * I)
+    else:
+        f += 2.0 * d * spec.proj_dim
+    return f
+
+
+def text_flops(spec: ModelSpec, L: int) -> float:
+    t = spec.text
+    d, I = t.hidden, t.intermediate
+    f = t.layers * (2.0 * L * d * (3 * d + d + 2 * I) + 4.0 * L * L * d)
+    f += 2.0 * d * spec.proj_dim
+    return f

@@ -1,0 +1,102 @@
+"""Multi-GPU sharding of the encode + retrieval job (one process per GPU).
+
+The reference is single-process (main.py:92); this is build-only scope
+(SURVEY.md §8e). Partitioning: rank r owns images [lo, hi), their caption-0
+T2I queries and captions [5·lo, 5·hi) — caption ownership follows image
+ownership, so encoding needs no communication at all. Exchange, once per job:
+  * all-gather of the text embeddings (T2I and all captions) and of the image
+    embeddings (bf16, 69 MB + 11.5 MB at SigLIP D = 1152) over RCCL/xGMI;
+  * every rank then ranks ITS rows against the full tables (T2I: its caption-0
+    rows vs all images; I2T / I2T-Sym: its images vs all captions) — no
+    cross-rank top-k merge is needed;
+  * one all-reduce(SUM) of the 9 int64 hit counters.
+The compute callbacks are injectable so the orchestration is testable on the
+CPU with gloo (tests/test_distributed.py).
+"""
+from __future__ import annotations
+
+from typing import Callable, Dict, Optional, Sequence, Tuple
+
+import torch
+import torch.distributed as dist
+
+KS = (1, 5, 10)
+
+
+def shard_range(n: int, rank: int, world: int) -> Tuple[int, int]:
+    """Contiguous balanced split of n items (first n % world ranks get one more)."""
+    q, r = divmod(n, world)
+    lo = rank * q + min(rank, r)
+    return lo, lo + q + (1 if rank < r else 0)
+
+
+def all_gather_rows(x: torch.Tensor, world: int, group=None) -> torch.Tensor:
+    """Concatenate every rank's [n_r, D] rows in rank order (ragged n_r allowed)."""
+    if world == 1:
+        return x
+    n = torch.tensor([x.shape[0]], dtype=torch.int64, device=x.device)
+    sizes = [torch.zeros_like(n) for _ in range(world)]
+    dist.all_gather(sizes, n, group=group)
+    sizes = [int(s.item()) for s in sizes]
+    mx = max(sizes)
+    xp = x if x.shape[0] == mx else torch.cat([x, x.new_zeros(mx - x.shape[0], *x.shape[1:])])
+    xp = xp.contiguous()
+    if x.is_cuda:
+        out = x.new_empty(world * mx, *x.shape[1:])
+        dist.all_gather_into_tensor(out, xp, group=group)
+        parts = out.split(mx)
+    else:
+        parts = [torch.empty_like(xp) for _ in range(world)]
+        dist.all_gather(parts, xp, group=group)
+    return torch.cat([p[:s] for p, s in zip(parts, sizes)])
+
+
+class DeviceOps:
+    """Default compute: libmme fused sim/top-k + recall counters."""
+
+    def topk(self, q: torch.Tensor, d: torch.Tensor, k: int) -> torch.Tensor:
+        from . import ops
+        return ops.sim_topk(q.contiguous(), d.contiguous(), k)[0]
+
+    def hits(self, idx: torch.Tensor, tgt_count: int, ks: Sequence[int], row_offset: int) -> torch.Tensor:
+        from . import ops
+        return ops.recall_hits(idx, tgt_count, ks, row_offset=row_offset)
+
+
+def sharded_recall(img_l: torch.Tensor, t2i_l: torch.Tensor, all_l: torch.Tensor, rank: int, world: int,
+                   n_img: int, caps_per_image: int = 5, ks: Sequence[int] = KS, group=None,
+                   compute: Optional[object] = None) -> Dict[str, float]:
+    """Global R@k from per-rank shards (see module docstring)."""
+    compute = compute or DeviceOps()
+    lo, _ = shard_range(n_img, rank, world)
+    img_all = all_gather_rows(img_l, world, group)
+    t2i_all = all_gather_rows(t2i_l, world, group)
+    all_all = all_gather_rows(all_l, world, group)
+    kmax = max(ks)
+    res = []
+    for name, q, d, tcount in (("T2I", t2i_l, img_all, 1), ("I2T", img_l, all_all, caps_per_image),
+                               ("I2T_Sym", img_l, t2i_all, 1)):
+        k = min(kmax, d.shape[0])
+        kk = [min(x, k) for x in ks]
+        if q.shape[0]:
+            idx = compute.topk(q, d, k)
+            h = compute.hits(idx, tcount, kk, lo)
+        else:
+            h = torch.zeros(len(ks), dtype=torch.int64, device=q.device)
+        res.append(h.to(torch.int64))
+    counts = torch.cat(res)
+    if world > 1:
+        dist.all_reduce(counts, op=dist.ReduceOp.SUM, group=group)
+    c = counts.tolist()
+    out = {}
+    for j, name in enumerate(("T2I", "I2T", "I2T_Sym")):
+        denom = n_img
+        for i, k in enumerate(ks):
+            out[f"{name}_R@{k}"] = 100.0 * c[j * len(ks) + i] / denom
+    return out
+
+
+def env_rank_world() -> Tuple[int, int, int]:
+    """(rank, world_size, local_rank) from torchrun's environment (defaults 0/1/0)."""
+    import os
+    return int(os.environ.get("RANK", 0)), int(os.environ.get("WORLD_SIZE", 1)), int(os.environ.get("LOCAL_RANK", 0))

@@ -1,0 +1,284 @@
+"""Dual-encoder models behind the reference's HF duck type.
+
+``SiglipModel`` / ``CLIPModel`` expose exactly what main.py consumes:
+  * get_image_features(pixel_values=[B,3,S,S]) -> Tensor[B, D]   (main.py:408-409)
+  * get_text_features(input_ids=[B,L], attention_mask=None) -> Tensor[B, D] (main.py:428-429)
+  * eval() / to() returning self (main.py:812-819)
+returning plain tensors (transformers-4 semantics), plus the
+fast device paths encode_images(u8 images) / encode_texts(ids) and score().
+
+Every arithmetic step runs in libmme (mme.ops); this module only sequences
+kernels and sizes buffers. The tower structure follows
+TF:models/siglip/modeling_siglip.py:325-357,553-644 and
+TF:models/clip/modeling_clip.py:494-656.
+"""
+from __future__ import annotations
+
+from typing import List, Optional, Sequence, Tuple
+
+import torch
+
+from . import ops
+from .config import ACTS, ModelSpec, TowerConfig, get_spec
+from .weights import LayerW, ModelW, TextW, VisionW, from_hf_state_dict, random_state_dict
+
+BF16 = torch.bfloat16
+
+
+class _Bufs:
+    """Per-forward activation buffers: x (residual stream), h (LN / attention
+    output) and one wide buffer shared by QKV and the MLP hidden."""
+
+    def __init__(self, rows: int, cfg: TowerConfig, device):
+        d = cfg.hidden
+        wide = max(3 * d, cfg.inter_pad)
+        self.h = torch.empty(rows, d, dtype=BF16, device=device)
+        self.wide = torch.empty(rows, wide, dtype=BF16, device=device)
+
+
+def encoder_layer(x: torch.Tensor, L: LayerW, cfg: TowerConfig, B: int, T: int, bufs: _Bufs, *,
+                  seq_lens: Optional[torch.Tensor] = None, causal: bool = False) -> None:
+    """Pre-LN transformer block, in place on x (SiglipEncoderLayer.forward, TF:…siglip.py:341-357)."""
+    d, H, hd = cfg.hidden, cfg.heads, cfg.head_dim
+    act = ACTS[cfg.act]
+    h = ops.layernorm(x, L.ln1_g, L.ln1_b, cfg.eps, out=bufs.h)
+    qkv = ops.gemm(h, L.qkv_w, L.qkv_b, out=bufs.wide[:, : 3 * d])
+    a = ops.attention(qkv, B, T, H, hd, seq_lens=seq_lens, causal=causal, out=bufs.h)
+    ops.gemm(a, L.o_w, L.o_b, residual=x, out=x)
+    h = ops.layernorm(x, L.ln2_g, L.ln2_b, cfg.eps, out=bufs.h)
+    mlp_flops = 2.0 * x.shape[0] * d * cfg.intermediate  # unpadded intermediate width
+    mid = ops.gemm(h, L.fc1_w, L.fc1_b, act=act, out=bufs.wide[:, : cfg.inter_pad], algo_flops=mlp_flops)
+    ops.gemm(mid, L.fc2_w, L.fc2_b, residual=x, out=x, algo_flops=mlp_flops)
+
+
+class VisionTower:
+    def __init__(self, spec: ModelSpec, w: VisionW):
+        self.spec, self.cfg, self.w = spec, spec.vision, w
+
+    def forward_patches(self, patches: torch.Tensor, B: int) -> torch.Tensor:
+        """patches: bf16 [B*P, kpad] im2col image -> pooled features [B, D] (bf16)."""
+        cfg, w = self.cfg, self.w
+        P, d = cfg.num_patches, cfg.hidden
+        dev = patches.device
+        if self.spec.family == "siglip":
+            T = P
+            x = ops.gemm(patches, w.patch_w, w.patch_b, residual=w.pos, res_period=P,  # conv + bias + pos
+                         algo_flops=2.0 * B * P * d * 3 * cfg.patch ** 2)
+        else:
+            T = P + 1
+            pe = ops.gemm(patches, w.patch_w, algo_flops=2.0 * B * P * d * 3 * cfg.patch ** 2)
+            x = ops.clip_embed_ln(pe, w.cls, w.pos, w.pre_ln_g, w.pre_ln_b, cfg.eps, B, P)
+            del pe
+        bufs = _Bufs(B * T, cfg, dev)
+        for L in w.layers:
+            encoder_layer(x, L, cfg, B, T, bufs)
+        if self.spec.family == "siglip":
+            return self._map_head(x, B, T, bufs)
+        rows = torch.arange(B, device=dev, dtype=torch.int32) * T  # CLS rows
+        pooled = ops.layernorm(x, w.post_ln_g, w.post_ln_b, cfg.eps, rows_idx=rows)
+        return ops.gemm(pooled, w.proj_w)
+
+    def _map_head(self, x, B, T, bufs) -> torch.Tensor:
+        """post_layernorm + SiglipMultiheadAttentionPoolingHead (TF:…siglip.py:611-644)."""
+        cfg, w, hw = self.cfg, self.w, self.w.head
+        d = cfg.hidden
+        h = ops.layernorm(x, w.post_ln_g, w.post_ln_b, cfg.eps, out=bufs.h)
+        kv = ops.gemm(h, hw.kv_w, hw.kv_b, out=bufs.wide[:, : 2 * d])
+        a = ops.probe_attention(hw.q, kv, B, T, cfg.heads, cfg.head_dim)
+        y = ops.gemm(a, hw.out_w, hw.out_b)
+        z = ops.layernorm(y, hw.ln_g, hw.ln_b, cfg.eps)
+        m = ops.gemm(z, hw.fc1_w, hw.fc1_b, act=ACTS[cfg.act])
+        return ops.gemm(m, hw.fc2_w, hw.fc2_b, residual=y)
+
+
+class TextTower:
+    def __init__(self, spec: ModelSpec, w: TextW):
+        self.spec, self.cfg, self.w = spec, spec.text, w
+
+    def forward_ids(self, ids: torch.Tensor, seq_lens: Optional[torch.Tensor]) -> torch.Tensor:
+        """ids: int64 [B, L] on device -> pooled features [B, D] (bf16)."""
+        cfg, w = self.cfg, self.w
+        B, L = ids.shape
+        x = ops.token_embed(ids, w.tok, w.pos)
+        bufs = _Bufs(B * L, cfg, ids.device)
+        for layer in w.layers:
+            encoder_layer(x, layer, cfg, B, L, bufs, seq_lens=seq_lens, causal=cfg.causal)
+        mode = {"eos": 0, "argmax": 1, "last": 2}[cfg.pool]
+        rows = ops.text_pool_rows(ids, cfg.eos_id, mode)
+        pooled = ops.layernorm(x, w.final_ln_g, w.final_ln_b, cfg.eps, rows_idx=rows)
+        return ops.gemm(pooled, w.head_w, w.head_b)
+
+
+def plan_text_batches(n: int, Lmax: int, lens: Optional[List[int]], ref_batch: int, exec_batch: int):
+    """Execution plan reproducing processor(padding=True) per reference batch.
+
+    The reference pads each batch of `ref_batch` captions (main.py:420-427) to
+    its longest caption, and SigLIP pools position L_b - 1 of that padded
+    batch, so a caption's embedding depends on its batch's padded length L_b.
+    Captions are therefore grouped by L_b (caption order preserved) and each
+    group is cut into execution batches of <= exec_batch rows.
+    Yields (L_b, rows) with rows a range (contiguous) or a list of indices.
+    """
+    if lens is None:
+        for s in range(0, n, exec_batch):
+            yield Lmax, range(s, min(n, s + exec_batch))
+        return
+    groups = {}
+    for s in range(0, n, ref_batch):
+        e = min(n, s + ref_batch)
+        groups.setdefault(max(lens[s:e]), []).extend(range(s, e))
+    for Lb, rows in groups.items():
+        for j in range(0, len(rows), exec_batch):
+            part = rows[j:j + exec_batch]
+            yield Lb, (range(part[0], part[-1] + 1) if part[-1] - part[0] + 1 == len(part) else part)
+
+
+def _seq_lens(attention_mask: Optional[torch.Tensor], B: int, L: int, device) -> Optional[torch.Tensor]:
+    """Right-padded attention_mask -> int32 valid lengths (None if no padding)."""
+    if attention_mask is None:
+        return None
+    m = attention_mask.to(device=device)
+    lens = m.sum(dim=1).to(torch.int32)
+    # the kernels mask keys >= len: require the mask to be a prefix mask
+    ar = torch.arange(L, device=device).unsqueeze(0)
+    if not torch.equal(m.bool(), ar < lens.unsqueeze(1)):
+        raise ValueError("attention_mask must be right-padded (a prefix of ones per row)")
+    if int(lens.min()) == L:
+        return None
+    return lens
+
+
+class DualEncoder:
+    """Shared implementation of the SigLIP / CLIP duck type."""
+
+    family = "?"
+
+    def __init__(self, spec: ModelSpec, weights: ModelW, device="cuda"):
+        self.spec = spec
+        self.config = spec
+        self.device = torch.device(device)
+        self.weights = weights
+        self.vision = VisionTower(spec, weights.vision)
+        self.text = TextTower(spec, weights.text)
+        self.dtype = BF16
+
+    # ---- construction
+    @classmethod
+    def from_spec(cls, spec, seed: int = 0, device="cuda", state_dict=None) -> "DualEncoder":
+        spec = get_spec(spec) if isinstance(spec, str) else spec
+        sd = state_dict if state_dict is not None else random_state_dict(spec, seed, device)
+        return cls(spec, from_hf_state_dict(spec, sd, device), device)
+
+    # ---- HF-style surface
+    def eval(self):
+        return self
+
+    def to(self, *args, **kwargs):
+        return self
+
+    @torch.no_grad()
+    def get_image_features(self, pixel_values: torch.Tensor, **_) -> torch.Tensor:
+        """pixel_values [B,3,S,S] (fp32 or bf16) -> pooled image features [B, D] bf16."""
+        v = self.spec.vision
+        if pixel_values.shape[-1] != v.image_size:
+            raise ValueError(f"pixel_values size {tuple(pixel_values.shape)} != model image size {v.image_size}")
+        pv = pixel_values.to(self.device)
+        B = pv.shape[0]
+        patches = ops.im2col(pv, v.patch, v.kpad)
+        return self.vision.forward_patches(patches, B)
+
+    @torch.no_grad()
+    def get_text_features(self, input_ids: torch.Tensor, attention_mask: Optional[torch.Tensor] = None,
+                          **_) -> torch.Tensor:
+        ids = input_ids.to(self.device, dtype=torch.int64)
+        B, L = ids.shape
+        return self.text.forward_ids(ids, _seq_lens(attention_mask, B, L, self.device))
+
+    def __call__(self, *args, **kwargs):
+        raise TypeError("use get_image_features / get_text_features (main.py:408-431)")
+
+    # ---- fast device paths (u8 images / token ids resident in HBM)
+    @torch.no_grad()
+    def encode_images(self, images_u8: torch.Tensor, batch: int = 256, out: Optional[torch.Tensor] = None
+                      ) -> torch.Tensor:
+        """u8 [n,H,W,3] device images -> L2-normalised bf16 embeddings [n, D].
+
+        Fuses the processor (PIL-exact bicubic + normalise) into an im2col
+        kernel feeding the patch GEMM. Batch size does not change results
+        (images never interact)."""
+        from .processor import image_geometry
+        v, ip = self.spec.vision, self.spec.image_proc
+        n, H, W, _ = images_u8.shape
+        rh, rw, top, left = image_geometry(H, W, ip)
+        if out is None:
+            out = torch.empty(n, self.spec.proj_dim, dtype=BF16, device=self.device)
+        for i in range(0, n, batch):
+            chunk = images_u8[i:i + batch]
+            b = chunk.shape[0]
+            patches = ops.preprocess_u8(chunk, resize=(rh, rw), crop=(top, left), size=ip.size, mean=ip.mean,
+                                        std=ip.std, patch=v.patch, kpad=v.kpad)
+            feats = self.vision.forward_patches(patches, b)
+            ops.l2norm(feats, out=out[i:i + b])
+        return out
+
+    @torch.no_grad()
+    def encode_texts(self, ids: torch.Tensor, lens: Optional[torch.Tensor] = None, ref_batch: Optional[int] = None,
+                     exec_batch: int = 1024, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """Token ids -> L2-normalised bf16 embeddings, reproducing the reference's
+        batch-padding semantics exactly: each reference batch of `ref_batch`
+        captions (main.py:420) is padded to its own longest caption (processor
+        padding=True); reference batches with equal padded length are fused into
+        one execution batch of up to `exec_batch` rows.
+
+        ids: int64 [n, Lmax] (right-padded, on device), lens: int [n] (None = all Lmax).
+        """
+        ref_batch = ref_batch or self.spec.batch_size
+        n, Lmax = ids.shape
+        if out is None:
+            out = torch.empty(n, self.spec.proj_dim, dtype=BF16, device=self.device)
+        if n == 0:
+            return out
+        lens_h = None if lens is None else lens.to("cpu", torch.int64).tolist()
+        lens_d = None if lens is None else lens.to(self.device, torch.int32)
+        for Lb, rows in plan_text_batches(n, Lmax, lens_h, ref_batch, exec_batch):
+            if isinstance(rows, range):  # contiguous run: slice, no gather
+                sel = slice(rows.start, rows.stop)
+                bids, dst = ids[sel, :Lb], out[sel]
+                sl = None if lens_d is None else lens_d[sel]
+            else:
+                r = torch.tensor(rows, device=self.device)
+                bids, dst = ids.index_select(0, r)[:, :Lb], None
+                sl = lens_d.index_select(0, r)
+            if sl is not None and all(lens_h[i] == Lb for i in rows):
+                sl = None
+            feats = self.text.forward_ids(bids.contiguous(), sl)
+            if dst is not None:
+                ops.l2norm(feats, out=dst)
+            else:
+                out.index_copy_(0, r, ops.l2norm(feats))
+        return out
+
+    def score(self, query_emb: torch.Tensor, doc_emb: torch.Tensor) -> torch.Tensor:
+        """Cosine score matrix fp32 [nq, nd] (compute_similarity_scores, main.py:473)."""
+        return ops.gemm(query_emb, doc_emb, out_f32=True)
+
+
+class SiglipModel(DualEncoder):
+    family = "siglip"
+
+
+class CLIPModel(DualEncoder):
+    family = "clip"
+
+
+def load_model(name: str, seed: int = 0, device="cuda", state_dict=None, batch_size: Optional[int] = None
+               ) -> Tuple[DualEncoder, "object"]:
+    """(model, processor) for a registry name — the offline counterpart of
+    from_pretrained(m_info['id']) (main.py:808-820)."""
+    from .processor import Processor
+    spec = get_spec(name)
+    if batch_size is not None:
+        spec = spec.with_batch_size(batch_size)
+    cls = SiglipModel if spec.family == "siglip" else CLIPModel
+    model = cls.from_spec(spec, seed=seed, device=device, state_dict=state_dict)
+    return model, Processor(spec, device=device)

@@ -1,0 +1,341 @@
+"""Tensor-level wrappers over the libmme C ABI.
+
+PyTorch is plumbing here: it owns device memory and streams. Every function
+checks shapes / dtypes / devices on the host, then hands raw device pointers
+and the current HIP stream to libmme. Nothing in this module computes on the
+host or falls back to torch ops: a missing library or a CPU tensor raises.
+"""
+from __future__ import annotations
+
+import math
+from typing import Optional, Sequence
+
+import torch
+
+from . import _lib
+from ._lib import call, query
+
+BF16 = torch.bfloat16
+
+
+def _stream() -> int:
+    return torch.cuda.current_stream().cuda_stream
+
+
+def _ptr(t: Optional[torch.Tensor]) -> Optional[int]:
+    return None if t is None else t.data_ptr()
+
+
+def _dev(*ts: Optional[torch.Tensor]) -> None:
+    for t in ts:
+        if t is not None and not t.is_cuda:
+            raise ValueError("mme ops take device tensors (got a CPU tensor); there is no host fallback")
+
+
+def _rowmajor(t: torch.Tensor, name: str) -> int:
+    """Return the leading dimension of a 2-D tensor with unit column stride."""
+    if t.dim() != 2 or t.stride(1) != 1:
+        raise ValueError(f"{name}: expected a 2-D tensor with contiguous rows, got shape {tuple(t.shape)} "
+                         f"stride {t.stride()}")
+    return t.stride(0)
+
+
+class Workspace:
+    """Grow-only device scratch buffer (one per stream/user)."""
+
+    def __init__(self) -> None:
+        self.buf: Optional[torch.Tensor] = None
+
+    def get(self, nbytes: int, device) -> torch.Tensor:
+        nbytes = max(256, int(nbytes))
+        if self.buf is None or self.buf.numel() < nbytes or self.buf.device != torch.device(device):
+            self.buf = torch.empty(nbytes, dtype=torch.uint8, device=device)
+        return self.buf
+
+
+_ws = Workspace()
+
+
+class KernelTimer:
+    """Optional HIP-event timing of libmme launches (bench.py's roofline).
+
+    When enabled, each timed op records a start/end event pair on the stream it
+    launches on and the op's algorithmic FLOPs; summary() syncs once and
+    aggregates. Disabled (the default) it costs one attribute check."""
+
+    enabled = False
+    records = []
+
+    @classmethod
+    def start(cls):
+        cls.records = []
+        cls.enabled = True
+
+    @classmethod
+    def stop(cls):
+        cls.enabled = False
+
+    @classmethod
+    def begin(cls):
+        if not cls.enabled:
+            return None
+        ev = torch.cuda.Event(enable_timing=True)
+        ev.record()
+        return ev
+
+    @classmethod
+    def end(cls, ev, name: str, flops: float, nbytes: float = 0.0):
+        if ev is None:
+            return
+        e = torch.cuda.Event(enable_timing=True)
+        e.record()
+        cls.records.append((name, ev, e, flops, nbytes))
+
+    @classmethod
+    def summary(cls):
+        torch.cuda.synchronize()
+        out = {}
+        for name, s, e, fl, nb in cls.records:
+            d = out.setdefault(name, {"launches": 0, "ms": 0.0, "flops": 0.0, "bytes": 0.0})
+            d["launches"] += 1
+            d["ms"] += s.elapsed_time(e)
+            d["flops"] += fl
+            d["bytes"] += nb
+        return out
+
+
+# ---------------------------------------------------------------- GEMM / norms
+def gemm(a: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None, *,
+         residual: Optional[torch.Tensor] = None, res_period: int = 0, act: int = _lib.ACT_NONE,
+         out: Optional[torch.Tensor] = None, out_f32: bool = False,
+         algo_flops: Optional[float] = None) -> torch.Tensor:
+    """out = act(a @ w.T + bias) + residual[row % res_period or row]  (bf16, fp32 accumulate).
+
+    a: [M, K] bf16, w: [N, K] bf16 (nn.Linear layout), K % 64 == 0.
+    algo_flops: the algorithmic FLOPs of this product when the operands carry
+    zero padding (KernelTimer accounting only; default 2*M*N*K).
+    """
+    _dev(a, w, bias, residual, out)
+    M, K = a.shape
+    N = w.shape[0]
+    if w.shape[1] != K:
+        raise ValueError(f"gemm: a is [*, {K}] but w is {tuple(w.shape)}")
+    if out is None:
+        out = torch.empty(M, N, dtype=torch.float32 if out_f32 else BF16, device=a.device)
+    lda, ldb, ldc = _rowmajor(a, "a"), _rowmajor(w, "w"), _rowmajor(out, "out")
+    ldr = 0
+    if residual is not None:
+        ldr = _rowmajor(residual, "residual")
+    if bias is not None and bias.numel() < N:
+        raise ValueError("gemm: bias shorter than N")
+    ev = KernelTimer.begin()
+    call("mme_gemm", a.data_ptr(), lda, w.data_ptr(), ldb, out.data_ptr(), ldc, M, N, K, _ptr(bias),
+         _ptr(residual), ldr, res_period, act, int(out_f32), _stream())
+    KernelTimer.end(ev, "gemm", algo_flops if algo_flops is not None else 2.0 * M * N * K, 2.0 * (M * K + N * K + M * N))
+    return out
+
+
+def layernorm(x: torch.Tensor, gamma: torch.Tensor, beta: torch.Tensor, eps: float, *,
+              rows_idx: Optional[torch.Tensor] = None, out: Optional[torch.Tensor] = None,
+              d: Optional[int] = None) -> torch.Tensor:
+    """LayerNorm over the first `d` columns of each row (optionally of rows x[rows_idx])."""
+    _dev(x, gamma, beta, rows_idx, out)
+    d = d or gamma.numel()
+    rows = rows_idx.numel() if rows_idx is not None else x.shape[0]
+    if out is None:
+        out = torch.empty(rows, d, dtype=BF16, device=x.device)
+    if rows_idx is not None and rows_idx.dtype != torch.int32:
+        raise ValueError("layernorm: rows_idx must be int32")
+    call("mme_layernorm", x.data_ptr(), _rowmajor(x, "x"), gamma.data_ptr(), beta.data_ptr(), out.data_ptr(),
+         _rowmajor(out, "out"), rows, d, float(eps), _ptr(rows_idx), _stream())
+    return out
+
+
+def l2norm(x: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """bf16(x / bf16(||x||)) per row — main.py:414,434 semantics."""
+    _dev(x, out)
+    rows, d = x.shape
+    if out is None:
+        out = torch.empty(rows, d, dtype=BF16, device=x.device)
+    call("mme_l2norm", x.data_ptr(), _rowmajor(x, "x"), out.data_ptr(), _rowmajor(out, "out"), rows, d, _stream())
+    return out
+
+
+# ---------------------------------------------------------------- attention
+def attention(qkv: torch.Tensor, B: int, T: int, H: int, hd: int, *, seq_lens: Optional[torch.Tensor] = None,
+              causal: bool = False, scale: Optional[float] = None, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    _dev(qkv, seq_lens, out)
+    if qkv.shape[0] != B * T:
+        raise ValueError(f"attention: qkv has {qkv.shape[0]} rows, expected B*T={B * T}")
+    if out is None:
+        out = torch.empty(B * T, H * hd, dtype=BF16, device=qkv.device)
+    if seq_lens is not None and (seq_lens.dtype != torch.int32 or seq_lens.numel() != B):
+        raise ValueError("attention: seq_lens must be int32 [B]")
+    scale = hd ** -0.5 if scale is None else scale
+    ev = KernelTimer.begin()
+    call("mme_attention", qkv.data_ptr(), _rowmajor(qkv, "qkv"), out.data_ptr(), _rowmajor(out, "out"), B, T, H, hd,
+         _ptr(seq_lens), int(causal), float(scale), _stream())
+    KernelTimer.end(ev, "attention", 4.0 * B * H * T * T * hd * (0.5 if causal else 1.0))
+    return out
+
+
+def probe_attention(q: torch.Tensor, kv: torch.Tensor, B: int, T: int, H: int, hd: int, *,
+                    scale: Optional[float] = None, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    _dev(q, kv, out)
+    if out is None:
+        out = torch.empty(B, H * hd, dtype=BF16, device=kv.device)
+    scale = hd ** -0.5 if scale is None else scale
+    call("mme_probe_attention", q.data_ptr(), kv.data_ptr(), _rowmajor(kv, "kv"), out.data_ptr(),
+         _rowmajor(out, "out"), B, T, H, hd, float(scale), _stream())
+    return out
+
+
+# ---------------------------------------------------------------- embeddings
+def token_embed(ids: torch.Tensor, tok: torch.Tensor, pos: torch.Tensor, out: Optional[torch.Tensor] = None):
+    _dev(ids, tok, pos, out)
+    if ids.dtype != torch.int64 or ids.dim() != 2:
+        raise ValueError("token_embed: ids must be int64 [B, L]")
+    B, L = ids.shape
+    d = tok.shape[1]
+    if L > pos.shape[0]:
+        raise ValueError(f"token_embed: sequence length {L} exceeds max_position_embeddings {pos.shape[0]}")
+    ids = ids.contiguous()
+    if out is None:
+        out = torch.empty(B * L, d, dtype=BF16, device=ids.device)
+    call("mme_token_embed", ids.data_ptr(), B, L, tok.data_ptr(), pos.data_ptr(), d, out.data_ptr(),
+         _rowmajor(out, "out"), _stream())
+    return out
+
+
+def clip_embed_ln(patch: torch.Tensor, cls: torch.Tensor, pos: torch.Tensor, gamma, beta, eps: float, B: int, P: int,
+                  out: Optional[torch.Tensor] = None):
+    _dev(patch, cls, pos, gamma, beta, out)
+    d = cls.numel()
+    if out is None:
+        out = torch.empty(B * (P + 1), d, dtype=BF16, device=patch.device)
+    call("mme_clip_embed_ln", patch.data_ptr(), _rowmajor(patch, "patch"), cls.data_ptr(), pos.data_ptr(),
+         gamma.data_ptr(), beta.data_ptr(), float(eps), out.data_ptr(), _rowmajor(out, "out"), B, P, d, _stream())
+    return out
+
+
+def text_pool_rows(ids: torch.Tensor, eos_id: int, mode: int) -> torch.Tensor:
+    """Row index (b*L + pos) of the pooled token per sequence (mode 0 eos, 1 argmax, 2 last)."""
+    _dev(ids)
+    B, L = ids.shape
+    ids = ids.contiguous()
+    rows = torch.empty(B, dtype=torch.int32, device=ids.device)
+    call("mme_text_pool_rows", ids.data_ptr(), B, L, int(eos_id), int(mode), rows.data_ptr(), _stream())
+    return rows
+
+
+# ---------------------------------------------------------------- image preprocessing
+def preprocess_u8(imgs: torch.Tensor, *, resize: Sequence[int], crop: Sequence[int], size: int,
+                  mean: Sequence[float], std: Sequence[float], patch: int = 0, kpad: int = 0) -> torch.Tensor:
+    """PIL-exact bicubic resize + crop + rescale + normalise of u8 NHWC images on the device.
+
+    patch == 0 -> pixel_values fp32 [n,3,S,S]; patch > 0 -> bf16 im2col patches [n*(S/p)^2, kpad].
+    """
+    _dev(imgs)
+    if imgs.dtype != torch.uint8 or imgs.dim() != 4 or imgs.shape[3] != 3:
+        raise ValueError("preprocess_u8: expected uint8 [n, H, W, 3]")
+    imgs = imgs.contiguous()
+    n, H, W, _ = imgs.shape
+    rh, rw = resize
+    top, left = crop
+    S = size
+    dev = imgs.device
+    wsb = query("mme_preprocess_workspace_bytes", n, H, W, rh, rw)
+    ws = torch.empty(wsb, dtype=torch.uint8, device=dev)
+    if patch:
+        G = S // patch
+        out = torch.empty(n * G * G, kpad, dtype=BF16, device=dev)
+        kind = _lib.PIX_PATCHES
+    else:
+        out = torch.empty(n, 3, S, S, dtype=torch.float32, device=dev)
+        kind = _lib.PIX_F32_NCHW
+    # mean/std are HOST float[3] (copied by value into the kernel arguments)
+    mean_h = torch.tensor(list(mean), dtype=torch.float32)
+    std_h = torch.tensor(list(std), dtype=torch.float32)
+    call("mme_preprocess_u8", imgs.data_ptr(), n, H, W, rh, rw, top, left, S, mean_h.data_ptr(), std_h.data_ptr(),
+         kind, patch, kpad, out.data_ptr(), ws.data_ptr(), wsb, _stream())
+    return out
+
+
+def im2col(pixels: torch.Tensor, patch: int, kpad: int) -> torch.Tensor:
+    _dev(pixels)
+    if pixels.dim() != 4 or pixels.shape[1] != 3 or pixels.shape[2] != pixels.shape[3]:
+        raise ValueError("im2col: expected pixel_values [n, 3, S, S]")
+    if pixels.dtype not in (torch.float32, BF16):
+        pixels = pixels.float()
+    pixels = pixels.contiguous()
+    n, _, S, _ = pixels.shape
+    G = S // patch
+    out = torch.empty(n * G * G, kpad, dtype=BF16, device=pixels.device)
+    call("mme_im2col", pixels.data_ptr(), int(pixels.dtype == torch.float32), n, S, patch, kpad, out.data_ptr(),
+         _stream())
+    return out
+
+
+# ---------------------------------------------------------------- retrieval
+def sim_topk(q: torch.Tensor, d: torch.Tensor, k: int, col_offset: int = 0):
+    """Top-k columns of q @ d.T per row: (idx int32 [nq,k], score fp32 [nq,k]), order (score desc, idx asc)."""
+    _dev(q, d)
+    nq, D = q.shape
+    nd = d.shape[0]
+    idx = torch.empty(nq, k, dtype=torch.int32, device=q.device)
+    sc = torch.empty(nq, k, dtype=torch.float32, device=q.device)
+    wsb = query("mme_sim_topk_workspace_bytes", nq, nd, k)
+    ws = _ws.get(wsb, q.device)
+    call("mme_sim_topk", q.data_ptr(), _rowmajor(q, "q"), d.data_ptr(), _rowmajor(d, "d"), nq, nd, D, k, col_offset,
+         idx.data_ptr(), sc.data_ptr(), ws.data_ptr(), ws.numel(), _stream())
+    return idx, sc
+
+
+def topk_merge(idx: torch.Tensor, score: torch.Tensor, parts: int, k: int):
+    """Merge `parts` top-k lists per row: inputs [rows, parts*k]."""
+    _dev(idx, score)
+    rows = idx.shape[0]
+    idx = idx.contiguous()
+    score = score.contiguous()
+    oi = torch.empty(rows, k, dtype=torch.int32, device=idx.device)
+    os_ = torch.empty(rows, k, dtype=torch.float32, device=idx.device)
+    call("mme_topk_merge", idx.data_ptr(), score.data_ptr(), rows, parts, k, oi.data_ptr(), os_.data_ptr(),
+         _stream())
+    return oi, os_
+
+
+def recall_hits(topk_idx: torch.Tensor, tgt_count: int, ks: Sequence[int], *, tgt_start: Optional[torch.Tensor] = None,
+                row_offset: int = 0, hits: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """int64 [len(ks)] counts of rows whose first ks[j] indices contain a target column."""
+    _dev(topk_idx, tgt_start, hits)
+    rows, k = topk_idx.shape
+    kk = torch.tensor(list(ks), dtype=torch.int32, device=topk_idx.device)
+    if hits is None:
+        hits = torch.zeros(len(ks), dtype=torch.int64, device=topk_idx.device)
+    call("mme_recall_hits", topk_idx.contiguous().data_ptr(), rows, k, _ptr(tgt_start), tgt_count, row_offset,
+         kk.data_ptr(), len(ks), hits.data_ptr(), _stream())
+    return hits
+
+
+def maxsim(Q: torch.Tensor, q_lens: torch.Tensor, D: torch.Tensor, d_lens: torch.Tensor,
+           d_zero: Optional[torch.Tensor] = None, max_ws_bytes: int = 4 << 30) -> torch.Tensor:
+    """ColPali MaxSim scores fp32 [nq, nd] from zero-padded Q [nq,Lq,128], D [nd,Ld,128] (Ld % 16 == 0)."""
+    _dev(Q, q_lens, D, d_lens, d_zero)
+    nq, Lq, dim = Q.shape
+    nd, Ld, _ = D.shape
+    Q = Q.contiguous()
+    D = D.contiguous()
+    out = torch.empty(nq, nd, dtype=torch.float32, device=Q.device)
+    per_q = query("mme_maxsim_workspace_bytes", 1, Lq, nd)
+    chunk = max(1, min(nq, max_ws_bytes // max(per_q, 1)))
+    for q0 in range(0, nq, chunk):
+        q1 = min(nq, q0 + chunk)
+        wsb = query("mme_maxsim_workspace_bytes", q1 - q0, Lq, nd)
+        ws = _ws.get(wsb, Q.device)
+        call("mme_maxsim", Q[q0:q1].data_ptr(), q_lens[q0:q1].data_ptr(), q1 - q0, Lq, D.data_ptr(), d_lens.data_ptr(),
+             _ptr(d_zero), nd, Ld, dim, out[q0:q1].data_ptr(), ws.data_ptr(), ws.numel(), _stream())
+    return out
+
+
+def round_up(x: int, m: int) -> int:
+    return int(math.ceil(x / m) * m)

@@ -1,0 +1,63 @@
+"""Similarity + top-k recall restated in numpy (oracle).
+
+compute_similarity_scores dense branch (main.py:471-473): fp32 matmul of the
+bf16 embeddings; compute_metrics_detailed recall loops (main.py:331-378):
+hit if the target column is among the row's top-k (k = min(k, ncols)),
+R@k = 100 * hits / rows. I2T uses the v28 orientation
+(run_benchmark_grand_slam_v28_publication_ready.py:391). Ties are broken by
+lowest column (the kernel's documented rule; torch.topk's CPU order on exact
+ties is implementation-defined). Pinned by tests/golden/retrieval.npz.
+"""
+from __future__ import annotations
+
+from typing import Dict, Sequence
+
+import numpy as np
+
+KS = (1, 5, 10)
+
+
+def bf16_to_f32(bits: np.ndarray) -> np.ndarray:
+    return (bits.astype(np.uint32) << 16).view(np.float32)
+
+
+def scores(q: np.ndarray, d: np.ndarray) -> np.ndarray:
+    return q.astype(np.float32) @ d.astype(np.float32).T
+
+
+def topk(s: np.ndarray, k: int):
+    """(idx, score) of the k largest per row, ordered (score desc, column asc)."""
+    k = min(k, s.shape[1])
+    cols = np.arange(s.shape[1])
+    order = np.lexsort((np.broadcast_to(cols, s.shape), -s), axis=1)[:, :k]
+    return order.astype(np.int32), np.take_along_axis(s, order, 1)
+
+
+def recall(idx: np.ndarray, tgt_count: int, ks: Sequence[int] = KS, row_offset: int = 0) -> np.ndarray:
+    rows = np.arange(idx.shape[0]) + row_offset
+    lo = rows * tgt_count
+    hit = (idx >= lo[:, None]) & (idx < lo[:, None] + tgt_count)
+    first = np.where(hit.any(1), hit.argmax(1), idx.shape[1])
+    return np.array([(first < min(k, idx.shape[1])).sum() for k in ks], np.int64)
+
+
+def metrics(img: np.ndarray, t2i: np.ndarray, all_txt: np.ndarray, caps: int = 5, ks=KS) -> Dict[str, float]:
+    """The 9 R@k values of compute_metrics_detailed on the identity sample."""
+    n = img.shape[0]
+    out = {}
+    for name, q, d, tc, denom in (("T2I", t2i, img, 1, t2i.shape[0]), ("I2T", img, all_txt, caps, n),
+                                  ("I2T_Sym", img, t2i, 1, n)):
+        idx, _ = topk(scores(q, d), max(ks))
+        h = recall(idx, tc, ks)
+        for j, k in enumerate(ks):
+            out[f"{name}_R@{k}"] = 100.0 * h[j] / denom
+    return out
+
+
+def l2norm_bf16(x_bits: np.ndarray) -> np.ndarray:
+    """bf16 bits -> bf16 bits of x / bf16(||x||) (main.py:414 semantics on a bf16 tensor)."""
+    import torch
+    x = torch.from_numpy(x_bits.view(np.int16)).view(torch.bfloat16)
+    n = torch.sqrt((x.float() ** 2).sum(-1, keepdim=True)).to(torch.bfloat16)
+    y = (x.float() / n.float()).to(torch.bfloat16)
+    return y.view(torch.int16).numpy().view(np.uint16)

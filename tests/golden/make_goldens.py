@@ -1,0 +1,295 @@
+"""Generate the golden parity fixtures from the REFERENCE itself (run here only).
+
+This script imports /root/reference/main.py (read-only, never copied) and
+drives its own hot-path functions — encode_data (main.py:386-438),
+compute_similarity_scores (main.py:440-475), compute_metrics_detailed
+(main.py:305-383) — with in-container transformers models / image processors
+(transformers 5.15.0, PIL 12.2.0) and deterministic inputs. Only the
+resulting input/output arrays are committed (tests/golden/*.npz); the GPU box
+never needs /root/reference.
+
+Shims, none of which edits a reference file:
+  1. main.DEVICE = 'cpu', main.DTYPE = bf16 (or fp32 for the fp32 oracle run);
+  2. a model adapter whose get_*_features return .pooler_output (transformers
+     4 semantics);
+  3. compute_metrics_detailed is called with the un-transposed I2T matrix
+     (the v28 orientation; main.py:622-623's .t() is the KeyError bug §0.1);
+  4. identity sample (no bootstrap resampling, §0.5).
+
+Usage: python tests/golden/make_goldens.py   (writes tests/golden/*.npz)
+"""
+from __future__ import annotations
+
+import os
+import sys
+import tempfile
+
+import numpy as np
+import torch
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(os.path.dirname(HERE))
+REF = "/root/reference"
+sys.path.insert(0, os.path.join(REPO, "multimodal-embedding_amd"))
+sys.path.insert(0, HERE)
+
+from weights_gen import torch_state_dict  # noqa: E402
+from mme.config import TINY, OPENAI_CLIP_MEAN, OPENAI_CLIP_STD  # noqa: E402
+
+
+def import_reference():
+    cwd = os.getcwd()
+    os.chdir(tempfile.mkdtemp(prefix="mme_ref_"))  # main.py writes benchmark_v29.log into the cwd
+    sys.path.insert(0, REF)
+    import main  # noqa: E402
+    os.chdir(cwd)
+    return main
+
+
+def bf16_bits(t: torch.Tensor) -> np.ndarray:
+    return t.to(torch.bfloat16).contiguous().view(torch.int16).numpy().view(np.uint16)
+
+
+# ------------------------------------------------------------------ preprocess
+def make_preprocess():
+    from PIL import Image
+    from transformers.models.siglip.image_processing_pil_siglip import SiglipImageProcessorPil
+    from transformers.models.clip.image_processing_pil_clip import CLIPImageProcessorPil
+
+    rng = np.random.default_rng(0)
+    cases = [  # (name, H, W, processor kind, size)
+        ("siglip384", 224, 224, "siglip", 384),
+        ("clip336", 224, 224, "clip", 336),
+        ("dfn378", 224, 224, "clip", 378),
+        ("clip336_nonsq", 150, 200, "clip", 336),
+        ("vith224_down", 300, 260, "clip", 224),
+    ]
+    out = {}
+    for name, H, W, kind, S in cases:
+        img = rng.integers(0, 256, (H, W, 3), dtype=np.uint8)
+        pil = Image.fromarray(img)
+        if kind == "siglip":
+            proc = SiglipImageProcessorPil(size={"height": S, "width": S})
+            mean, std = (0.5, 0.5, 0.5), (0.5, 0.5, 0.5)
+        else:
+            proc = CLIPImageProcessorPil(size={"shortest_edge": S}, crop_size={"height": S, "width": S})
+            mean, std = OPENAI_CLIP_MEAN, OPENAI_CLIP_STD
+        pv = proc(images=[pil], return_tensors="np")["pixel_values"][0].astype(np.float32)  # [3,S,S]
+        # the resized + cropped u8 raster, recovered exactly: HF computes
+        # float32(float64(u8)/255) then (x - mean)/std in float32; invert by search
+        lut = np.empty((3, 256), np.float32)
+        for c in range(3):
+            r = (np.arange(256, dtype=np.float64) * (1 / 255)).astype(np.float32)
+            lut[c] = (r - np.float32(mean[c])) / np.float32(std[c])
+        u8 = np.empty((S, S, 3), np.uint8)
+        for c in range(3):
+            idx = np.searchsorted(lut[c], pv[c])
+            idx = np.clip(idx, 0, 255)
+            assert np.array_equal(lut[c][idx], pv[c]), f"{name}: pixel_values not on the u8 grid"
+            u8[:, :, c] = idx
+        out[f"{name}_in"] = img
+        out[f"{name}_u8"] = u8
+        out[f"{name}_meta"] = np.array([H, W, S, 0 if kind == "siglip" else 1], np.int64)
+    np.savez_compressed(os.path.join(HERE, "preprocess.npz"), **out)
+    print("preprocess.npz:", {k: v.shape for k, v in out.items()})
+
+
+# ------------------------------------------------------------------ tiny encoders
+class RefAdapter:
+    """get_*_features -> .pooler_output (transformers-4 return type)."""
+
+    def __init__(self, hf):
+        self.hf = hf
+
+    def get_image_features(self, **kw):
+        return self.hf.get_image_features(**kw).pooler_output
+
+    def get_text_features(self, **kw):
+        return self.hf.get_text_features(**kw).pooler_output
+
+
+class RefProcessor:
+    """HF PIL image processor + HF-style padding of pre-tokenized id lists."""
+
+    def __init__(self, image_proc, pad_id):
+        self.ip, self.pad_id = image_proc, pad_id
+
+    def __call__(self, images=None, text=None, return_tensors="pt", padding=True, truncation=True):
+        from transformers import BatchFeature
+        if images is not None:
+            return self.ip(images=images, return_tensors="pt")
+        L = max(len(t) for t in text)
+        ids = torch.full((len(text), L), self.pad_id, dtype=torch.int64)
+        mask = torch.zeros((len(text), L), dtype=torch.int64)
+        for i, t in enumerate(text):
+            ids[i, : len(t)] = torch.tensor(t)
+            mask[i, : len(t)] = 1
+        return BatchFeature({"input_ids": ids, "attention_mask": mask})
+
+
+def hf_model(spec, dtype):
+    from transformers import CLIPConfig, CLIPModel, SiglipConfig, SiglipModel
+    v, t = spec.vision, spec.text
+    vc = dict(hidden_size=v.hidden, intermediate_size=v.intermediate, num_hidden_layers=v.layers,
+              num_attention_heads=v.heads, image_size=v.image_size, patch_size=v.patch, hidden_act=v.act,
+              layer_norm_eps=v.eps)
+    tc = dict(hidden_size=t.hidden, intermediate_size=t.intermediate, num_hidden_layers=t.layers,
+              num_attention_heads=t.heads, vocab_size=t.vocab, max_position_embeddings=t.max_pos, hidden_act=t.act,
+              layer_norm_eps=t.eps, eos_token_id=t.eos_id, pad_token_id=t.pad_id)
+    if spec.family == "siglip":
+        tc["projection_size"] = spec.proj_dim
+        cfg = SiglipConfig(text_config=tc, vision_config=vc)
+        m = SiglipModel(cfg)
+    else:
+        tc["bos_token_id"] = t.bos_id
+        cfg = CLIPConfig(text_config=tc, vision_config=vc, projection_dim=spec.proj_dim)
+        m = CLIPModel(cfg)
+    sd = torch_state_dict(spec, seed=0)
+    missing, unexpected = m.load_state_dict(sd, strict=False)
+    missing = [k for k in missing if not k.endswith(("position_ids", "logit_scale", "logit_bias"))]
+    assert not missing and not unexpected, (missing, unexpected)
+    return m.to(dtype).eval()
+
+
+def make_encoders(main):
+    from PIL import Image
+    from transformers.models.siglip.image_processing_pil_siglip import SiglipImageProcessorPil
+    from transformers.models.clip.image_processing_pil_clip import CLIPImageProcessorPil
+
+    for name in ("tiny-siglip", "tiny-clip"):
+        spec = TINY[name]
+        S = spec.vision.image_size
+        rng = np.random.default_rng(7)
+        imgs = rng.integers(0, 256, (5, 112, 112, 3), dtype=np.uint8)
+        pil = [Image.fromarray(a) for a in imgs]
+        t = spec.text
+        lens = [t.max_pos, 5, 9, t.max_pos - 3, 3, 7, 11]
+        caps = []
+        for L in lens:
+            if t.bos_id is not None:
+                body = rng.integers(1, min(t.bos_id, t.eos_id), L - 2).tolist()
+                caps.append([t.bos_id] + body + [t.eos_id])
+            else:
+                body = rng.integers(2, t.vocab, L - 1).tolist()
+                caps.append(body + [t.eos_id])
+        if spec.family == "siglip":
+            ip = SiglipImageProcessorPil(size={"height": S, "width": S})
+        else:
+            ip = CLIPImageProcessorPil(size={"shortest_edge": S}, crop_size={"height": S, "width": S})
+        proc = RefProcessor(ip, t.pad_id)
+        m_info = {"name": name, "type": spec.m_info["type"], "batch_size": spec.batch_size}
+        out = {"images": imgs, "lens": np.array(lens, np.int64)}
+        Lmax = max(lens)
+        ids = np.full((len(caps), Lmax), t.pad_id, np.int64)
+        for i, c in enumerate(caps):
+            ids[i, : len(c)] = c
+        out["ids"] = ids
+        for tag, dtype in (("bf16", torch.bfloat16), ("f32", torch.float32)):
+            hf = hf_model(spec, dtype)
+            main.DEVICE, main.DTYPE = "cpu", dtype
+            with torch.no_grad():
+                img_e, txt_e = main.encode_data(RefAdapter(hf), proc, m_info, pil, caps)
+            if tag == "bf16":
+                out["img_bf16"], out["txt_bf16"] = bf16_bits(img_e), bf16_bits(txt_e)
+            else:
+                out["img_f32"], out["txt_f32"] = img_e.float().numpy(), txt_e.float().numpy()
+        np.savez_compressed(os.path.join(HERE, f"{name}.npz"), **out)
+        print(f"{name}.npz:", {k: v.shape for k, v in out.items()})
+
+
+# ------------------------------------------------------------------ retrieval
+def planted(n, caps, D, noise, seed=0):
+    """SURVEY.md §8d planted embeddings: img = norm(base + noise*N), cap_{5i+j} = norm(base_i + noise*N)."""
+    g = torch.Generator().manual_seed(seed)
+    base = torch.randn(n, D, generator=g)
+    img = base + noise * torch.randn(n, D, generator=g)
+    cap = base.repeat_interleave(caps, 0) + noise * torch.randn(n * caps, D, generator=g)
+    img = (img / img.norm(dim=-1, keepdim=True)).to(torch.bfloat16)
+    cap = (cap / cap.norm(dim=-1, keepdim=True)).to(torch.bfloat16)
+    return img, cap
+
+
+def make_retrieval(main):
+    n, caps, D = 500, 5, 128
+    img, all_txt = planted(n, caps, D, noise=1.6)
+    t2i = all_txt[::caps].contiguous()
+    m_info = {"type": "dense"}
+    main.DEVICE = "cpu"
+    s_t2i = main.compute_similarity_scores(img, t2i, m_info, None)           # [n, n] = t2i @ img.T
+    s_i2t = main.compute_similarity_scores(all_txt, img, m_info, None)       # [n, 5n] = img @ all.T (no .t())
+    s_sym = s_t2i.t()
+    metrics = main.compute_metrics_detailed(s_t2i, s_i2t, s_sym, list(range(n)),
+                                            {i: list(range(caps * i, caps * i + caps)) for i in range(n)},
+                                            {i: i for i in range(n)}, [""] * n)
+    out = {"img": bf16_bits(img), "all_txt": bf16_bits(all_txt)}
+    for tag, s in (("t2i", s_t2i), ("i2t", s_i2t), ("sym", s_sym.contiguous())):
+        v, ix = torch.topk(s, 11, dim=1)
+        out[f"{tag}_idx"] = ix[:, :10].numpy().astype(np.int32)
+        out[f"{tag}_score"] = v[:, :10].numpy()
+        out[f"{tag}_margin"] = (v[:, 9] - v[:, 10]).numpy()
+    keys = [k for k in metrics if not k.startswith("_")]
+    out["metric_names"] = np.array(keys)
+    out["metric_values"] = np.array([metrics[k] for k in keys], np.float64)
+    np.savez_compressed(os.path.join(HERE, "retrieval.npz"), **out)
+    print("retrieval.npz:", dict(zip(keys, out["metric_values"].round(2))))
+
+
+# ------------------------------------------------------------------ maxsim + l2norm
+def make_maxsim(main):
+    from transformers.models.colpali.processing_colpali import ColPaliProcessor
+
+    class Scorer:
+        def score(self, qs, ps):
+            return ColPaliProcessor.score_retrieval(None, qs, ps, output_dtype=torch.float32)
+
+    out = {}
+    rng = torch.Generator().manual_seed(3)
+    for case, (nq, nd, qr, dr) in {"ragged": (23, 27, (5, 31), (20, 71)), "fixed": (12, 14, (26, 27), (64, 65))}.items():
+        def mk(n, lo, hi):
+            vs = []
+            for _ in range(n):
+                T = int(torch.randint(lo, hi, (1,), generator=rng))
+                v = torch.randn(T, 128, generator=rng)
+                vs.append((v / v.norm(dim=-1, keepdim=True)).to(torch.bfloat16))
+            return vs
+        qs, ds = mk(nq, *qr), mk(nd, *dr)
+        main.DEVICE = "cpu"
+        # the reference's own 10 x 10 chunk loop (main.py:451-470)
+        s = main.compute_similarity_scores(ds, qs, {"type": "colpali"}, Scorer())
+        out[f"{case}_q"] = np.concatenate([bf16_bits(v) for v in qs])
+        out[f"{case}_qlen"] = np.array([v.shape[0] for v in qs], np.int32)
+        out[f"{case}_d"] = np.concatenate([bf16_bits(v) for v in ds])
+        out[f"{case}_dlen"] = np.array([v.shape[0] for v in ds], np.int32)
+        out[f"{case}_score"] = s.numpy().astype(np.float32)
+    np.savez_compressed(os.path.join(HERE, "maxsim.npz"), **out)
+    print("maxsim.npz:", {k: v.shape for k, v in out.items()})
+
+
+def make_l2norm(main):
+    """main.py:414 `out / out.norm(dim=-1, keepdim=True)` on bf16 model outputs."""
+    g = torch.Generator().manual_seed(5)
+    x = (torch.randn(96, 1152, generator=g) * torch.rand(96, 1, generator=g) * 4).to(torch.bfloat16)
+
+    class Feed:
+        def get_image_features(self, pixel_values):
+            return x[pixel_values[:, 0].long()]
+
+    class P:
+        def __call__(self, images=None, **_):
+            from transformers import BatchFeature
+            return BatchFeature({"pixel_values": torch.tensor(images, dtype=torch.float32)[:, None]})
+
+    main.DEVICE, main.DTYPE = "cpu", torch.bfloat16
+    y, _ = main.encode_data(Feed(), P(), {"type": "dense", "batch_size": 32}, list(range(96)), [])
+    np.savez_compressed(os.path.join(HERE, "l2norm.npz"), x=bf16_bits(x), y=bf16_bits(y))
+    print("l2norm.npz", y.shape)
+
+
+if __name__ == "__main__":
+    torch.manual_seed(0)
+    main = import_reference()
+    make_preprocess()
+    make_l2norm(main)
+    make_retrieval(main)
+    make_maxsim(main)
+    make_encoders(main)

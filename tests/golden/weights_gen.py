@@ -1,0 +1,87 @@
+"""Deterministic weights for the tiny parity models (test data generator).
+
+numpy PCG64 (default_rng) is bit-stable across platforms, so the GPU box
+regenerates exactly the weights tests/golden/make_goldens.py fed to the
+reference here — no weight files need to be committed. Every value is rounded
+to bf16 (RNE) and stored as fp32, so the fp32 and bf16 reference runs use the
+same numbers. Names/shapes follow transformers' SiglipModel / CLIPModel.
+"""
+from __future__ import annotations
+
+import math
+from typing import Dict
+
+import numpy as np
+
+
+def bf16_round(a: np.ndarray) -> np.ndarray:
+    """Round fp32 to the nearest bf16 (ties to even), returned as fp32."""
+    u = np.ascontiguousarray(a, dtype=np.float32).view(np.uint32).astype(np.uint64)
+    r = ((u + 0x7FFF + ((u >> 16) & 1)) >> 16) << 16
+    return r.astype(np.uint32).view(np.float32)
+
+
+def np_state_dict(spec, seed: int = 0) -> Dict[str, np.ndarray]:
+    rng = np.random.default_rng(seed)
+    sd: Dict[str, np.ndarray] = {}
+
+    def put(name, arr):
+        sd[name] = bf16_round(np.asarray(arr, dtype=np.float32))
+
+    def lin(name, out_f, in_f, bias=True):
+        a = math.sqrt(6.0 / (in_f + out_f))
+        put(name + ".weight", rng.uniform(-a, a, (out_f, in_f)))
+        if bias:
+            put(name + ".bias", rng.normal(0, 0.02, out_f))
+
+    def ln(name, d):
+        put(name + ".weight", 1.0 + rng.normal(0, 0.05, d))
+        put(name + ".bias", rng.normal(0, 0.02, d))
+
+    def layers(prefix, cfg):
+        d, I = cfg.hidden, cfg.intermediate
+        for i in range(cfg.layers):
+            p = f"{prefix}.encoder.layers.{i}."
+            ln(p + "layer_norm1", d)
+            for n in ("q_proj", "k_proj", "v_proj", "out_proj"):
+                lin(p + "self_attn." + n, d, d)
+            ln(p + "layer_norm2", d)
+            lin(p + "mlp.fc1", I, d)
+            lin(p + "mlp.fc2", d, I)
+
+    v, t = spec.vision, spec.text
+    d = v.hidden
+    put("vision_model.embeddings.patch_embedding.weight",
+        rng.normal(0, 1 / math.sqrt(3 * v.patch * v.patch), (d, 3, v.patch, v.patch)))
+    T = v.num_patches + (1 if spec.family == "clip" else 0)
+    put("vision_model.embeddings.position_embedding.weight", rng.normal(0, 1 / math.sqrt(d), (T, d)))
+    layers("vision_model", v)
+    ln("vision_model.post_layernorm", d)
+    put("text_model.embeddings.token_embedding.weight", rng.normal(0, 1 / math.sqrt(t.hidden), (t.vocab, t.hidden)))
+    put("text_model.embeddings.position_embedding.weight",
+        rng.normal(0, 1 / math.sqrt(t.hidden), (t.max_pos, t.hidden)))
+    layers("text_model", t)
+    ln("text_model.final_layer_norm", t.hidden)
+    if spec.family == "siglip":
+        put("vision_model.embeddings.patch_embedding.bias", rng.normal(0, 0.02, d))
+        put("vision_model.head.probe", rng.normal(0, 1 / math.sqrt(d), (1, 1, d)))
+        a = math.sqrt(6.0 / (4 * d))
+        put("vision_model.head.attention.in_proj_weight", rng.uniform(-a, a, (3 * d, d)))
+        put("vision_model.head.attention.in_proj_bias", rng.normal(0, 0.02, 3 * d))
+        lin("vision_model.head.attention.out_proj", d, d)
+        ln("vision_model.head.layernorm", d)
+        lin("vision_model.head.mlp.fc1", v.intermediate, d)
+        lin("vision_model.head.mlp.fc2", d, v.intermediate)
+        lin("text_model.head", spec.proj_dim, t.hidden)
+    else:
+        put("vision_model.embeddings.class_embedding", rng.normal(0, 1 / math.sqrt(d), d))
+        ln("vision_model.pre_layrnorm", d)
+        lin("visual_projection", spec.proj_dim, d, bias=False)
+        lin("text_projection", spec.proj_dim, t.hidden, bias=False)
+    return sd
+
+
+def torch_state_dict(spec, seed: int = 0, dtype=None):
+    import torch
+    dtype = dtype or torch.float32
+    return {k: torch.from_numpy(v.copy()).to(dtype) for k, v in np_state_dict(spec, seed).items()}

@@ -1,0 +1,64 @@
+"""The C ABI library loads, exports every declared entry point, and validates
+arguments before touching the GPU (runs on the CPU container)."""
+import ctypes
+import os
+import re
+
+import pytest
+
+from mme import _lib
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "mme.h")
+
+
+def declared_functions():
+    src = open(HEADER).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(mme_\w+)\s*\(", src)))
+
+
+def test_header_declares_expected_surface():
+    fns = declared_functions()
+    for f in ("mme_gemm", "mme_attention", "mme_layernorm", "mme_l2norm", "mme_preprocess_u8", "mme_sim_topk",
+              "mme_maxsim", "mme_recall_hits"):
+        assert f in fns
+
+
+def test_library_exports_every_declared_symbol():
+    lib = _lib.load()
+    missing = [f for f in declared_functions() if not hasattr(lib, f)]
+    assert not missing, missing
+
+
+def test_python_binding_covers_header():
+    assert set(declared_functions()) == set(_lib.SIGNATURES)
+
+
+def test_abi_version():
+    assert _lib.load().mme_abi_version() == _lib.ABI_VERSION
+
+
+@pytest.mark.parametrize("call,match", [
+    (lambda: _lib.call("mme_gemm", None, 64, None, 64, None, 64, 4, 8, 64, None, None, 0, 0, 0, 0, None),
+     "null operand"),
+    (lambda: _lib.call("mme_gemm", 16, 100, 16, 100, 16, 8, 4, 8, 100, None, None, 0, 0, 0, 0, None),
+     "multiple of 64"),
+    (lambda: _lib.call("mme_attention", 16, 3456, 16, 1152, 2, 729, 16, 96, None, 0, 0.1, None),
+     "head_dim 96"),
+    (lambda: _lib.call("mme_sim_topk", 16, 64, 16, 64, 10, 5, 64, 10, 0, 16, 16, 16, 1 << 20, None),
+     "k=10 out of range"),
+    (lambda: _lib.call("mme_maxsim", 16, 16, 2, 8, 16, 16, None, 2, 24, 128, 16, 16, 1 << 20, None),
+     "Ld % 16"),
+    (lambda: _lib.call("mme_layernorm", 16, 4096, 16, 16, 16, 4096, 4, 4096, 1e-5, None, None),
+     "unsupported"),
+])
+def test_argument_errors_are_reported(call, match):
+    with pytest.raises(_lib.MMEError, match=match):
+        call()
+
+
+def test_workspace_queries():
+    assert _lib.query("mme_sim_topk_workspace_bytes", 5000, 25000, 10) > 5000 * 10 * 8
+    assert _lib.query("mme_maxsim_workspace_bytes", 10, 32, 100) >= 10 * 32 * 100 * 2
+    assert _lib.query("mme_preprocess_workspace_bytes", 4, 224, 224, 384, 384) >= 4 * 224 * 384 * 3

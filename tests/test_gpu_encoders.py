@@ -1,0 +1,88 @@
+"""Encoder towers on the MI355X vs the reference's encode_data outputs.
+
+Tiny configs (head dims 72 / 80 / 64, ragged captions, padded MLP widths) are
+pinned by tests/golden/tiny-*.npz, produced by main.encode_data over the HF
+modules (make_goldens.py). Full-size towers (random weights at the exact
+architecture) are checked against the fp32 CPU oracle on a few inputs.
+Tolerance: the oracle is fp32, the device path bf16 with fp32 accumulation —
+per-row cosine >= 0.999 (SURVEY.md §8d parity criteria).
+"""
+import numpy as np
+import pytest
+import torch
+
+from helpers import bits_to_f32, row_cos
+from mme import encode, get_spec
+from mme.models import CLIPModel, SiglipModel
+from mme.processor import Processor
+from weights_gen import torch_state_dict
+
+pytestmark = pytest.mark.gpu
+
+COS_MIN = 0.999
+
+
+def _model(spec):
+    sd = torch_state_dict(spec, 0, torch.bfloat16)
+    cls = SiglipModel if spec.family == "siglip" else CLIPModel
+    return cls.from_spec(spec, device="cuda", state_dict=sd)
+
+
+def _inputs(g):
+    caps = [g["ids"][i, :l].tolist() for i, l in enumerate(g["lens"])]
+    return list(g["images"]), caps
+
+
+@pytest.mark.parametrize("name", ["tiny-siglip", "tiny-clip"])
+def test_encode_data_hf_surface(cuda, golden, name):
+    """mme.encode.encode_data (main.py:386-438 restated) through the processor/model duck type."""
+    spec = get_spec(name)
+    g = golden(name)
+    model, proc = _model(spec), Processor(spec)
+    imgs, caps = _inputs(g)
+    ie, te = encode.encode_data(model, proc, spec.m_info, imgs, caps)
+    for got, key in ((ie, "img"), (te, "txt")):
+        ref32 = torch.from_numpy(g[key + "_f32"])
+        ref16 = torch.from_numpy(bits_to_f32(g[key + "_bf16"]))
+        assert got.dtype == torch.bfloat16 and got.device.type == "cpu"
+        assert row_cos(got, ref32).min() >= COS_MIN, f"{name} {key} vs fp32 reference"
+        assert row_cos(got, ref16).min() >= COS_MIN, f"{name} {key} vs bf16 reference"
+        assert (got.float() - ref32).abs().max() < 1.5e-2
+
+
+@pytest.mark.parametrize("name", ["tiny-siglip", "tiny-clip"])
+def test_fast_paths_match_surface(cuda, golden, name):
+    """encode_images(u8) / encode_texts(ids, lens) == the HF-surface path (same kernels, fused preprocessing)."""
+    spec = get_spec(name)
+    g = golden(name)
+    model, proc = _model(spec), Processor(spec)
+    imgs, caps = _inputs(g)
+    ie, te = encode.encode_data(model, proc, spec.m_info, imgs, caps)
+    fi = model.encode_images(torch.from_numpy(g["images"]).cuda(), batch=2).cpu()
+    ids = torch.from_numpy(g["ids"]).cuda()
+    lens = torch.from_numpy(g["lens"])
+    ft = model.encode_texts(ids, lens, ref_batch=spec.batch_size, exec_batch=3).cpu()
+    assert torch.equal(fi, ie)
+    assert torch.equal(ft, te)
+
+
+@pytest.mark.slow
+@pytest.mark.parametrize("name,n_img,n_cap", [("SigLIP-400M", 2, 3), ("OpenAI-CLIP-L", 1, 2), ("LAION-CLIP-H", 1, 2)])
+def test_full_size_towers_vs_oracle(cuda, name, n_img, n_cap):
+    from oracle import encoders as oracle_enc
+    from mme.processor import synthetic_caption_ids, synthetic_images
+    from mme.weights import random_state_dict
+    spec = get_spec(name)
+    sd = random_state_dict(spec, seed=0, device="cuda")
+    cls = SiglipModel if spec.family == "siglip" else CLIPModel
+    model = cls.from_spec(spec, device="cuda", state_dict=sd)
+    imgs = synthetic_images(n_img)
+    ids = synthetic_caption_ids(spec, n_cap)
+    gi = model.encode_images(torch.from_numpy(imgs).cuda()).cpu()
+    gt = model.encode_texts(torch.from_numpy(ids).cuda()).cpu()
+    sd_cpu = {k: v.float().cpu() for k, v in sd.items()}
+    del sd
+    torch.set_num_threads(16)
+    oi, ot = oracle_enc.encode_data(spec, sd_cpu, list(imgs), ids.tolist(), bs=n_img, out_dtype=torch.float32)
+    assert row_cos(gi, oi).min() >= COS_MIN
+    assert row_cos(gt, ot).min() >= COS_MIN

@@ -1,0 +1,202 @@
+"""Numerics of the libmme kernels against plain PyTorch fp32 references (MI355X)."""
+import math
+
+import numpy as np
+import pytest
+import torch
+
+from helpers import bf16_bits, bits_to_bf16
+
+pytestmark = pytest.mark.gpu
+
+from mme import _lib, ops  # noqa: E402
+
+
+def act_ref(y, act):
+    if act == _lib.ACT_GELU_TANH:
+        return torch.nn.functional.gelu(y, approximate="tanh")
+    if act == _lib.ACT_QUICK_GELU:
+        return y * torch.sigmoid(1.702 * y)
+    if act == _lib.ACT_GELU_ERF:
+        return torch.nn.functional.gelu(y)
+    return y
+
+
+def rnd(*shape, scale=1.0, gen=None, device="cuda"):
+    return (torch.randn(*shape, generator=gen, device=device) * scale).to(torch.bfloat16)
+
+
+@pytest.mark.parametrize("M,N,K", [(1, 128, 64), (100, 200, 128), (1458, 1152, 1152), (300, 64, 640),
+                                   (4096, 4352, 1152), (2048, 3456, 1152), (517, 1152, 4352), (33, 8, 64)])
+@pytest.mark.parametrize("act", [0, 1, 2, 3])
+def test_gemm_bias_act(cuda, M, N, K, act):
+    g = torch.Generator(device="cuda").manual_seed(M * 7 + N + act)
+    a = rnd(M, K, gen=g)
+    w = rnd(N, K, scale=1 / math.sqrt(K), gen=g)
+    b = rnd(N, scale=0.1, gen=g)
+    out = ops.gemm(a, w, b, act=act)
+    ref = act_ref(a.float() @ w.float().T + b.float(), act)
+    torch.testing.assert_close(out.float(), ref, atol=2e-2, rtol=1e-2)
+
+
+@pytest.mark.parametrize("period", [0, 49, 729])
+def test_gemm_residual_period_inplace(cuda, period):
+    g = torch.Generator(device="cuda").manual_seed(period + 1)
+    M, N, K = 729 * 3, 1152, 640
+    a = rnd(M, K, gen=g)
+    w = rnd(N, K, scale=1 / math.sqrt(K), gen=g)
+    if period:
+        res = rnd(period, N, gen=g)
+        rows = torch.arange(M, device="cuda") % period
+        ref = a.float() @ w.float().T + res.float()[rows]
+        out = ops.gemm(a, w, residual=res, res_period=period)
+    else:
+        x = rnd(M, N, gen=g)
+        ref = a.float() @ w.float().T + x.float()
+        out = ops.gemm(a, w, residual=x, out=x)  # in place on the residual stream
+        assert out.data_ptr() == x.data_ptr()
+    torch.testing.assert_close(out.float(), ref, atol=3e-2, rtol=1e-2)
+
+
+def test_gemm_strided_views_and_f32(cuda):
+    g = torch.Generator(device="cuda").manual_seed(3)
+    big = rnd(640, 4352, gen=g)
+    a = big[:, :1152]  # ld = 4352
+    w = rnd(256, 1152, scale=1 / 34, gen=g)
+    out = torch.empty(640, 512, device="cuda", dtype=torch.float32)
+    ops.gemm(a, w, out=out[:, 128:384], out_f32=True)
+    ref = a.float() @ w.float().T
+    torch.testing.assert_close(out[:, 128:384], ref, atol=1e-4, rtol=1e-4)
+
+
+def test_gemm_rejects_bad_k(cuda):
+    a = torch.zeros(4, 100, dtype=torch.bfloat16, device="cuda")
+    w = torch.zeros(8, 100, dtype=torch.bfloat16, device="cuda")
+    with pytest.raises(_lib.MMEError, match="multiple of 64"):
+        ops.gemm(a, w)
+
+
+def test_gemm_rejects_cpu_tensor():
+    a = torch.zeros(4, 64, dtype=torch.bfloat16)
+    with pytest.raises(ValueError, match="no host fallback"):
+        ops.gemm(a, a)
+
+
+def attn_ref(qkv, B, T, H, hd, lens, causal, scale):
+    q, k, v = qkv.float().view(B, T, 3, H, hd).permute(2, 0, 3, 1, 4)
+    s = (q @ k.transpose(-1, -2)) * scale
+    mask = torch.zeros(B, 1, T, T, dtype=torch.bool, device=qkv.device)
+    if lens is not None:
+        ar = torch.arange(T, device=qkv.device)
+        mask |= (ar[None, :] >= lens[:, None].long())[:, None, None, :]
+    if causal:
+        mask |= torch.triu(torch.ones(T, T, dtype=torch.bool, device=qkv.device), 1)
+    s = s.masked_fill(mask, float("-inf"))
+    p = torch.softmax(s, -1)
+    return (p @ v).transpose(1, 2).reshape(B * T, H * hd)
+
+
+@pytest.mark.parametrize("B,T,H,hd,causal,lens", [
+    (2, 729, 16, 72, False, None),     # SigLIP-400M vision
+    (2, 64, 16, 72, False, [64, 23]),  # SigLIP text with padding mask
+    (3, 77, 12, 64, True, None),       # CLIP-L text
+    (3, 77, 16, 64, True, [77, 9, 40]),
+    (2, 257, 16, 80, False, None),     # ViT-H/14-224
+    (1, 730, 4, 80, False, None),      # DFN5B-H-378
+    (2, 577, 4, 64, False, None),      # CLIP-L-336
+    (3, 17, 4, 80, False, None),
+    (4, 16, 8, 72, False, [16, 5, 9, 13]),
+    (2, 1, 2, 64, False, None),
+])
+def test_attention(cuda, B, T, H, hd, causal, lens):
+    g = torch.Generator(device="cuda").manual_seed(B * T + hd)
+    qkv = rnd(B * T, 3 * H * hd, scale=1.5, gen=g)
+    sl = None if lens is None else torch.tensor(lens, dtype=torch.int32, device="cuda")
+    out = ops.attention(qkv, B, T, H, hd, seq_lens=sl, causal=causal)
+    ref = attn_ref(qkv, B, T, H, hd, sl, causal, hd ** -0.5)
+    torch.testing.assert_close(out.float(), ref, atol=2e-2, rtol=2e-2)
+
+
+def test_attention_strided_qkv(cuda):
+    B, T, H, hd = 2, 100, 16, 72
+    g = torch.Generator(device="cuda").manual_seed(9)
+    wide = rnd(B * T, 4352, gen=g)
+    qkv = wide[:, : 3 * H * hd]
+    out = ops.attention(qkv, B, T, H, hd)
+    torch.testing.assert_close(out.float(), attn_ref(qkv.contiguous(), B, T, H, hd, None, False, hd ** -0.5),
+                               atol=2e-2, rtol=2e-2)
+
+
+@pytest.mark.parametrize("B,T,H,hd", [(3, 729, 16, 72), (2, 49, 8, 72)])
+def test_probe_attention(cuda, B, T, H, hd):
+    g = torch.Generator(device="cuda").manual_seed(T)
+    d = H * hd
+    q = rnd(d, gen=g)
+    kv = rnd(B * T, 2 * d, gen=g)
+    out = ops.probe_attention(q, kv, B, T, H, hd)
+    k = kv.float()[:, :d].view(B, T, H, hd).transpose(1, 2)
+    v = kv.float()[:, d:].view(B, T, H, hd).transpose(1, 2)
+    qq = q.float().view(1, H, 1, hd)
+    p = torch.softmax((qq @ k.transpose(-1, -2)) * hd ** -0.5, -1)
+    ref = (p @ v).reshape(B, d)
+    torch.testing.assert_close(out.float(), ref, atol=2e-2, rtol=2e-2)
+
+
+@pytest.mark.parametrize("rows,d", [(1, 64), (1000, 1152), (37, 1280), (5, 768), (9, 320)])
+def test_layernorm(cuda, rows, d):
+    g = torch.Generator(device="cuda").manual_seed(rows + d)
+    x = rnd(rows, d, scale=3.0, gen=g) + 0.5
+    gm = rnd(d, gen=g)
+    bt = rnd(d, gen=g)
+    out = ops.layernorm(x, gm, bt, 1e-6)
+    ref = torch.nn.functional.layer_norm(x.float(), (d,), gm.float(), bt.float(), 1e-6)
+    torch.testing.assert_close(out.float(), ref, atol=3e-2, rtol=1e-2)
+    idx = torch.tensor([rows - 1, 0], dtype=torch.int32, device="cuda")
+    out2 = ops.layernorm(x, gm, bt, 1e-6, rows_idx=idx)
+    torch.testing.assert_close(out2.float(), ref[idx.long()], atol=3e-2, rtol=1e-2)
+
+
+def test_l2norm_bit_exact(cuda, golden):
+    g = golden("l2norm")
+    x = bits_to_bf16(g["x"]).cuda()
+    y = ops.l2norm(x)
+    assert np.array_equal(bf16_bits(y), g["y"]), "mme_l2norm differs from main.py:414 semantics"
+
+
+def test_token_embed(cuda):
+    g = torch.Generator(device="cuda").manual_seed(1)
+    tok = rnd(1000, 256, gen=g)
+    pos = rnd(20, 256, gen=g)
+    ids = torch.randint(0, 1000, (3, 20), device="cuda", generator=g)
+    out = ops.token_embed(ids, tok, pos)
+    ref = (tok.float()[ids] + pos.float()[None]).to(torch.bfloat16).view(60, 256)
+    assert torch.equal(out, ref)
+
+
+def test_clip_embed_ln(cuda):
+    g = torch.Generator(device="cuda").manual_seed(2)
+    B, P, d = 3, 16, 320
+    patch = rnd(B * P, d, gen=g)
+    cls = rnd(d, gen=g)
+    pos = rnd(P + 1, d, gen=g)
+    gm, bt = rnd(d, gen=g), rnd(d, gen=g)
+    out = ops.clip_embed_ln(patch, cls, pos, gm, bt, 1e-5, B, P)
+    x = torch.cat([cls.view(1, 1, d).expand(B, 1, d), patch.view(B, P, d)], 1)
+    x = (x.float() + pos.float()).to(torch.bfloat16).float()
+    ref = torch.nn.functional.layer_norm(x, (d,), gm.float(), bt.float(), 1e-5).view(B * (P + 1), d)
+    torch.testing.assert_close(out.float(), ref, atol=3e-2, rtol=1e-2)
+
+
+def test_text_pool_rows(cuda):
+    ids = torch.tensor([[5, 9, 7, 2, 2], [5, 3, 2, 8, 1], [1, 1, 1, 1, 1]], device="cuda")
+    assert ops.text_pool_rows(ids, 2, 0).tolist() == [3, 5 + 2, 10 + 0]  # first eos (argmax of mask)
+    assert ops.text_pool_rows(ids, 2, 1).tolist() == [1, 5 + 3, 10 + 0]  # argmax of ids (first max)
+    assert ops.text_pool_rows(ids, 2, 2).tolist() == [4, 9, 14]
+
+
+def test_im2col(cuda):
+    pv = torch.randn(2, 3, 56, 56, device="cuda")
+    out = ops.im2col(pv, 14, 640)
+    ref = torch.nn.functional.unfold(pv, 14, stride=14).transpose(1, 2).reshape(2 * 16, 588)
+    assert torch.equal(out[:, :588], ref.to(torch.bfloat16))
+    assert not out[:, 588:].any()

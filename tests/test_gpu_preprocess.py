@@ -1,0 +1,57 @@
+"""Device preprocessing vs PIL + HF (tests/golden/preprocess.npz): bit-exact."""
+import numpy as np
+import pytest
+import torch
+
+from mme import ops
+from mme.config import IMAGENET_STANDARD_MEAN, IMAGENET_STANDARD_STD, OPENAI_CLIP_MEAN, OPENAI_CLIP_STD, ImageProcConfig
+from mme.processor import image_geometry
+from oracle import pil_bicubic
+
+pytestmark = pytest.mark.gpu
+CASES = ["siglip384", "clip336", "dfn378", "clip336_nonsq", "vith224_down"]
+
+
+def _cfg(kind, S):
+    if kind == 0:
+        return ImageProcConfig(S, "square", IMAGENET_STANDARD_MEAN, IMAGENET_STANDARD_STD)
+    return ImageProcConfig(S, "shortest_edge", OPENAI_CLIP_MEAN, OPENAI_CLIP_STD)
+
+
+@pytest.mark.parametrize("case", CASES)
+def test_preprocess_pixel_values_bit_exact(cuda, golden, case):
+    g = golden("preprocess")
+    H, W, S, kind = (int(v) for v in g[case + "_meta"])
+    ip = _cfg(kind, S)
+    rh, rw, top, left = image_geometry(H, W, ip)
+    imgs = torch.from_numpy(g[case + "_in"][None]).cuda()
+    pv = ops.preprocess_u8(imgs, resize=(rh, rw), crop=(top, left), size=S, mean=ip.mean, std=ip.std)
+    ref = pil_bicubic.normalize(g[case + "_u8"], ip.mean, ip.std)
+    got = pv[0].cpu().numpy()
+    assert np.array_equal(got.view(np.uint32), ref.view(np.uint32)), \
+        f"{case}: {np.sum(got != ref)} pixel values differ from PIL+HF"
+
+
+@pytest.mark.parametrize("case", ["siglip384", "clip336"])
+def test_preprocess_patches_match_im2col(cuda, golden, case):
+    g = golden("preprocess")
+    H, W, S, kind = (int(v) for v in g[case + "_meta"])
+    ip = _cfg(kind, S)
+    rh, rw, top, left = image_geometry(H, W, ip)
+    imgs = torch.from_numpy(np.stack([g[case + "_in"]] * 3)).cuda()
+    patches = ops.preprocess_u8(imgs, resize=(rh, rw), crop=(top, left), size=S, mean=ip.mean, std=ip.std,
+                                patch=14, kpad=640)
+    pv = torch.from_numpy(pil_bicubic.normalize(g[case + "_u8"], ip.mean, ip.std)).cuda()
+    ref = ops.im2col(pv[None].expand(3, -1, -1, -1).contiguous(), 14, 640)
+    assert torch.equal(patches, ref)
+
+
+def test_preprocess_batch_of_synthetic(cuda):
+    rng = np.random.default_rng(11)
+    imgs = rng.integers(0, 256, (6, 224, 224, 3), dtype=np.uint8)
+    ip = _cfg(0, 384)
+    pv = ops.preprocess_u8(torch.from_numpy(imgs).cuda(), resize=(384, 384), crop=(0, 0), size=384, mean=ip.mean,
+                           std=ip.std).cpu().numpy()
+    for i in range(6):
+        ref = pil_bicubic.normalize(pil_bicubic.preprocess_u8(imgs[i], 384, "square"), ip.mean, ip.std)
+        assert np.array_equal(pv[i], ref)
