@@ -59,7 +59,7 @@ int mme_abi_version(void);
  * (rh, rw) resized size, then a crop of S x S at (top, left) (CLIP center crop;
  *          SigLIP: rh = rw = S, top = left = 0).
  * out   : MME_PIX_F32_NCHW -> float [n,3,S,S]
- *         MME_PIX_PATCHES  -> bf16 [n*(S/patch)^2, kpad], column c*p*p+ky*p+kx
+ *         MME_PIX_PATCHES  -> bf16 [n*G*G, kpad], G = floor(S/patch) (Conv2d 'valid'), column c*p*p+ky*p+kx
  *                             (Conv2d weight flattening), zero for col >= 3*p*p.
  * mean3/std3: HOST float[3] (per-channel, copied into the kernel arguments).
  * workspace: >= mme_preprocess_workspace_bytes(n, H, W, rh, rw) bytes. */
@@ -80,7 +80,7 @@ int mme_im2col(const void* pixels, int in_is_f32, int n, int S, int patch, int k
  * Replaces nn.Linear / Conv2d GEMMs of the SigLIP / CLIP towers
  * (TF:models/siglip/modeling_siglip.py:268-322, TF:models/clip/modeling_clip.py).
  * bf16 in, fp32 accumulate (MFMA 16x16x32), bf16 out (or fp32 if out_f32).
- * Requires K % 64 == 0, N % 8 == 0, lda/ldb/ldc/ldr % 8 == 0, 16-B aligned rows. */
+ * Requires K % 64 == 0, lda/ldb % 8 == 0 and 16-B aligned A/B rows (C/residual: any ld). */
 int mme_gemm(const void* A, int lda, const void* B, int ldb, void* C, int ldc, int M, int N, int K,
              const void* bias, const void* residual, int ldr, int res_period, int act, int out_f32,
              void* stream);

@@ -96,8 +96,7 @@ extern "C" int mme_gemm(const void* A, int lda, const void* B, int ldb, void* Cp
     MME_REQUIRE(A && B && Cp, "mme_gemm: null operand");
     MME_REQUIRE(M > 0 && N > 0 && K > 0, "mme_gemm: empty shape M=%d N=%d K=%d", M, N, K);
     MME_REQUIRE(K % BK == 0, "mme_gemm: K=%d must be a multiple of %d (pad weights/activations)", K, BK);
-    MME_REQUIRE(N % 8 == 0, "mme_gemm: N=%d must be a multiple of 8", N);
-    MME_REQUIRE(lda % 8 == 0 && ldb % 8 == 0 && ldc % 8 == 0, "mme_gemm: leading dims must be multiples of 8");
+    MME_REQUIRE(lda % 8 == 0 && ldb % 8 == 0, "mme_gemm: lda/ldb must be multiples of 8 (16-B rows)");
     MME_REQUIRE(lda >= K && ldb >= K && ldc >= N, "mme_gemm: leading dim smaller than the row");
     MME_REQUIRE(((uintptr_t)A & 15) == 0 && ((uintptr_t)B & 15) == 0, "mme_gemm: A/B must be 16-byte aligned");
     MME_REQUIRE(!residual || ldr >= N, "mme_gemm: ldr < N");

@@ -199,7 +199,7 @@ extern "C" int mme_preprocess_u8(const uint8_t* imgs, int n, int H, int W, int r
     MME_REQUIRE(ws_bytes >= mme_preprocess_workspace_bytes(n, H, W, rh, rw),
                 "mme_preprocess_u8: workspace too small");
     if (out_kind == MME_PIX_PATCHES)
-        MME_REQUIRE(patch > 0 && S % patch == 0 && kpad >= 3 * patch * patch && kpad % 8 == 0,
+        MME_REQUIRE(patch > 0 && S >= patch && kpad >= 3 * patch * patch && kpad % 8 == 0,
                     "mme_preprocess_u8: bad patch/kpad");
     else
         MME_REQUIRE(out_kind == MME_PIX_F32_NCHW, "mme_preprocess_u8: bad out_kind %d", out_kind);
@@ -243,7 +243,7 @@ extern "C" int mme_preprocess_u8(const uint8_t* imgs, int n, int H, int W, int r
 extern "C" int mme_im2col(const void* pixels, int in_is_f32, int n, int S, int patch, int kpad, void* out,
                           void* stream) {
     MME_REQUIRE(pixels && out, "mme_im2col: null pointer");
-    MME_REQUIRE(n >= 0 && patch > 0 && S % patch == 0 && kpad >= 3 * patch * patch && kpad % 8 == 0,
+    MME_REQUIRE(n >= 0 && patch > 0 && S >= patch && kpad >= 3 * patch * patch && kpad % 8 == 0,
                 "mme_im2col: bad shape");
     if (n == 0) return MME_OK;
     const int G = S / patch;
