@@ -37,17 +37,40 @@ struct GemmArgs {
     int res_period, act, out_f32;
 };
 
-template <class C>
+// Tile order: XCD remap (each XCD gets a contiguous range of tile ids), then
+// GROUP_M-row bands walked column-major inside the band, so the 32 tiles an
+// XCD runs concurrently form a GROUP_M x (32/GROUP_M) patch that shares A row
+// panels and B column panels in that XCD's L2.
+template <int GROUP_M>
+__device__ __forceinline__ void tile_coords(int tile, int nbm, int nbn, int& bm, int& bn) {
+    if (GROUP_M <= 1) {
+        bm = tile / nbn;
+        bn = tile % nbn;
+        return;
+    }
+    const int per_group = GROUP_M * nbn;
+    const int gid = tile / per_group;
+    const int first_m = gid * GROUP_M;
+    const int gsz = min(nbm - first_m, GROUP_M);
+    const int r = tile % per_group;
+    bm = first_m + r % gsz;
+    bn = r / gsz;
+}
+
+template <class C, int GROUP_M>
 __global__ __launch_bounds__(C::NT) void gemm_tn_kernel(GemmArgs p) {
     __shared__ __attribute__((aligned(16))) char lds[C::LDS];
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int wm = wave / C::WN, wn = wave % C::WN;
 
+    const int nbm = (p.M + C::BM - 1) / C::BM;
     const int nbn = (p.N + C::BN - 1) / C::BN;
     const int tile = xcd_remap(blockIdx.x, gridDim.x);
-    const int m0 = (tile / nbn) * C::BM;
-    const int n0 = (tile % nbn) * C::BN;
+    int bm, bn;
+    tile_coords<GROUP_M>(tile, nbm, nbn, bm, bn);
+    const int m0 = bm * C::BM;
+    const int n0 = bn * C::BN;
 
     f32x4 acc[C::FM][C::FN];
     mainloop<C>(p.A, p.lda, p.M, m0, p.B, p.ldb, p.N, n0, p.K, lds, acc, wave, lane);
@@ -78,17 +101,25 @@ __global__ __launch_bounds__(C::NT) void gemm_tn_kernel(GemmArgs p) {
     }
 }
 
-template <class C>
+template <class C, int GROUP_M>
 int launch(const GemmArgs& a, hipStream_t s) {
     const int nbm = (a.M + C::BM - 1) / C::BM, nbn = (a.N + C::BN - 1) / C::BN;
-    hipLaunchKernelGGL(gemm_tn_kernel<C>, dim3(nbm * nbn), dim3(C::NT), 0, s, a);
+    hipLaunchKernelGGL((gemm_tn_kernel<C, GROUP_M>), dim3(nbm * nbn), dim3(C::NT), 0, s, a);
     return mme_check_launch("mme_gemm");
 }
 
 using BigCfg = Cfg<256, 128, 4, 2>;
+using SqCfg = Cfg<256, 256, 2, 4>;
 using SmallCfg = Cfg<128, 128, 2, 2>;
 
+int g_variant = -1;  // dev-only override (tools/gemm_bench.py)
+
 }  // namespace
+
+extern "C" int mme_gemm_variant(int v) {
+    g_variant = v;
+    return MME_OK;
+}
 
 extern "C" int mme_gemm(const void* A, int lda, const void* B, int ldb, void* Cp, int ldc, int M, int N, int K,
                         const void* bias, const void* residual, int ldr, int res_period, int act, int out_f32,
@@ -104,6 +135,17 @@ extern "C" int mme_gemm(const void* A, int lda, const void* B, int ldb, void* Cp
     MME_REQUIRE(act >= MME_ACT_NONE && act <= MME_ACT_GELU_ERF, "mme_gemm: bad act %d", act);
     GemmArgs a{(const bf16*)A, (const bf16*)B, Cp, (const bf16*)bias, (const bf16*)residual,
                lda, ldb, ldc, ldr, M, N, K, res_period, act, out_f32};
-    if ((long)M * N >= 2048L * 1024) return launch<BigCfg>(a, as_stream(stream));
-    return launch<SmallCfg>(a, as_stream(stream));
+    hipStream_t s = as_stream(stream);
+    switch (g_variant) {
+        case 0: return launch<BigCfg, 1>(a, s);
+        case 1: return launch<BigCfg, 4>(a, s);
+        case 2: return launch<BigCfg, 8>(a, s);
+        case 3: return launch<SqCfg, 1>(a, s);
+        case 4: return launch<SqCfg, 4>(a, s);
+        case 5: return launch<SqCfg, 8>(a, s);
+        case 6: return launch<SmallCfg, 8>(a, s);
+        default: break;
+    }
+    if ((long)M * N >= 2048L * 1024) return launch<BigCfg, 1>(a, s);
+    return launch<SmallCfg, 1>(a, s);
 }

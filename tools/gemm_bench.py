@@ -1,0 +1,72 @@
+#!/usr/bin/env python3
+"""GEMM microbenchmark on the SigLIP-400M encoder shapes (HIP-event timed).
+
+Usage: python tools/gemm_bench.py [--rows 186624] [--iters 10] [--variant V]
+Prints per-shape ms and TFLOP/s; --variant selects a dev kernel variant
+(mme_gemm_variant) when the library exposes one.
+"""
+import argparse
+import ctypes
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "multimodal-embedding_amd"))
+import torch  # noqa: E402
+from mme import _lib, ops  # noqa: E402
+
+SHAPES = {  # name: (N, K)  with M = rows (SigLIP vision: 256 images x 729 tokens)
+    "qkv": (3456, 1152), "o_proj": (1152, 1152), "fc1": (4352, 1152), "fc2": (1152, 4352),
+}
+
+
+def main():
+    p = argparse.ArgumentParser()
+    p.add_argument("--rows", type=int, default=256 * 729)
+    p.add_argument("--iters", type=int, default=10)
+    p.add_argument("--variants", default="")
+    p.add_argument("--shapes", default=",".join(SHAPES))
+    a = p.parse_args()
+    lib = _lib.load()
+    has_var = hasattr(lib, "mme_gemm_variant")
+    if has_var:
+        lib.mme_gemm_variant.restype = ctypes.c_int
+        lib.mme_gemm_variant.argtypes = [ctypes.c_int]
+    variants = [int(v) for v in a.variants.split(",")] if a.variants else [-1]
+    g = torch.Generator(device="cuda").manual_seed(0)
+    M = a.rows
+    res = {}
+    for name in a.shapes.split(","):
+        N, K = SHAPES[name]
+        A = (torch.randn(M, K, device="cuda", generator=g)).to(torch.bfloat16)
+        W = (torch.randn(N, K, device="cuda", generator=g) / K ** 0.5).to(torch.bfloat16)
+        C = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
+        ref = None
+        for v in variants:
+            if v >= 0:
+                lib.mme_gemm_variant(v)
+            ops.gemm(A, W, out=C)
+            if ref is None:
+                ref = C.clone()
+            else:
+                err = (C.float() - ref.float()).abs().max().item()
+                assert err < 0.05, f"variant {v} differs: {err}"
+            torch.cuda.synchronize()
+            s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            s.record()
+            for _ in range(a.iters):
+                ops.gemm(A, W, out=C)
+            e.record()
+            torch.cuda.synchronize()
+            ms = s.elapsed_time(e) / a.iters
+            tf = 2.0 * M * N * K / ms / 1e9
+            res[f"{name}/v{v}"] = {"ms": round(ms, 4), "tflops": round(tf, 1)}
+            print(f"{name:7s} v{v:<2d} M={M} N={N} K={K}: {ms:8.3f} ms  {tf:7.1f} TFLOP/s", flush=True)
+    if has_var:
+        lib.mme_gemm_variant(-1)
+    print(json.dumps(res))
+
+
+if __name__ == "__main__":
+    main()
