@@ -101,6 +101,192 @@ __global__ __launch_bounds__(C::NT) void gemm_tn_kernel(GemmArgs p) {
     }
 }
 
+// ---------------------------------------------------------------------------
+// Pipelined kernel (the production path for the encoder GEMMs).
+//
+//   * 256 x {256,128} block tile, 8 waves; each wave owns a TM x TN sub-tile
+//     of 16x16 MFMA tiles computed SWAPPED (D = W-frag x X-frag), so every
+//     lane ends with 4 consecutive output COLUMNS of one row -> 8-byte packed
+//     bf16 writes in the epilogue;
+//   * K in stages of 32 through a 4-deep LDS ring filled by LDS-DMA
+//     (global_load_lds_dwordx4): stages t+1, t+2 stay in flight while stage t
+//     feeds the MFMAs, retired by a COUNTED s_waitcnt vmcnt before a raw
+//     s_barrier (never vmcnt(0) in the loop, no __syncthreads drain);
+//   * 64-byte LDS rows, 16-byte chunk XOR swizzle chunk ^ 3*((row>>3)&1):
+//     conflict-free ds_read_b128 for the 16x16x32 operand pattern; applied on
+//     the DMA source address (the DMA destination is lane-linear);
+//   * epilogue: bias + activation in registers, bf16 tile staged in LDS
+//     (row pitch BN*2+16 B: conflict-free ds_write_b64), then 16-byte
+//     coalesced stores with the residual / position-table add fused.
+// ---------------------------------------------------------------------------
+template <int N>
+__device__ __forceinline__ void vm_wait() {
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+__device__ __forceinline__ int pswz(int row, int chunk) { return chunk ^ (3 * ((row >> 3) & 1)); }
+
+template <int BM_, int BN_, int WM_, int WN_>
+struct PCfg {
+    static constexpr int BM = BM_, BN = BN_, WM = WM_, WN = WN_;
+    static constexpr int NW = WM * WN, NT = NW * 64;
+    static constexpr int TM = BM / WM, TN = BN / WN, FM = TM / 16, FN = TN / 16;
+    static constexpr int BKS = 32, NSTAGE = 4;
+    static constexpr int A_ST = BM * BKS * 2, B_ST = BN * BKS * 2, STAGE = A_ST + B_ST;
+    static constexpr int A_PIECES = A_ST / 1024, PIECES = STAGE / 1024;
+    static constexpr int PPW = PIECES / NW;  // DMA pieces per wave per stage
+    static constexpr int OUT_LD = BN * 2 + 16;
+    static constexpr int LDS_MAIN = NSTAGE * STAGE, LDS_OUT = BM * OUT_LD;
+    static constexpr int LDS = LDS_MAIN > LDS_OUT ? LDS_MAIN : LDS_OUT;
+    static_assert(PPW * NW == PIECES, "stage must split evenly into 1 KiB pieces per wave");
+};
+
+template <class C>
+__device__ __forceinline__ void pipe_wait(int remaining) {
+    // wait until only `remaining` (0..2) later stages of this wave's DMA are in flight
+    if (remaining >= 2)
+        vm_wait<2 * C::PPW>();
+    else if (remaining == 1)
+        vm_wait<C::PPW>();
+    else
+        vm_wait<0>();
+}
+
+template <class C, int GROUP_M, int ACT>
+__global__ __launch_bounds__(C::NT, 2) void gemm_pipe_kernel(GemmArgs p) {
+    __shared__ __attribute__((aligned(16))) char lds[C::LDS];
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wm = wave / C::WN, wn = wave % C::WN;
+    const int g = lane >> 4, li = lane & 15;
+
+    const int nbm = (p.M + C::BM - 1) / C::BM;
+    const int nbn = (p.N + C::BN - 1) / C::BN;
+    const int tile = xcd_remap(blockIdx.x, gridDim.x);
+    int bm, bn;
+    tile_coords<GROUP_M>(tile, nbm, nbn, bm, bn);
+    const int m0 = bm * C::BM, n0 = bn * C::BN;
+
+    // loop-invariant DMA source pointers: piece q of this wave covers 16 rows
+    const bf16* src[C::PPW];
+    int dst[C::PPW];
+#pragma unroll
+    for (int q = 0; q < C::PPW; ++q) {
+        const int piece = wave * C::PPW + q;
+        const bool isA = piece < C::A_PIECES;
+        const int prow = (isA ? piece : piece - C::A_PIECES) * 16 + (lane >> 2);
+        const int logical = pswz(prow, lane & 3);
+        if (isA)
+            src[q] = p.A + (size_t)min(m0 + prow, p.M - 1) * p.lda + logical * 8;
+        else
+            src[q] = p.B + (size_t)min(n0 + prow, p.N - 1) * p.ldb + logical * 8;
+        dst[q] = piece * 1024;
+    }
+    auto issue = [&](int st) {
+        char* base = lds + (st & (C::NSTAGE - 1)) * C::STAGE;
+        const int k0 = st * C::BKS;
+#pragma unroll
+        for (int q = 0; q < C::PPW; ++q) glds16(src[q] + k0, base + dst[q]);
+    };
+
+    f32x4 acc[C::FM][C::FN];
+#pragma unroll
+    for (int i = 0; i < C::FM; ++i)
+#pragma unroll
+        for (int j = 0; j < C::FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    const int nk = p.K / C::BKS;
+    for (int st = 0; st < 3 && st < nk; ++st) issue(st);
+    for (int t = 0; t < nk; ++t) {
+        pipe_wait<C>(min(2, nk - 1 - t));
+        __builtin_amdgcn_s_barrier();
+        if (t + 3 < nk) issue(t + 3);
+        const char* As = lds + (t & (C::NSTAGE - 1)) * C::STAGE;
+        const char* Bs = As + C::A_ST;
+        bf16x8 a[C::FM], b[C::FN];
+#pragma unroll
+        for (int j = 0; j < C::FN; ++j) {
+            const int row = wn * C::TN + j * 16 + li;
+            b[j] = *reinterpret_cast<const bf16x8*>(Bs + row * 64 + (pswz(row, g) << 4));
+        }
+#pragma unroll
+        for (int i = 0; i < C::FM; ++i) {
+            const int row = wm * C::TM + i * 16 + li;
+            a[i] = *reinterpret_cast<const bf16x8*>(As + row * 64 + (pswz(row, g) << 4));
+        }
+        __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+        for (int i = 0; i < C::FM; ++i)
+#pragma unroll
+            for (int j = 0; j < C::FN; ++j)
+                acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b[j], a[i], acc[i][j], 0, 0, 0);
+        __builtin_amdgcn_s_setprio(0);
+    }
+
+    // ---- epilogue: bias + act in registers -> bf16 tile in LDS -> 16-B stores (+ residual)
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < C::FN; ++j) {
+        const int nl = wn * C::TN + j * 16 + 4 * g;
+        float bv[4] = {0.f, 0.f, 0.f, 0.f};
+        if (p.bias) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) bv[r] = bf2f(p.bias[min(n0 + nl + r, p.N - 1)]);
+        }
+#pragma unroll
+        for (int i = 0; i < C::FM; ++i) {
+            const int ml = wm * C::TM + i * 16 + li;
+            bf16x4 o;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) o[r] = f2bf(apply_act(acc[i][j][r] + bv[r], ACT));
+            *reinterpret_cast<bf16x4*>(lds + ml * C::OUT_LD + nl * 2) = o;
+        }
+    }
+    __syncthreads();
+    constexpr int CPR = C::BN / 8;  // 16-B chunks per tile row
+    bf16* Cout = reinterpret_cast<bf16*>(p.C);
+    for (int c = tid; c < C::BM * CPR; c += C::NT) {
+        const int row = c / CPR, cc = c % CPR;
+        const int gr = m0 + row, gc = n0 + cc * 8;
+        if (gr >= p.M || gc >= p.N) continue;
+        u16x8 v = *reinterpret_cast<const u16x8*>(lds + row * C::OUT_LD + cc * 16);
+        if (p.res) {
+            const int rr = p.res_period ? gr % p.res_period : gr;
+            const u16x8 rv = *reinterpret_cast<const u16x8*>(p.res + (size_t)rr * p.ldr + gc);
+            bf16x8 o;
+#pragma unroll
+            for (int e = 0; e < 8; ++e) o[e] = f2bf(bits2f(v[e]) + bits2f(rv[e]));
+            *reinterpret_cast<bf16x8*>(Cout + (size_t)gr * p.ldc + gc) = o;
+        } else {
+            *reinterpret_cast<u16x8*>(Cout + (size_t)gr * p.ldc + gc) = v;
+        }
+    }
+}
+
+template <class C, int GROUP_M>
+int launch_pipe(const GemmArgs& a, hipStream_t s) {
+    const int nbm = (a.M + C::BM - 1) / C::BM, nbn = (a.N + C::BN - 1) / C::BN;
+    const dim3 grid(nbm * nbn), block(C::NT);
+    switch (a.act) {
+        case MME_ACT_GELU_TANH:
+            hipLaunchKernelGGL((gemm_pipe_kernel<C, GROUP_M, MME_ACT_GELU_TANH>), grid, block, 0, s, a);
+            break;
+        case MME_ACT_QUICK_GELU:
+            hipLaunchKernelGGL((gemm_pipe_kernel<C, GROUP_M, MME_ACT_QUICK_GELU>), grid, block, 0, s, a);
+            break;
+        case MME_ACT_GELU_ERF:
+            hipLaunchKernelGGL((gemm_pipe_kernel<C, GROUP_M, MME_ACT_GELU_ERF>), grid, block, 0, s, a);
+            break;
+        default:
+            hipLaunchKernelGGL((gemm_pipe_kernel<C, GROUP_M, MME_ACT_NONE>), grid, block, 0, s, a);
+            break;
+    }
+    return mme_check_launch("mme_gemm");
+}
+
+using Pipe256 = PCfg<256, 256, 2, 4>;
+using Pipe128 = PCfg<256, 128, 4, 2>;
+
 template <class C, int GROUP_M>
 int launch(const GemmArgs& a, hipStream_t s) {
     const int nbm = (a.M + C::BM - 1) / C::BM, nbn = (a.N + C::BN - 1) / C::BN;
@@ -144,8 +330,21 @@ extern "C" int mme_gemm(const void* A, int lda, const void* B, int ldb, void* Cp
         case 4: return launch<SqCfg, 4>(a, s);
         case 5: return launch<SqCfg, 8>(a, s);
         case 6: return launch<SmallCfg, 8>(a, s);
+        case 7: return launch_pipe<Pipe256, 4>(a, s);
+        case 8: return launch_pipe<Pipe128, 4>(a, s);
+        case 9: return launch_pipe<Pipe256, 8>(a, s);
+        case 10: return launch_pipe<Pipe128, 8>(a, s);
+        case 11: return launch_pipe<Pipe256, 1>(a, s);
         default: break;
     }
+    // production dispatch: the pipelined 256x256 kernel whenever its 16-byte
+    // vector epilogue applies (bf16 out, 16-B aligned rows); else the generic kernel
+    const bool vec_ok = !out_f32 && ldc % 8 == 0 && ((uintptr_t)Cp & 15) == 0 &&
+                        (!residual || (ldr % 8 == 0 && ((uintptr_t)residual & 15) == 0)) && N % 8 == 0;
+    if (vec_ok && (long)M * N >= 1024L * 1024) {
+        if (N >= 4096) return launch_pipe<Pipe256, 4>(a, s);
+        return launch_pipe<Pipe256, 8>(a, s);
+    }
     if ((long)M * N >= 2048L * 1024) return launch<BigCfg, 1>(a, s);
-    return launch<SmallCfg, 1>(a, s);
+    return launch<SmallCfg, 8>(a, s);
 }
