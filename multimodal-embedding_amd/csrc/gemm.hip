@@ -263,6 +263,364 @@ __global__ __launch_bounds__(C::NT, 2) void gemm_pipe_kernel(GemmArgs p) {
     }
 }
 
+// Variant with a half-stage register pipeline: the MFMAs of one half of
+// stage t run while the ds_reads of the other half (or of stage t+1) are in
+// flight, and the single barrier per stage sits between the two halves.
+template <class C, int GROUP_M, int ACT>
+__global__ __launch_bounds__(C::NT, 2) void gemm_pipe2_kernel(GemmArgs p) {
+    __shared__ __attribute__((aligned(16))) char lds[C::LDS];
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wm = wave / C::WN, wn = wave % C::WN;
+    const int g = lane >> 4, li = lane & 15;
+    constexpr int FH = C::FM / 2;
+
+    const int nbm = (p.M + C::BM - 1) / C::BM;
+    const int nbn = (p.N + C::BN - 1) / C::BN;
+    const int tile = xcd_remap(blockIdx.x, gridDim.x);
+    int bm, bn;
+    tile_coords<GROUP_M>(tile, nbm, nbn, bm, bn);
+    const int m0 = bm * C::BM, n0 = bn * C::BN;
+
+    const bf16* src[C::PPW];
+    int dst[C::PPW];
+#pragma unroll
+    for (int q = 0; q < C::PPW; ++q) {
+        const int piece = wave * C::PPW + q;
+        const bool isA = piece < C::A_PIECES;
+        const int prow = (isA ? piece : piece - C::A_PIECES) * 16 + (lane >> 2);
+        const int logical = pswz(prow, lane & 3);
+        if (isA)
+            src[q] = p.A + (size_t)min(m0 + prow, p.M - 1) * p.lda + logical * 8;
+        else
+            src[q] = p.B + (size_t)min(n0 + prow, p.N - 1) * p.ldb + logical * 8;
+        dst[q] = piece * 1024;
+    }
+    auto issue = [&](int st) {
+        char* base = lds + (st & (C::NSTAGE - 1)) * C::STAGE;
+        const int k0 = st * C::BKS;
+#pragma unroll
+        for (int q = 0; q < C::PPW; ++q) glds16(src[q] + k0, base + dst[q]);
+    };
+    // per-lane LDS byte offsets of this wave's fragments inside a stage
+    int boff[C::FN], aoff[C::FM];
+#pragma unroll
+    for (int j = 0; j < C::FN; ++j) {
+        const int row = wn * C::TN + j * 16 + li;
+        boff[j] = C::A_ST + row * 64 + (pswz(row, g) << 4);
+    }
+#pragma unroll
+    for (int i = 0; i < C::FM; ++i) {
+        const int row = wm * C::TM + i * 16 + li;
+        aoff[i] = row * 64 + (pswz(row, g) << 4);
+    }
+    auto stage_ptr = [&](int st) -> const char* { return lds + (st & (C::NSTAGE - 1)) * C::STAGE; };
+
+    f32x4 acc[C::FM][C::FN];
+#pragma unroll
+    for (int i = 0; i < C::FM; ++i)
+#pragma unroll
+        for (int j = 0; j < C::FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    bf16x8 b0[C::FN], b1[C::FN], lo0[FH], lo1[FH], hi[FH];
+    const int nk = p.K / C::BKS;
+
+    auto read_b_lo = [&](int st, bf16x8 (&b)[C::FN], bf16x8 (&lo)[FH]) {
+        const char* S = stage_ptr(st);
+#pragma unroll
+        for (int j = 0; j < C::FN; ++j) b[j] = *reinterpret_cast<const bf16x8*>(S + boff[j]);
+#pragma unroll
+        for (int i = 0; i < FH; ++i) lo[i] = *reinterpret_cast<const bf16x8*>(S + aoff[i]);
+    };
+    auto step = [&](int t, bf16x8 (&bc)[C::FN], bf16x8 (&lc)[FH], bf16x8 (&bnx)[C::FN], bf16x8 (&lnx)[FH]) {
+        const char* S = stage_ptr(t);
+#pragma unroll
+        for (int i = 0; i < FH; ++i) hi[i] = *reinterpret_cast<const bf16x8*>(S + aoff[FH + i]);
+        __builtin_amdgcn_sched_barrier(0);
+        __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+        for (int i = 0; i < FH; ++i)
+#pragma unroll
+            for (int j = 0; j < C::FN; ++j)
+                acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bc[j], lc[i], acc[i][j], 0, 0, 0);
+        __builtin_amdgcn_s_setprio(0);
+        __builtin_amdgcn_sched_barrier(0);
+        if (t + 1 < nk) {
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            pipe_wait<C>(min(2, nk - 2 - t));
+            __builtin_amdgcn_s_barrier();
+            if (t + 4 < nk) issue(t + 4);
+            read_b_lo(t + 1, bnx, lnx);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+        for (int i = 0; i < FH; ++i)
+#pragma unroll
+            for (int j = 0; j < C::FN; ++j)
+                acc[FH + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bc[j], hi[i], acc[FH + i][j], 0, 0, 0);
+        __builtin_amdgcn_s_setprio(0);
+        __builtin_amdgcn_sched_barrier(0);
+    };
+
+    for (int st = 0; st < 3 && st < nk; ++st) issue(st);
+    pipe_wait<C>(min(2, nk - 1));
+    __builtin_amdgcn_s_barrier();
+    if (3 < nk) issue(3);
+    read_b_lo(0, b0, lo0);
+    for (int t = 0; t < nk; t += 2) {
+        step(t, b0, lo0, b1, lo1);
+        if (t + 1 < nk) step(t + 1, b1, lo1, b0, lo0);
+    }
+
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < C::FN; ++j) {
+        const int nl = wn * C::TN + j * 16 + 4 * g;
+        float bv[4] = {0.f, 0.f, 0.f, 0.f};
+        if (p.bias) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) bv[r] = bf2f(p.bias[min(n0 + nl + r, p.N - 1)]);
+        }
+#pragma unroll
+        for (int i = 0; i < C::FM; ++i) {
+            const int ml = wm * C::TM + i * 16 + li;
+            bf16x4 o;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) o[r] = f2bf(apply_act(acc[i][j][r] + bv[r], ACT));
+            *reinterpret_cast<bf16x4*>(lds + ml * C::OUT_LD + nl * 2) = o;
+        }
+    }
+    __syncthreads();
+    constexpr int CPR = C::BN / 8;
+    bf16* Cout = reinterpret_cast<bf16*>(p.C);
+    for (int c = tid; c < C::BM * CPR; c += C::NT) {
+        const int row = c / CPR, cc = c % CPR;
+        const int gr = m0 + row, gc = n0 + cc * 8;
+        if (gr >= p.M || gc >= p.N) continue;
+        u16x8 v = *reinterpret_cast<const u16x8*>(lds + row * C::OUT_LD + cc * 16);
+        if (p.res) {
+            const int rr = p.res_period ? gr % p.res_period : gr;
+            const u16x8 rv = *reinterpret_cast<const u16x8*>(p.res + (size_t)rr * p.ldr + gc);
+            bf16x8 o;
+#pragma unroll
+            for (int e = 0; e < 8; ++e) o[e] = f2bf(bits2f(v[e]) + bits2f(rv[e]));
+            *reinterpret_cast<bf16x8*>(Cout + (size_t)gr * p.ldc + gc) = o;
+        } else {
+            *reinterpret_cast<u16x8*>(Cout + (size_t)gr * p.ldc + gc) = v;
+        }
+    }
+}
+
+template <class C, int GROUP_M>
+int launch_pipe2(const GemmArgs& a, hipStream_t s) {
+    const int nbm = (a.M + C::BM - 1) / C::BM, nbn = (a.N + C::BN - 1) / C::BN;
+    const dim3 grid(nbm * nbn), block(C::NT);
+    switch (a.act) {
+        case MME_ACT_GELU_TANH:
+            hipLaunchKernelGGL((gemm_pipe2_kernel<C, GROUP_M, MME_ACT_GELU_TANH>), grid, block, 0, s, a);
+            break;
+        case MME_ACT_QUICK_GELU:
+            hipLaunchKernelGGL((gemm_pipe2_kernel<C, GROUP_M, MME_ACT_QUICK_GELU>), grid, block, 0, s, a);
+            break;
+        case MME_ACT_GELU_ERF:
+            hipLaunchKernelGGL((gemm_pipe2_kernel<C, GROUP_M, MME_ACT_GELU_ERF>), grid, block, 0, s, a);
+            break;
+        default:
+            hipLaunchKernelGGL((gemm_pipe2_kernel<C, GROUP_M, MME_ACT_NONE>), grid, block, 0, s, a);
+            break;
+    }
+    return mme_check_launch("mme_gemm");
+}
+
+// Variant 3: same schedule as pipe2 with the fragment loads as inline-asm
+// ds_read_b128 and hand-counted lgkmcnt waits (hipcc's waitcnt pass drains
+// lgkmcnt(0) at the loop head otherwise, serialising reads and MFMAs).
+template <int N>
+__device__ __forceinline__ void lgkm_wait() {
+    asm volatile("s_waitcnt lgkmcnt(%0)" ::"n"(N) : "memory");
+    __builtin_amdgcn_sched_barrier(0);
+}
+template <int OFF>
+__device__ __forceinline__ void ds_read16(bf16x8& r, unsigned addr) {
+    asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(r) : "v"(addr), "n"(OFF));
+}
+
+template <class C, int GROUP_M, int ACT>
+__global__ __launch_bounds__(C::NT, 2) void gemm_pipe3_kernel(GemmArgs p) {
+    __shared__ __attribute__((aligned(16))) char lds[C::LDS];
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wm = wave / C::WN, wn = wave % C::WN;
+    const int g = lane >> 4, li = lane & 15;
+    constexpr int FH = C::FM / 2;
+    static_assert(C::FN == 4 && FH == 4, "pipe3 is written for 4 B frags and 2 x 4 A frags per wave");
+
+    const int nbm = (p.M + C::BM - 1) / C::BM;
+    const int nbn = (p.N + C::BN - 1) / C::BN;
+    const int tile = xcd_remap(blockIdx.x, gridDim.x);
+    int bm, bn;
+    tile_coords<GROUP_M>(tile, nbm, nbn, bm, bn);
+    const int m0 = bm * C::BM, n0 = bn * C::BN;
+
+    const bf16* src[C::PPW];
+    int dst[C::PPW];
+#pragma unroll
+    for (int q = 0; q < C::PPW; ++q) {
+        const int piece = wave * C::PPW + q;
+        const bool isA = piece < C::A_PIECES;
+        const int prow = (isA ? piece : piece - C::A_PIECES) * 16 + (lane >> 2);
+        const int logical = pswz(prow, lane & 3);
+        if (isA)
+            src[q] = p.A + (size_t)min(m0 + prow, p.M - 1) * p.lda + logical * 8;
+        else
+            src[q] = p.B + (size_t)min(n0 + prow, p.N - 1) * p.ldb + logical * 8;
+        dst[q] = piece * 1024;
+    }
+    auto issue = [&](int st) {
+        char* base = lds + (st & (C::NSTAGE - 1)) * C::STAGE;
+        const int k0 = st * C::BKS;
+#pragma unroll
+        for (int q = 0; q < C::PPW; ++q) glds16(src[q] + k0, base + dst[q]);
+    };
+    // lane fragment addresses inside stage 0 (the swizzle only depends on li)
+    const unsigned lds0 = (unsigned)(uintptr_t)(LDS_AS char*)lds;
+    const unsigned b_lane = lds0 + C::A_ST + (wn * C::TN + li) * 64 + (pswz(li, g) << 4);
+    const unsigned a_lane = lds0 + (wm * C::TM + li) * 64 + (pswz(li, g) << 4);
+
+    f32x4 acc[C::FM][C::FN];
+#pragma unroll
+    for (int i = 0; i < C::FM; ++i)
+#pragma unroll
+        for (int j = 0; j < C::FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    bf16x8 b0[4], b1[4], l0[4], l1[4], hi[4];
+    const int nk = p.K / C::BKS;
+
+    auto read_b_lo = [&](int st, bf16x8 (&b)[4], bf16x8 (&lo)[4]) {
+        const unsigned so = (st & (C::NSTAGE - 1)) * C::STAGE;
+        const unsigned bb = b_lane + so, aa = a_lane + so;
+        ds_read16<0>(b[0], bb);
+        ds_read16<1024>(b[1], bb);
+        ds_read16<2048>(b[2], bb);
+        ds_read16<3072>(b[3], bb);
+        ds_read16<0>(lo[0], aa);
+        ds_read16<1024>(lo[1], aa);
+        ds_read16<2048>(lo[2], aa);
+        ds_read16<3072>(lo[3], aa);
+    };
+    auto read_hi = [&](int st) {
+        const unsigned aa = a_lane + (st & (C::NSTAGE - 1)) * C::STAGE;
+        ds_read16<4096>(hi[0], aa);
+        ds_read16<5120>(hi[1], aa);
+        ds_read16<6144>(hi[2], aa);
+        ds_read16<7168>(hi[3], aa);
+    };
+    auto mma = [&](bf16x8 (&b)[4], bf16x8 (&a)[4], int ib) {
+        __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+                acc[ib + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b[j], a[i], acc[ib + i][j], 0, 0, 0);
+        __builtin_amdgcn_s_setprio(0);
+        __builtin_amdgcn_sched_barrier(0);
+    };
+    // one stage; `full` = a next stage exists and stage t+4 must be issued
+    auto step = [&](int t, bf16x8 (&bc)[4], bf16x8 (&lc)[4], bf16x8 (&bnx)[4], bf16x8 (&lnx)[4], bool full) {
+        read_hi(t);
+        lgkm_wait<4>();  // bc / lc (issued one half-stage earlier) have landed
+        mma(bc, lc, 0);
+        lgkm_wait<0>();  // hi landed; this wave no longer reads stage t
+        if (full) {
+            vm_wait<2 * C::PPW>();
+            __builtin_amdgcn_s_barrier();
+            issue(t + 4);
+            read_b_lo(t + 1, bnx, lnx);
+        } else if (t + 1 < nk) {
+            pipe_wait<C>(min(2, nk - 2 - t));
+            __builtin_amdgcn_s_barrier();
+            read_b_lo(t + 1, bnx, lnx);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        mma(bc, hi, FH);
+    };
+
+    for (int st = 0; st < 3 && st < nk; ++st) issue(st);
+    pipe_wait<C>(min(2, nk - 1));
+    __builtin_amdgcn_s_barrier();
+    if (3 < nk) issue(3);
+    read_b_lo(0, b0, l0);
+    int t = 0;
+    for (; t + 5 < nk; t += 2) {
+        step(t, b0, l0, b1, l1, true);
+        step(t + 1, b1, l1, b0, l0, true);
+    }
+    for (; t < nk; t += 2) {
+        step(t, b0, l0, b1, l1, t + 4 < nk);
+        if (t + 1 < nk) step(t + 1, b1, l1, b0, l0, t + 5 < nk);
+    }
+
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < C::FN; ++j) {
+        const int nl = wn * C::TN + j * 16 + 4 * g;
+        float bv[4] = {0.f, 0.f, 0.f, 0.f};
+        if (p.bias) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) bv[r] = bf2f(p.bias[min(n0 + nl + r, p.N - 1)]);
+        }
+#pragma unroll
+        for (int i = 0; i < C::FM; ++i) {
+            const int ml = wm * C::TM + i * 16 + li;
+            bf16x4 o;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) o[r] = f2bf(apply_act(acc[i][j][r] + bv[r], ACT));
+            *reinterpret_cast<bf16x4*>(lds + ml * C::OUT_LD + nl * 2) = o;
+        }
+    }
+    __syncthreads();
+    constexpr int CPR = C::BN / 8;
+    bf16* Cout = reinterpret_cast<bf16*>(p.C);
+    for (int c = tid; c < C::BM * CPR; c += C::NT) {
+        const int row = c / CPR, cc = c % CPR;
+        const int gr = m0 + row, gc = n0 + cc * 8;
+        if (gr >= p.M || gc >= p.N) continue;
+        u16x8 v = *reinterpret_cast<const u16x8*>(lds + row * C::OUT_LD + cc * 16);
+        if (p.res) {
+            const int rr = p.res_period ? gr % p.res_period : gr;
+            const u16x8 rv = *reinterpret_cast<const u16x8*>(p.res + (size_t)rr * p.ldr + gc);
+            bf16x8 o;
+#pragma unroll
+            for (int e = 0; e < 8; ++e) o[e] = f2bf(bits2f(v[e]) + bits2f(rv[e]));
+            *reinterpret_cast<bf16x8*>(Cout + (size_t)gr * p.ldc + gc) = o;
+        } else {
+            *reinterpret_cast<u16x8*>(Cout + (size_t)gr * p.ldc + gc) = v;
+        }
+    }
+}
+
+template <class C, int GROUP_M>
+int launch_pipe3(const GemmArgs& a, hipStream_t s) {
+    const int nbm = (a.M + C::BM - 1) / C::BM, nbn = (a.N + C::BN - 1) / C::BN;
+    const dim3 grid(nbm * nbn), block(C::NT);
+    switch (a.act) {
+        case MME_ACT_GELU_TANH:
+            hipLaunchKernelGGL((gemm_pipe3_kernel<C, GROUP_M, MME_ACT_GELU_TANH>), grid, block, 0, s, a);
+            break;
+        case MME_ACT_QUICK_GELU:
+            hipLaunchKernelGGL((gemm_pipe3_kernel<C, GROUP_M, MME_ACT_QUICK_GELU>), grid, block, 0, s, a);
+            break;
+        case MME_ACT_GELU_ERF:
+            hipLaunchKernelGGL((gemm_pipe3_kernel<C, GROUP_M, MME_ACT_GELU_ERF>), grid, block, 0, s, a);
+            break;
+        default:
+            hipLaunchKernelGGL((gemm_pipe3_kernel<C, GROUP_M, MME_ACT_NONE>), grid, block, 0, s, a);
+            break;
+    }
+    return mme_check_launch("mme_gemm");
+}
+
 template <class C, int GROUP_M>
 int launch_pipe(const GemmArgs& a, hipStream_t s) {
     const int nbm = (a.M + C::BM - 1) / C::BM, nbn = (a.N + C::BN - 1) / C::BN;
@@ -335,6 +693,10 @@ extern "C" int mme_gemm(const void* A, int lda, const void* B, int ldb, void* Cp
         case 9: return launch_pipe<Pipe256, 8>(a, s);
         case 10: return launch_pipe<Pipe128, 8>(a, s);
         case 11: return launch_pipe<Pipe256, 1>(a, s);
+        case 12: return launch_pipe2<Pipe256, 8>(a, s);
+        case 13: return launch_pipe2<Pipe256, 4>(a, s);
+        case 14: return launch_pipe3<Pipe256, 8>(a, s);
+        case 15: return launch_pipe3<Pipe256, 4>(a, s);
         default: break;
     }
     // production dispatch: the pipelined 256x256 kernel whenever its 16-byte
