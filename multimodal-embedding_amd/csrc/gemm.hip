@@ -704,8 +704,7 @@ extern "C" int mme_gemm(const void* A, int lda, const void* B, int ldb, void* Cp
     const bool vec_ok = !out_f32 && ldc % 8 == 0 && ((uintptr_t)Cp & 15) == 0 &&
                         (!residual || (ldr % 8 == 0 && ((uintptr_t)residual & 15) == 0)) && N % 8 == 0;
     if (vec_ok && (long)M * N >= 1024L * 1024) {
-        if (N >= 4096) return launch_pipe<Pipe256, 4>(a, s);
-        return launch_pipe<Pipe256, 8>(a, s);
+        return launch_pipe3<Pipe256, 4>(a, s);
     }
     if ((long)M * N >= 2048L * 1024) return launch<BigCfg, 1>(a, s);
     return launch<SmallCfg, 8>(a, s);

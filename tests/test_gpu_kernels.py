@@ -27,7 +27,9 @@ def rnd(*shape, scale=1.0, gen=None, device="cuda"):
 
 
 @pytest.mark.parametrize("M,N,K", [(1, 128, 64), (100, 200, 128), (1458, 1152, 1152), (300, 64, 640),
-                                   (4096, 4352, 1152), (2048, 3456, 1152), (517, 1152, 4352), (33, 8, 64)])
+                                   (4096, 4352, 1152), (2048, 3456, 1152), (517, 1152, 4352), (33, 8, 64),
+                                   # pipelined-kernel stage-count edge cases (nk = K/32 = 2, 4, 6, 10)
+                                   (2048, 1024, 64), (2048, 1024, 128), (1500, 1024, 192), (2048, 1536, 320)])
 @pytest.mark.parametrize("act", [0, 1, 2, 3])
 def test_gemm_bias_act(cuda, M, N, K, act):
     g = torch.Generator(device="cuda").manual_seed(M * 7 + N + act)
