@@ -1,6 +1,6 @@
 // Fused multi-head attention for the ViT / text encoders (flash-style, gfx950).
 //
-// softmax(Q K^T * scale + mask) V for one (batch, head, 64-query block) per
+// softmax(Q K^T * scale + mask) V for one (batch, head, 128-query block) per
 // workgroup, streaming 64-key K/V tiles through LDS with online softmax —
 // replaces eager/SDPA attention of SiglipAttention / CLIPAttention
 // (TF:models/siglip/modeling_siglip.py:228-247,273-306).
@@ -16,8 +16,11 @@
 //   * the V^T operand is read from the row-major V tile with
 //     ds_read_b64_tr_b16 (hardware transpose), V rows padded to 80 elements
 //     (160 B) which makes the transposed reads bank-conflict-free;
-//   * head dims 72 and 80 run as 2 x K32 + 1 x K16 MFMA steps (padding 72 to
-//     80, not 96); the O^T accumulators cover 5 d-tiles of 16.
+//   * head dims 72 and 80 run as 3 x K32 MFMA steps over a zero-padded 96-deep
+//     reduction (same-shape accumulation chains only); the O^T accumulators
+//     cover 5 d-tiles of 16 (80 columns).
+//   * 4 waves x 32 query rows per workgroup: the K and V^T fragments read
+//     from LDS feed two query tiles each.
 //   * K/V tiles are double-buffered through registers: the global loads of
 //     tile t+1 are issued before the MFMAs of tile t and written to the other
 //     LDS buffer afterwards.
@@ -25,92 +28,106 @@
 
 namespace {
 
-typedef short s16x8 __attribute__((ext_vector_type(8)));
 
 struct AttnArgs {
     const bf16* qkv;
     bf16* out;
     const int32_t* seq_lens;
-    int ld, ldo, T, H, hd, causal;
+    int ld, ldo, T, H, hd, causal;  // hd is also the kernel's template parameter
     float scale_log2;
 };
 
-template <int HDP>
-__global__ __launch_bounds__(256) void attn_fwd_kernel(AttnArgs a) {
+template <int HD>
+__global__ __launch_bounds__(256, 2) void attn_fwd_kernel(AttnArgs a) {
+    // QK^T reduction depth covered by 16x16x32 steps: 64, or 96 for head dims
+    // 72/80 zero-padded. Only same-shape MFMA accumulation chains are used: a
+    // 16x16x16 tail step chained on a 16x16x32 result was observed to be
+    // scheduled without the wait states it needs (wrong scores on gfx950).
+    constexpr int HDP = HD == 64 ? 64 : 96;
+    constexpr int NKS = HDP / 32;    // K32 steps
     constexpr int KS = HDP + 8;      // K LDS row stride (elements)
     constexpr int VS = 80;           // V LDS row stride (elements): conflict-free tr reads
-    constexpr int NCH_K = HDP / 8;   // 16-B chunks of a K row kept in LDS
-    constexpr int NCH_V = VS / 8;
-    constexpr int NDT = HDP / 16;    // output d-tiles of 16
-    constexpr int NCHUNK = 64 * (NCH_K + NCH_V);
-    constexpr int CPT = (NCHUNK + 255) / 256;
+    constexpr int NCHL = HD / 8;     // 16-B chunks loaded per K / V row
+    constexpr int NDT = (HD + 15) / 16;  // output d-tiles of 16
+    constexpr int QW = 32;           // query rows per wave (2 MFMA column tiles)
     __shared__ __attribute__((aligned(16))) bf16 Ks[2][64 * KS];
     __shared__ __attribute__((aligned(16))) bf16 Vs[2][64 * VS];
 
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int g = lane >> 4, li = lane & 15;
     const int b = blockIdx.z, h = blockIdx.y;
-    const int T = a.T, hd = a.hd, D = a.H * a.hd;
+    const int T = a.T, D = a.H * HD;
     const bf16* base = a.qkv + (long)b * T * a.ld;
-    const int q = blockIdx.x * 64 + wave * 16 + li;
+    const int qw0 = blockIdx.x * (4 * QW) + wave * QW;  // first query row of this wave
     const int Tk = a.seq_lens ? a.seq_lens[b] : T;
+    const float c = a.scale_log2;
 
-    // Q^T fragments (B operand): lane holds Q[q][32ks + 8g + j]
-    bf16x8 qf[2];
-    s16x4 qt = {0, 0, 0, 0};
-    {
-        const bf16* qrow = base + (long)min(q, T - 1) * a.ld + h * hd;
+    // zero the padding columns (K: HD..HDP, V: HD..VS) of both buffers once;
+    // the tile loads below never write them
+    for (int i = tid; i < 2 * 64; i += 256) {
+        bf16* kr = &Ks[i >> 6][(i & 63) * KS];
+        for (int col = HD; col < HDP; col += 8) *reinterpret_cast<u16x8*>(kr + col) = u16x8{0, 0, 0, 0, 0, 0, 0, 0};
+        bf16* vr = &Vs[i >> 6][(i & 63) * VS];
+        for (int col = HD; col < VS; col += 8) *reinterpret_cast<u16x8*>(vr + col) = u16x8{0, 0, 0, 0, 0, 0, 0, 0};
+    }
+
+    // Q^T fragments (B operand) for the wave's two 16-row query tiles; columns >= HD are zero
+    bf16x8 qf[2][NKS];
 #pragma unroll
-        for (int ks = 0; ks < 2; ++ks) qf[ks] = *reinterpret_cast<const bf16x8*>(qrow + ks * 32 + 8 * g);
-        if constexpr (HDP == 80) {
-            if (64 + 4 * g < hd) qt = *reinterpret_cast<const s16x4*>(qrow + 64 + 4 * g);
+    for (int u = 0; u < 2; ++u) {
+        const bf16* qrow = base + (long)min(qw0 + u * 16 + li, T - 1) * a.ld + h * HD;
+#pragma unroll
+        for (int ks = 0; ks < NKS; ++ks) {
+            const int col = ks * 32 + 8 * g;
+            if (col < HD)
+                qf[u][ks] = *reinterpret_cast<const bf16x8*>(qrow + col);
+            else
+                qf[u][ks] = bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
         }
     }
 
-    int nkt = (T + 63) / 64;
-    if (a.causal) nkt = min(nkt, (min(T, (int)blockIdx.x * 64 + 64) + 63) / 64);
+    int nkt = (Tk + 63) / 64;
+    if (a.causal) nkt = min(nkt, (min(T, (int)blockIdx.x * 4 * QW + 4 * QW) + 63) / 64);
 
-    u16x8 pre[CPT];
+    // K/V tile staging through registers; rows beyond T are clamped (finite
+    // values whose scores are masked / weights are 0). K and V chunks are
+    // distributed by separate loops so no lane branches on the tensor.
+    constexpr int NCH = 64 * NCHL;              // chunks per K (or V) tile
+    constexpr int CPT1 = (NCH + 255) / 256;
+    u16x8 pk[CPT1], pv[CPT1];
     auto load_tile = [&](int t) {
 #pragma unroll
-        for (int i = 0; i < CPT; ++i) {
-            const int c = tid + i * 256;
-            u16x8 v = {0, 0, 0, 0, 0, 0, 0, 0};
-            if (c < NCHUNK) {
-                const bool isk = c < 64 * NCH_K;
-                const int cc = isk ? c : c - 64 * NCH_K;
-                const int nch = isk ? NCH_K : NCH_V;
-                const int row = cc / nch, ch = cc % nch;
-                const int key = t * 64 + row;
-                if (key < T && ch * 8 < hd)
-                    v = *reinterpret_cast<const u16x8*>(base + (long)key * a.ld + (isk ? D : 2 * D) + h * hd + ch * 8);
+        for (int i = 0; i < CPT1; ++i) {
+            const int cidx = tid + i * 256;
+            if (NCH % 256 == 0 || cidx < NCH) {
+                const int row = cidx / NCHL, ch = cidx % NCHL;
+                const bf16* r = base + (long)min(t * 64 + row, T - 1) * a.ld + h * HD + ch * 8;
+                pk[i] = *reinterpret_cast<const u16x8*>(r + D);
+                pv[i] = *reinterpret_cast<const u16x8*>(r + 2 * D);
             }
-            pre[i] = v;
         }
     };
     auto store_tile = [&](int buf) {
 #pragma unroll
-        for (int i = 0; i < CPT; ++i) {
-            const int c = tid + i * 256;
-            if (c < NCHUNK) {
-                if (c < 64 * NCH_K) {
-                    const int row = c / NCH_K, ch = c % NCH_K;
-                    *reinterpret_cast<u16x8*>(&Ks[buf][row * KS + ch * 8]) = pre[i];
-                } else {
-                    const int cc = c - 64 * NCH_K;
-                    const int row = cc / NCH_V, ch = cc % NCH_V;
-                    *reinterpret_cast<u16x8*>(&Vs[buf][row * VS + ch * 8]) = pre[i];
-                }
+        for (int i = 0; i < CPT1; ++i) {
+            const int cidx = tid + i * 256;
+            if (NCH % 256 == 0 || cidx < NCH) {
+                const int row = cidx / NCHL, ch = cidx % NCHL;
+                *reinterpret_cast<u16x8*>(&Ks[buf][row * KS + ch * 8]) = pk[i];
+                *reinterpret_cast<u16x8*>(&Vs[buf][row * VS + ch * 8]) = pv[i];
             }
         }
     };
 
-    f32x4 o[NDT];
+    f32x4 o[2][NDT];
 #pragma unroll
-    for (int i = 0; i < NDT; ++i) o[i] = f32x4{0.f, 0.f, 0.f, 0.f};
-    float m = -1e30f, lsum = 0.f;
+    for (int u = 0; u < 2; ++u)
+#pragma unroll
+        for (int i = 0; i < NDT; ++i) o[u][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+    float m[2] = {-1e30f, -1e30f}, lsum[2] = {0.f, 0.f};  // running max in raw-score units
 
     load_tile(0);
+    __syncthreads();  // padding zeroes visible before the first tile overwrites its rows
     store_tile(0);
     __syncthreads();
     for (int t = 0; t < nkt; ++t) {
@@ -119,70 +136,82 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(AttnArgs a) {
         const bf16* Kb = Ks[buf];
         const bf16* Vb = Vs[buf];
 
-        // S^T[key][q] for 4 sub-tiles of 16 keys
-        f32x4 s[4];
+        // S^T[key][q] for 4 sub-tiles of 16 keys x 2 query tiles; K fragments shared
+        f32x4 sc[2][4];
 #pragma unroll
         for (int kt = 0; kt < 4; ++kt) {
-            s[kt] = f32x4{0.f, 0.f, 0.f, 0.f};
             const bf16* krow = Kb + (kt * 16 + li) * KS;
+            bf16x8 kf[NKS];
 #pragma unroll
-            for (int ks = 0; ks < 2; ++ks) {
-                const bf16x8 ka = *reinterpret_cast<const bf16x8*>(krow + ks * 32 + 8 * g);
-                s[kt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ka, qf[ks], s[kt], 0, 0, 0);
-            }
-            if constexpr (HDP == 80) {
-                const s16x4 ka = *reinterpret_cast<const s16x4*>(krow + 64 + 4 * g);
-                s[kt] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(ka, qt, s[kt], 0, 0, 0);
+            for (int ks = 0; ks < NKS; ++ks) kf[ks] = *reinterpret_cast<const bf16x8*>(krow + ks * 32 + 8 * g);
+#pragma unroll
+            for (int u = 0; u < 2; ++u) {
+                f32x4 z = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+                for (int ks = 0; ks < NKS; ++ks) z = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf[ks], qf[u][ks], z, 0, 0, 0);
+                sc[u][kt] = z;
             }
         }
 
-        // online softmax over this tile (log2 domain)
-        float mloc = -1e30f;
+        // masking only where the tile crosses the key length or the causal diagonal
+        if ((t * 64 + 64 > Tk) || (a.causal && t * 64 + 63 > qw0)) {
 #pragma unroll
-        for (int kt = 0; kt < 4; ++kt)
+            for (int u = 0; u < 2; ++u) {
+                const int q = qw0 + u * 16 + li;
+                const int lim = a.causal ? min(Tk, q + 1) : Tk;  // valid keys: key < lim
 #pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                const int key = t * 64 + kt * 16 + 4 * g + r;
-                const bool ok = key < Tk && (!a.causal || key <= q);
-                const float x = ok ? s[kt][r] * a.scale_log2 : -INFINITY;
-                s[kt][r] = x;
-                mloc = fmaxf(mloc, x);
+                for (int kt = 0; kt < 4; ++kt)
+#pragma unroll
+                    for (int r = 0; r < 4; ++r)
+                        if (t * 64 + kt * 16 + 4 * g + r >= lim) sc[u][kt][r] = -INFINITY;
             }
-        mloc = fmaxf(mloc, __shfl_xor(mloc, 16, 64));
-        mloc = fmaxf(mloc, __shfl_xor(mloc, 32, 64));
-        const float mnew = fmaxf(m, mloc);
-        const float alpha = exp2f(m - mnew);
-        m = mnew;
-        float psum = 0.f;
-#pragma unroll
-        for (int kt = 0; kt < 4; ++kt)
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                const float p = exp2f(s[kt][r] - mnew);
-                s[kt][r] = p;
-                psum += p;
-            }
-        lsum = lsum * alpha + psum;
-#pragma unroll
-        for (int i = 0; i < NDT; ++i) o[i] *= alpha;
+        }
 
-        // O^T[d][q] += V^T[d][key] . P^T[key][q]
+        // online softmax (log2 domain, scale folded into one FMA per score)
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+            float mloc = fmaxf(fmaxf(sc[u][0][0], sc[u][0][1]), fmaxf(sc[u][0][2], sc[u][0][3]));
+#pragma unroll
+            for (int kt = 1; kt < 4; ++kt)
+                mloc = fmaxf(mloc, fmaxf(fmaxf(sc[u][kt][0], sc[u][kt][1]), fmaxf(sc[u][kt][2], sc[u][kt][3])));
+            mloc = fmaxf(mloc, __shfl_xor(mloc, 16, 64));
+            mloc = fmaxf(mloc, __shfl_xor(mloc, 32, 64));
+            const float mnew = fmaxf(m[u], mloc);
+            const float alpha = __builtin_amdgcn_exp2f((m[u] - mnew) * c);
+            m[u] = mnew;
+            const float mc = mnew * c;
+            float psum = 0.f;
+#pragma unroll
+            for (int kt = 0; kt < 4; ++kt)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const float pv = __builtin_amdgcn_exp2f(sc[u][kt][r] * c - mc);
+                    sc[u][kt][r] = pv;
+                    psum += pv;
+                }
+            lsum[u] = lsum[u] * alpha + psum;
+#pragma unroll
+            for (int i = 0; i < NDT; ++i) o[u][i] *= alpha;
+        }
+
+        // O^T[d][q] += V^T[d][key] . P^T[key][q]; V^T fragments shared by both query tiles
 #pragma unroll
         for (int hh = 0; hh < 2; ++hh) {
-            bf16x8 pb;
+            bf16x8 pb[2];
 #pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                pb[j] = f2bf(s[2 * hh][j]);
-                pb[4 + j] = f2bf(s[2 * hh + 1][j]);
-            }
+            for (int u = 0; u < 2; ++u)
+                pb[u] = __builtin_convertvector(__builtin_shufflevector(sc[u][2 * hh], sc[u][2 * hh + 1], 0, 1, 2, 3,
+                                                                        4, 5, 6, 7), bf16x8);
             const int r1 = 32 * hh + 4 * g + (li >> 2);
 #pragma unroll
             for (int dt = 0; dt < NDT; ++dt) {
                 const int col = dt * 16 + 4 * (li & 3);
                 const s16x4 v0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS_AS s16x4*)(Vb + r1 * VS + col));
                 const s16x4 v1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS_AS s16x4*)(Vb + (r1 + 16) * VS + col));
-                const s16x8 vv = __builtin_shufflevector(v0, v1, 0, 1, 2, 3, 4, 5, 6, 7);
-                o[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, vv), pb, o[dt], 0, 0, 0);
+                const bf16x8 vv = __builtin_bit_cast(bf16x8, __builtin_shufflevector(v0, v1, 0, 1, 2, 3, 4, 5, 6, 7));
+#pragma unroll
+                for (int u = 0; u < 2; ++u)
+                    o[u][dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vv, pb[u], o[u][dt], 0, 0, 0);
             }
         }
 
@@ -190,19 +219,23 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(AttnArgs a) {
         __syncthreads();
     }
 
-    float ltot = lsum + __shfl_xor(lsum, 16, 64);
-    ltot += __shfl_xor(ltot, 32, 64);
-    const float inv = 1.0f / ltot;
-    if (q < T) {
-        bf16* orow = a.out + ((long)b * T + q) * a.ldo + h * hd;
 #pragma unroll
-        for (int dt = 0; dt < NDT; ++dt) {
-            const int d0 = dt * 16 + 4 * g;
-            if (d0 < hd) {
-                bf16x4 v;
+    for (int u = 0; u < 2; ++u) {
+        float ltot = lsum[u] + __shfl_xor(lsum[u], 16, 64);
+        ltot += __shfl_xor(ltot, 32, 64);
+        const float inv = 1.0f / ltot;
+        const int q = qw0 + u * 16 + li;
+        if (q < T) {
+            bf16* orow = a.out + ((long)b * T + q) * a.ldo + h * HD;
 #pragma unroll
-                for (int r = 0; r < 4; ++r) v[r] = f2bf(o[dt][r] * inv);
-                *reinterpret_cast<bf16x4*>(orow + d0) = v;
+            for (int dt = 0; dt < NDT; ++dt) {
+                const int d0 = dt * 16 + 4 * g;
+                if (d0 < HD) {
+                    bf16x4 v;
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) v[r] = f2bf(o[u][dt][r] * inv);
+                    *reinterpret_cast<bf16x4*>(orow + d0) = v;
+                }
             }
         }
     }
@@ -282,10 +315,12 @@ extern "C" int mme_attention(const void* qkv, int ld_qkv, void* out, int ld_out,
     MME_REQUIRE(((uintptr_t)qkv & 15) == 0 && ((uintptr_t)out & 7) == 0, "mme_attention: misaligned");
     if (B == 0) return MME_OK;
     AttnArgs a{(const bf16*)qkv, (bf16*)out, seq_lens, ld_qkv, ld_out, T, H, hd, causal ? 1 : 0,
-               scale * 1.4426950408889634f};
-    dim3 grid(cdiv(T, 64), H, B);
+               scale * 1.4426950408889634f};  // exp(x*scale) = exp2(x*scale*log2 e)
+    dim3 grid(cdiv(T, 128), H, B);
     if (hd == 64)
         hipLaunchKernelGGL(attn_fwd_kernel<64>, grid, dim3(256), 0, as_stream(stream), a);
+    else if (hd == 72)
+        hipLaunchKernelGGL(attn_fwd_kernel<72>, grid, dim3(256), 0, as_stream(stream), a);
     else
         hipLaunchKernelGGL(attn_fwd_kernel<80>, grid, dim3(256), 0, as_stream(stream), a);
     return mme_check_launch("mme_attention");

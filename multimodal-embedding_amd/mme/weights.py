@@ -243,6 +243,54 @@ def random_state_dict(spec: ModelSpec, seed: int = 0, device="cuda") -> Dict[str
     return sd
 
 
+def hf_param_shapes(spec: ModelSpec) -> Dict[str, tuple]:
+    """Name -> shape of every learned tensor of the HF SiglipModel / CLIPModel at
+    this architecture (the state dict from_hf_state_dict consumes)."""
+    sh: Dict[str, tuple] = {}
+    v, t = spec.vision, spec.text
+
+    def layers(prefix, cfg):
+        d, I = cfg.hidden, cfg.intermediate
+        for i in range(cfg.layers):
+            p = f"{prefix}.encoder.layers.{i}."
+            for n in ("layer_norm1", "layer_norm2"):
+                sh[p + n + ".weight"] = (d,)
+                sh[p + n + ".bias"] = (d,)
+            for n in ("q_proj", "k_proj", "v_proj", "out_proj"):
+                sh[p + "self_attn." + n + ".weight"] = (d, d)
+                sh[p + "self_attn." + n + ".bias"] = (d,)
+            sh[p + "mlp.fc1.weight"], sh[p + "mlp.fc1.bias"] = (I, d), (I,)
+            sh[p + "mlp.fc2.weight"], sh[p + "mlp.fc2.bias"] = (d, I), (d,)
+
+    d = v.hidden
+    sh["vision_model.embeddings.patch_embedding.weight"] = (d, 3, v.patch, v.patch)
+    T = v.num_patches + (1 if spec.family == "clip" else 0)
+    sh["vision_model.embeddings.position_embedding.weight"] = (T, d)
+    layers("vision_model", v)
+    sh["vision_model.post_layernorm.weight"] = sh["vision_model.post_layernorm.bias"] = (d,)
+    sh["text_model.embeddings.token_embedding.weight"] = (t.vocab, t.hidden)
+    sh["text_model.embeddings.position_embedding.weight"] = (t.max_pos, t.hidden)
+    layers("text_model", t)
+    sh["text_model.final_layer_norm.weight"] = sh["text_model.final_layer_norm.bias"] = (t.hidden,)
+    if spec.family == "siglip":
+        sh["vision_model.embeddings.patch_embedding.bias"] = (d,)
+        sh["vision_model.head.probe"] = (1, 1, d)
+        sh["vision_model.head.attention.in_proj_weight"] = (3 * d, d)
+        sh["vision_model.head.attention.in_proj_bias"] = (3 * d,)
+        sh["vision_model.head.attention.out_proj.weight"] = (d, d)
+        sh["vision_model.head.attention.out_proj.bias"] = (d,)
+        sh["vision_model.head.layernorm.weight"] = sh["vision_model.head.layernorm.bias"] = (d,)
+        sh["vision_model.head.mlp.fc1.weight"], sh["vision_model.head.mlp.fc1.bias"] = (v.intermediate, d), (v.intermediate,)
+        sh["vision_model.head.mlp.fc2.weight"], sh["vision_model.head.mlp.fc2.bias"] = (d, v.intermediate), (d,)
+        sh["text_model.head.weight"], sh["text_model.head.bias"] = (spec.proj_dim, t.hidden), (spec.proj_dim,)
+    else:
+        sh["vision_model.embeddings.class_embedding"] = (d,)
+        sh["vision_model.pre_layrnorm.weight"] = sh["vision_model.pre_layrnorm.bias"] = (d,)
+        sh["visual_projection.weight"] = (spec.proj_dim, d)
+        sh["text_projection.weight"] = (spec.proj_dim, t.hidden)
+    return sh
+
+
 def load_safetensors(path: str) -> Dict[str, torch.Tensor]:
     from safetensors.torch import load_file  # executes nothing from the file
     return load_file(path)
