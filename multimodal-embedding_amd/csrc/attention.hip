@@ -55,10 +55,20 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(AttnArgs a) {
 
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int g = lane >> 4, li = lane & 15;
-    const int b = blockIdx.z, h = blockIdx.y;
+    // 1-D grid, XCD-aware: blocks b and b+8 share an XCD (round-robin dispatch), so
+    // remap ids so each XCD runs a contiguous range of (batch, head, q-block)
+    // tuples -> the q-blocks of one head re-read its K/V from the same L2.
+    const int nqb = (a.T + 4 * QW - 1) / (4 * QW);
+    int id;
+    {
+        const int bid = blockIdx.x, nwg = gridDim.x;
+        const int xcd = bid & 7, loc = bid >> 3, q8 = nwg >> 3, r8 = nwg & 7;
+        id = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + loc;
+    }
+    const int qb = id % nqb, h = (id / nqb) % a.H, b = id / (nqb * a.H);
     const int T = a.T, D = a.H * HD;
     const bf16* base = a.qkv + (long)b * T * a.ld;
-    const int qw0 = blockIdx.x * (4 * QW) + wave * QW;  // first query row of this wave
+    const int qw0 = qb * (4 * QW) + wave * QW;  // first query row of this wave
     const int Tk = a.seq_lens ? a.seq_lens[b] : T;
     const float c = a.scale_log2;
 
@@ -87,7 +97,7 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(AttnArgs a) {
     }
 
     int nkt = (Tk + 63) / 64;
-    if (a.causal) nkt = min(nkt, (min(T, (int)blockIdx.x * 4 * QW + 4 * QW) + 63) / 64);
+    if (a.causal) nkt = min(nkt, (min(T, qb * 4 * QW + 4 * QW) + 63) / 64);
 
     // K/V tile staging through registers; rows beyond T are clamped (finite
     // values whose scores are masked / weights are 0). K and V chunks are
@@ -316,7 +326,7 @@ extern "C" int mme_attention(const void* qkv, int ld_qkv, void* out, int ld_out,
     if (B == 0) return MME_OK;
     AttnArgs a{(const bf16*)qkv, (bf16*)out, seq_lens, ld_qkv, ld_out, T, H, hd, causal ? 1 : 0,
                scale * 1.4426950408889634f};  // exp(x*scale) = exp2(x*scale*log2 e)
-    dim3 grid(cdiv(T, 128), H, B);
+    const dim3 grid(cdiv(T, 128) * H * B);
     if (hd == 64)
         hipLaunchKernelGGL(attn_fwd_kernel<64>, grid, dim3(256), 0, as_stream(stream), a);
     else if (hd == 72)

@@ -126,12 +126,12 @@ __device__ __forceinline__ void vm_wait() {
 
 __device__ __forceinline__ int pswz(int row, int chunk) { return chunk ^ (3 * ((row >> 3) & 1)); }
 
-template <int BM_, int BN_, int WM_, int WN_>
+template <int BM_, int BN_, int WM_, int WN_, int NSTAGE_ = 4>
 struct PCfg {
     static constexpr int BM = BM_, BN = BN_, WM = WM_, WN = WN_;
     static constexpr int NW = WM * WN, NT = NW * 64;
     static constexpr int TM = BM / WM, TN = BN / WN, FM = TM / 16, FN = TN / 16;
-    static constexpr int BKS = 32, NSTAGE = 4;
+    static constexpr int BKS = 32, NSTAGE = NSTAGE_;
     static constexpr int A_ST = BM * BKS * 2, B_ST = BN * BKS * 2, STAGE = A_ST + B_ST;
     static constexpr int A_PIECES = A_ST / 1024, PIECES = STAGE / 1024;
     static constexpr int PPW = PIECES / NW;  // DMA pieces per wave per stage
@@ -477,8 +477,9 @@ __global__ __launch_bounds__(C::NT, 2) void gemm_pipe3_kernel(GemmArgs p) {
             src[q] = p.B + (size_t)min(n0 + prow, p.N - 1) * p.ldb + logical * 8;
         dst[q] = piece * 1024;
     }
+    constexpr int PF = C::NSTAGE - 1;  // stages in flight ahead of the one being read
     auto issue = [&](int st) {
-        char* base = lds + (st & (C::NSTAGE - 1)) * C::STAGE;
+        char* base = lds + (st % C::NSTAGE) * C::STAGE;
         const int k0 = st * C::BKS;
 #pragma unroll
         for (int q = 0; q < C::PPW; ++q) glds16(src[q] + k0, base + dst[q]);
@@ -498,7 +499,7 @@ __global__ __launch_bounds__(C::NT, 2) void gemm_pipe3_kernel(GemmArgs p) {
     const int nk = p.K / C::BKS;
 
     auto read_b_lo = [&](int st, bf16x8 (&b)[4], bf16x8 (&lo)[4]) {
-        const unsigned so = (st & (C::NSTAGE - 1)) * C::STAGE;
+        const unsigned so = (st % C::NSTAGE) * C::STAGE;
         const unsigned bb = b_lane + so, aa = a_lane + so;
         ds_read16<0>(b[0], bb);
         ds_read16<1024>(b[1], bb);
@@ -510,7 +511,7 @@ __global__ __launch_bounds__(C::NT, 2) void gemm_pipe3_kernel(GemmArgs p) {
         ds_read16<3072>(lo[3], aa);
     };
     auto read_hi = [&](int st) {
-        const unsigned aa = a_lane + (st & (C::NSTAGE - 1)) * C::STAGE;
+        const unsigned aa = a_lane + (st % C::NSTAGE) * C::STAGE;
         ds_read16<4096>(hi[0], aa);
         ds_read16<5120>(hi[1], aa);
         ds_read16<6144>(hi[2], aa);
@@ -526,19 +527,24 @@ __global__ __launch_bounds__(C::NT, 2) void gemm_pipe3_kernel(GemmArgs p) {
         __builtin_amdgcn_s_setprio(0);
         __builtin_amdgcn_sched_barrier(0);
     };
-    // one stage; `full` = a next stage exists and stage t+4 must be issued
+    // one stage; `full` = a next stage exists and stage t+NSTAGE must be issued
     auto step = [&](int t, bf16x8 (&bc)[4], bf16x8 (&lc)[4], bf16x8 (&bnx)[4], bf16x8 (&lnx)[4], bool full) {
         read_hi(t);
         lgkm_wait<4>();  // bc / lc (issued one half-stage earlier) have landed
         mma(bc, lc, 0);
         lgkm_wait<0>();  // hi landed; this wave no longer reads stage t
         if (full) {
-            vm_wait<2 * C::PPW>();
+            vm_wait<(PF - 1) * C::PPW>();
             __builtin_amdgcn_s_barrier();
-            issue(t + 4);
+            issue(t + C::NSTAGE);
             read_b_lo(t + 1, bnx, lnx);
         } else if (t + 1 < nk) {
-            pipe_wait<C>(min(2, nk - 2 - t));
+            // stages t+2 .. min(nk-1, t+PF) may still be in flight
+            const int rem = min(PF - 1, nk - 2 - t);
+            if (rem >= 3) vm_wait<3 * C::PPW>();
+            else if (rem == 2) vm_wait<2 * C::PPW>();
+            else if (rem == 1) vm_wait<C::PPW>();
+            else vm_wait<0>();
             __builtin_amdgcn_s_barrier();
             read_b_lo(t + 1, bnx, lnx);
         }
@@ -546,19 +552,26 @@ __global__ __launch_bounds__(C::NT, 2) void gemm_pipe3_kernel(GemmArgs p) {
         mma(bc, hi, FH);
     };
 
-    for (int st = 0; st < 3 && st < nk; ++st) issue(st);
-    pipe_wait<C>(min(2, nk - 1));
+    static_assert(PF >= 3 && PF <= 4, "pipe3 is written for 4 or 5 LDS stages");
+    for (int st = 0; st < PF && st < nk; ++st) issue(st);
+    {
+        const int rem = min(PF - 1, nk - 1);  // stages beyond 0 in flight
+        if (rem >= 3) vm_wait<3 * C::PPW>();
+        else if (rem == 2) vm_wait<2 * C::PPW>();
+        else if (rem == 1) vm_wait<C::PPW>();
+        else vm_wait<0>();
+    }
     __builtin_amdgcn_s_barrier();
-    if (3 < nk) issue(3);
+    if (PF < nk) issue(PF);
     read_b_lo(0, b0, l0);
     int t = 0;
-    for (; t + 5 < nk; t += 2) {
+    for (; t + C::NSTAGE + 1 < nk; t += 2) {
         step(t, b0, l0, b1, l1, true);
         step(t + 1, b1, l1, b0, l0, true);
     }
     for (; t < nk; t += 2) {
-        step(t, b0, l0, b1, l1, t + 4 < nk);
-        if (t + 1 < nk) step(t + 1, b1, l1, b0, l0, t + 5 < nk);
+        step(t, b0, l0, b1, l1, t + C::NSTAGE < nk);
+        if (t + 1 < nk) step(t + 1, b1, l1, b0, l0, t + 1 + C::NSTAGE < nk);
     }
 
     __syncthreads();
@@ -643,6 +656,7 @@ int launch_pipe(const GemmArgs& a, hipStream_t s) {
 }
 
 using Pipe256 = PCfg<256, 256, 2, 4>;
+using Pipe256s5 = PCfg<256, 256, 2, 4, 5>;
 using Pipe128 = PCfg<256, 128, 4, 2>;
 
 template <class C, int GROUP_M>
@@ -697,6 +711,8 @@ extern "C" int mme_gemm(const void* A, int lda, const void* B, int ldb, void* Cp
         case 13: return launch_pipe2<Pipe256, 4>(a, s);
         case 14: return launch_pipe3<Pipe256, 8>(a, s);
         case 15: return launch_pipe3<Pipe256, 4>(a, s);
+        case 16: return launch_pipe3<Pipe256s5, 4>(a, s);
+        case 17: return launch_pipe3<Pipe256s5, 8>(a, s);
         default: break;
     }
     // production dispatch: the pipelined 256x256 kernel whenever its 16-byte
