@@ -446,7 +446,7 @@ __device__ __forceinline__ void ds_read16(bf16x8& r, unsigned addr) {
     asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(r) : "v"(addr), "n"(OFF));
 }
 
-template <class C, int GROUP_M, int ACT>
+template <class C, int GROUP_M, int ACT, int PRIO = 0>
 __global__ __launch_bounds__(C::NT, 2) void gemm_pipe3_kernel(GemmArgs p) {
     __shared__ __attribute__((aligned(16))) char lds[C::LDS];
     const int tid = threadIdx.x, lane = tid & 63;
@@ -518,15 +518,16 @@ __global__ __launch_bounds__(C::NT, 2) void gemm_pipe3_kernel(GemmArgs p) {
         ds_read16<7168>(hi[3], aa);
     };
     auto mma = [&](bf16x8 (&b)[4], bf16x8 (&a)[4], int ib) {
-        __builtin_amdgcn_s_setprio(1);
+        if (PRIO == 0) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
         for (int i = 0; i < 4; ++i)
 #pragma unroll
             for (int j = 0; j < 4; ++j)
                 acc[ib + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b[j], a[i], acc[ib + i][j], 0, 0, 0);
-        __builtin_amdgcn_s_setprio(0);
+        if (PRIO == 0) __builtin_amdgcn_s_setprio(0);
         __builtin_amdgcn_sched_barrier(0);
     };
+    if (PRIO == 1 && __builtin_amdgcn_readfirstlane(tid) >= C::NT / 2) __builtin_amdgcn_s_setprio(1);
     // one stage; `full` = a next stage exists and stage t+NSTAGE must be issued
     auto step = [&](int t, bf16x8 (&bc)[4], bf16x8 (&lc)[4], bf16x8 (&bnx)[4], bf16x8 (&lnx)[4], bool full) {
         read_hi(t);
@@ -552,7 +553,7 @@ __global__ __launch_bounds__(C::NT, 2) void gemm_pipe3_kernel(GemmArgs p) {
         mma(bc, hi, FH);
     };
 
-    static_assert(PF >= 3 && PF <= 4, "pipe3 is written for 4 or 5 LDS stages");
+    static_assert(PF >= 2 && PF <= 4, "pipe3 is written for 3 to 5 LDS stages");
     for (int st = 0; st < PF && st < nk; ++st) issue(st);
     {
         const int rem = min(PF - 1, nk - 1);  // stages beyond 0 in flight
@@ -613,22 +614,22 @@ __global__ __launch_bounds__(C::NT, 2) void gemm_pipe3_kernel(GemmArgs p) {
     }
 }
 
-template <class C, int GROUP_M>
+template <class C, int GROUP_M, int PRIO = 0>
 int launch_pipe3(const GemmArgs& a, hipStream_t s) {
     const int nbm = (a.M + C::BM - 1) / C::BM, nbn = (a.N + C::BN - 1) / C::BN;
     const dim3 grid(nbm * nbn), block(C::NT);
     switch (a.act) {
         case MME_ACT_GELU_TANH:
-            hipLaunchKernelGGL((gemm_pipe3_kernel<C, GROUP_M, MME_ACT_GELU_TANH>), grid, block, 0, s, a);
+            hipLaunchKernelGGL((gemm_pipe3_kernel<C, GROUP_M, MME_ACT_GELU_TANH, PRIO>), grid, block, 0, s, a);
             break;
         case MME_ACT_QUICK_GELU:
-            hipLaunchKernelGGL((gemm_pipe3_kernel<C, GROUP_M, MME_ACT_QUICK_GELU>), grid, block, 0, s, a);
+            hipLaunchKernelGGL((gemm_pipe3_kernel<C, GROUP_M, MME_ACT_QUICK_GELU, PRIO>), grid, block, 0, s, a);
             break;
         case MME_ACT_GELU_ERF:
-            hipLaunchKernelGGL((gemm_pipe3_kernel<C, GROUP_M, MME_ACT_GELU_ERF>), grid, block, 0, s, a);
+            hipLaunchKernelGGL((gemm_pipe3_kernel<C, GROUP_M, MME_ACT_GELU_ERF, PRIO>), grid, block, 0, s, a);
             break;
         default:
-            hipLaunchKernelGGL((gemm_pipe3_kernel<C, GROUP_M, MME_ACT_NONE>), grid, block, 0, s, a);
+            hipLaunchKernelGGL((gemm_pipe3_kernel<C, GROUP_M, MME_ACT_NONE, PRIO>), grid, block, 0, s, a);
             break;
     }
     return mme_check_launch("mme_gemm");
@@ -657,6 +658,7 @@ int launch_pipe(const GemmArgs& a, hipStream_t s) {
 
 using Pipe256 = PCfg<256, 256, 2, 4>;
 using Pipe256s5 = PCfg<256, 256, 2, 4, 5>;
+using Pipe128x256 = PCfg<128, 256, 1, 4, 3>;  // 4 waves, 72 KB LDS: two workgroups per CU
 using Pipe128 = PCfg<256, 128, 4, 2>;
 
 template <class C, int GROUP_M>
@@ -713,6 +715,10 @@ extern "C" int mme_gemm(const void* A, int lda, const void* B, int ldb, void* Cp
         case 15: return launch_pipe3<Pipe256, 4>(a, s);
         case 16: return launch_pipe3<Pipe256s5, 4>(a, s);
         case 17: return launch_pipe3<Pipe256s5, 8>(a, s);
+        case 18: return launch_pipe3<Pipe128x256, 4>(a, s);
+        case 19: return launch_pipe3<Pipe128x256, 8>(a, s);
+        case 20: return launch_pipe3<Pipe256, 4, 1>(a, s);
+        case 21: return launch_pipe3<Pipe256, 4, 2>(a, s);
         default: break;
     }
     // production dispatch: the pipelined 256x256 kernel whenever its 16-byte
