@@ -52,11 +52,22 @@ class MMEError(RuntimeError):
 _lib = None
 
 
+def _build() -> None:
+    """Compile the in-tree library with hipcc (a checkout without the built .so)."""
+    import subprocess
+    pkg = os.path.dirname(_HERE)
+    if os.path.exists(os.path.join(pkg, "Makefile")):
+        subprocess.run(["make", "-C", pkg, "-j", str(min(16, os.cpu_count() or 8))], check=False,
+                       stdout=subprocess.DEVNULL)
+
+
 def load() -> ctypes.CDLL:
     """Load libmme.so once and bind every entry point; raise loudly on failure."""
     global _lib
     if _lib is not None:
         return _lib
+    if not os.path.exists(LIB_PATH) and os.environ.get("MME_AUTOBUILD", "1") != "0":
+        _build()
     if not os.path.exists(LIB_PATH):
         raise MMEError(
             f"libmme.so not found at {LIB_PATH}; build it with `make -C multimodal-embedding_amd` "
