@@ -157,18 +157,24 @@ def main():
 
     roofline = None
     if "gemm" in kt:
+        # dominant kernel family: mme_gemm (gemm_pipe4_kernel; gemm_tn_kernel for the few small shapes).
+        # achieved = algorithmic FLOPs per launch (2*M*N*K, zero-padding excluded) / average launch time
+        # from HIP events recorded on the launch stream over the timed region.
         g = kt["gemm"]
         avg_ms = g["ms"] / g["launches"]
         achieved = g["flops"] / (g["ms"] / 1e3) / 1e12
-        roofline = {"bound": "mfma", "kernel": "gemm_tn_kernel (mme_gemm)", "achieved": round(achieved, 1),
+        roofline = {"bound": "mfma", "kernel": "mme_gemm (gemm_pipe4_kernel)", "achieved": round(achieved, 1),
                     "peak": MFMA_BF16_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": round(achieved / MFMA_BF16_PEAK_TFLOPS, 4),
                     "traffic": None, "launches": g["launches"], "avg_launch_ms": round(avg_ms, 4),
+                    "algorithmic_bytes_per_launch": round(g["bytes"] / g["launches"]),
                     "share_of_step_time": round(g["ms"] / 1e3 / dt, 3)}
+        # HBM bytes per launch from the rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes (tools/pmc_gemm.sh,
+        # gfx950-corrected by tools/pmc_summary.py) of the same launch shapes
         pmc = os.path.join(ROOT, "profiles", "gemm_traffic.json")
         if os.path.exists(pmc):
             try:
-                roofline["traffic"] = json.load(open(pmc)).get("hbm_bytes_per_launch")
-            except Exception:
+                roofline["traffic"] = round(json.load(open(pmc))["mme_gemm"]["hbm_bytes_per_launch"])
+            except (KeyError, ValueError, TypeError):
                 pass
         if "attention" in kt:
             a = kt["attention"]

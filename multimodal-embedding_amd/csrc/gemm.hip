@@ -102,22 +102,27 @@ __global__ __launch_bounds__(C::NT) void gemm_tn_kernel(GemmArgs p) {
 }
 
 // ---------------------------------------------------------------------------
-// Pipelined kernel (the production path for the encoder GEMMs).
+// Pipelined kernels for the encoder GEMMs (common to pipe3 and pipe4):
 //
-//   * 256 x {256,128} block tile, 8 waves; each wave owns a TM x TN sub-tile
-//     of 16x16 MFMA tiles computed SWAPPED (D = W-frag x X-frag), so every
-//     lane ends with 4 consecutive output COLUMNS of one row -> 8-byte packed
-//     bf16 writes in the epilogue;
-//   * K in stages of 32 through a 4-deep LDS ring filled by LDS-DMA
-//     (global_load_lds_dwordx4): stages t+1, t+2 stay in flight while stage t
-//     feeds the MFMAs, retired by a COUNTED s_waitcnt vmcnt before a raw
-//     s_barrier (never vmcnt(0) in the loop, no __syncthreads drain);
-//   * 64-byte LDS rows, 16-byte chunk XOR swizzle chunk ^ 3*((row>>3)&1):
-//     conflict-free ds_read_b128 for the 16x16x32 operand pattern; applied on
-//     the DMA source address (the DMA destination is lane-linear);
+//   * 256 x 256 block tile, 8 waves (2 x 4); each wave owns a 128 x 64
+//     sub-tile of 16x16 MFMA tiles computed SWAPPED (D = W-frag x X-frag), so
+//     every lane ends with 4 consecutive output COLUMNS of one row -> 8-byte
+//     packed bf16 writes in the epilogue;
+//   * operands staged by LDS-DMA (global_load_lds_dwordx4), XOR-swizzled on
+//     the DMA source address (the DMA destination is lane-linear); retired by
+//     a COUNTED s_waitcnt vmcnt before a raw s_barrier (no __syncthreads
+//     drain); fragment reads are inline-asm ds_read_b128 with hand-counted
+//     lgkmcnt waits (hipcc's waitcnt pass drains lgkmcnt(0) at loop heads);
 //   * epilogue: bias + activation in registers, bf16 tile staged in LDS
 //     (row pitch BN*2+16 B: conflict-free ds_write_b64), then 16-byte
 //     coalesced stores with the residual / position-table add fused.
+//
+// pipe3: K stages of 32 (64-B LDS rows) in a 4-deep ring, half-stage register
+// pipeline. pipe4 (production): K stages of 64 (whole 128-B cache lines per
+// DMA row), 2 stages, one barrier per stage -- 5-7 % faster on the SigLIP
+// shapes (tools/gemm_bench.py). The diagnostic builds (DIAG) show the loop at
+// ~1.55 PF without the DMA and ~1.45 PF without the MFMAs: the overlap of the
+// two, not either alone, sets the ~1.08 PF it reaches.
 // ---------------------------------------------------------------------------
 template <int N>
 __device__ __forceinline__ void vm_wait() {
@@ -141,301 +146,7 @@ struct PCfg {
     static_assert(PPW * NW == PIECES, "stage must split evenly into 1 KiB pieces per wave");
 };
 
-template <class C>
-__device__ __forceinline__ void pipe_wait(int remaining) {
-    // wait until only `remaining` (0..2) later stages of this wave's DMA are in flight
-    if (remaining >= 2)
-        vm_wait<2 * C::PPW>();
-    else if (remaining == 1)
-        vm_wait<C::PPW>();
-    else
-        vm_wait<0>();
-}
-
-template <class C, int GROUP_M, int ACT>
-__global__ __launch_bounds__(C::NT, 2) void gemm_pipe_kernel(GemmArgs p) {
-    __shared__ __attribute__((aligned(16))) char lds[C::LDS];
-    const int tid = threadIdx.x, lane = tid & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int wm = wave / C::WN, wn = wave % C::WN;
-    const int g = lane >> 4, li = lane & 15;
-
-    const int nbm = (p.M + C::BM - 1) / C::BM;
-    const int nbn = (p.N + C::BN - 1) / C::BN;
-    const int tile = xcd_remap(blockIdx.x, gridDim.x);
-    int bm, bn;
-    tile_coords<GROUP_M>(tile, nbm, nbn, bm, bn);
-    const int m0 = bm * C::BM, n0 = bn * C::BN;
-
-    // loop-invariant DMA source pointers: piece q of this wave covers 16 rows
-    const bf16* src[C::PPW];
-    int dst[C::PPW];
-#pragma unroll
-    for (int q = 0; q < C::PPW; ++q) {
-        const int piece = wave * C::PPW + q;
-        const bool isA = piece < C::A_PIECES;
-        const int prow = (isA ? piece : piece - C::A_PIECES) * 16 + (lane >> 2);
-        const int logical = pswz(prow, lane & 3);
-        if (isA)
-            src[q] = p.A + (size_t)min(m0 + prow, p.M - 1) * p.lda + logical * 8;
-        else
-            src[q] = p.B + (size_t)min(n0 + prow, p.N - 1) * p.ldb + logical * 8;
-        dst[q] = piece * 1024;
-    }
-    auto issue = [&](int st) {
-        char* base = lds + (st & (C::NSTAGE - 1)) * C::STAGE;
-        const int k0 = st * C::BKS;
-#pragma unroll
-        for (int q = 0; q < C::PPW; ++q) glds16(src[q] + k0, base + dst[q]);
-    };
-
-    f32x4 acc[C::FM][C::FN];
-#pragma unroll
-    for (int i = 0; i < C::FM; ++i)
-#pragma unroll
-        for (int j = 0; j < C::FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-    const int nk = p.K / C::BKS;
-    for (int st = 0; st < 3 && st < nk; ++st) issue(st);
-    for (int t = 0; t < nk; ++t) {
-        pipe_wait<C>(min(2, nk - 1 - t));
-        __builtin_amdgcn_s_barrier();
-        if (t + 3 < nk) issue(t + 3);
-        const char* As = lds + (t & (C::NSTAGE - 1)) * C::STAGE;
-        const char* Bs = As + C::A_ST;
-        bf16x8 a[C::FM], b[C::FN];
-#pragma unroll
-        for (int j = 0; j < C::FN; ++j) {
-            const int row = wn * C::TN + j * 16 + li;
-            b[j] = *reinterpret_cast<const bf16x8*>(Bs + row * 64 + (pswz(row, g) << 4));
-        }
-#pragma unroll
-        for (int i = 0; i < C::FM; ++i) {
-            const int row = wm * C::TM + i * 16 + li;
-            a[i] = *reinterpret_cast<const bf16x8*>(As + row * 64 + (pswz(row, g) << 4));
-        }
-        __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-        for (int i = 0; i < C::FM; ++i)
-#pragma unroll
-            for (int j = 0; j < C::FN; ++j)
-                acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b[j], a[i], acc[i][j], 0, 0, 0);
-        __builtin_amdgcn_s_setprio(0);
-    }
-
-    // ---- epilogue: bias + act in registers -> bf16 tile in LDS -> 16-B stores (+ residual)
-    __syncthreads();
-#pragma unroll
-    for (int j = 0; j < C::FN; ++j) {
-        const int nl = wn * C::TN + j * 16 + 4 * g;
-        float bv[4] = {0.f, 0.f, 0.f, 0.f};
-        if (p.bias) {
-#pragma unroll
-            for (int r = 0; r < 4; ++r) bv[r] = bf2f(p.bias[min(n0 + nl + r, p.N - 1)]);
-        }
-#pragma unroll
-        for (int i = 0; i < C::FM; ++i) {
-            const int ml = wm * C::TM + i * 16 + li;
-            bf16x4 o;
-#pragma unroll
-            for (int r = 0; r < 4; ++r) o[r] = f2bf(apply_act(acc[i][j][r] + bv[r], ACT));
-            *reinterpret_cast<bf16x4*>(lds + ml * C::OUT_LD + nl * 2) = o;
-        }
-    }
-    __syncthreads();
-    constexpr int CPR = C::BN / 8;  // 16-B chunks per tile row
-    bf16* Cout = reinterpret_cast<bf16*>(p.C);
-    for (int c = tid; c < C::BM * CPR; c += C::NT) {
-        const int row = c / CPR, cc = c % CPR;
-        const int gr = m0 + row, gc = n0 + cc * 8;
-        if (gr >= p.M || gc >= p.N) continue;
-        u16x8 v = *reinterpret_cast<const u16x8*>(lds + row * C::OUT_LD + cc * 16);
-        if (p.res) {
-            const int rr = p.res_period ? gr % p.res_period : gr;
-            const u16x8 rv = *reinterpret_cast<const u16x8*>(p.res + (size_t)rr * p.ldr + gc);
-            bf16x8 o;
-#pragma unroll
-            for (int e = 0; e < 8; ++e) o[e] = f2bf(bits2f(v[e]) + bits2f(rv[e]));
-            *reinterpret_cast<bf16x8*>(Cout + (size_t)gr * p.ldc + gc) = o;
-        } else {
-            *reinterpret_cast<u16x8*>(Cout + (size_t)gr * p.ldc + gc) = v;
-        }
-    }
-}
-
-// Variant with a half-stage register pipeline: the MFMAs of one half of
-// stage t run while the ds_reads of the other half (or of stage t+1) are in
-// flight, and the single barrier per stage sits between the two halves.
-template <class C, int GROUP_M, int ACT>
-__global__ __launch_bounds__(C::NT, 2) void gemm_pipe2_kernel(GemmArgs p) {
-    __shared__ __attribute__((aligned(16))) char lds[C::LDS];
-    const int tid = threadIdx.x, lane = tid & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int wm = wave / C::WN, wn = wave % C::WN;
-    const int g = lane >> 4, li = lane & 15;
-    constexpr int FH = C::FM / 2;
-
-    const int nbm = (p.M + C::BM - 1) / C::BM;
-    const int nbn = (p.N + C::BN - 1) / C::BN;
-    const int tile = xcd_remap(blockIdx.x, gridDim.x);
-    int bm, bn;
-    tile_coords<GROUP_M>(tile, nbm, nbn, bm, bn);
-    const int m0 = bm * C::BM, n0 = bn * C::BN;
-
-    const bf16* src[C::PPW];
-    int dst[C::PPW];
-#pragma unroll
-    for (int q = 0; q < C::PPW; ++q) {
-        const int piece = wave * C::PPW + q;
-        const bool isA = piece < C::A_PIECES;
-        const int prow = (isA ? piece : piece - C::A_PIECES) * 16 + (lane >> 2);
-        const int logical = pswz(prow, lane & 3);
-        if (isA)
-            src[q] = p.A + (size_t)min(m0 + prow, p.M - 1) * p.lda + logical * 8;
-        else
-            src[q] = p.B + (size_t)min(n0 + prow, p.N - 1) * p.ldb + logical * 8;
-        dst[q] = piece * 1024;
-    }
-    auto issue = [&](int st) {
-        char* base = lds + (st & (C::NSTAGE - 1)) * C::STAGE;
-        const int k0 = st * C::BKS;
-#pragma unroll
-        for (int q = 0; q < C::PPW; ++q) glds16(src[q] + k0, base + dst[q]);
-    };
-    // per-lane LDS byte offsets of this wave's fragments inside a stage
-    int boff[C::FN], aoff[C::FM];
-#pragma unroll
-    for (int j = 0; j < C::FN; ++j) {
-        const int row = wn * C::TN + j * 16 + li;
-        boff[j] = C::A_ST + row * 64 + (pswz(row, g) << 4);
-    }
-#pragma unroll
-    for (int i = 0; i < C::FM; ++i) {
-        const int row = wm * C::TM + i * 16 + li;
-        aoff[i] = row * 64 + (pswz(row, g) << 4);
-    }
-    auto stage_ptr = [&](int st) -> const char* { return lds + (st & (C::NSTAGE - 1)) * C::STAGE; };
-
-    f32x4 acc[C::FM][C::FN];
-#pragma unroll
-    for (int i = 0; i < C::FM; ++i)
-#pragma unroll
-        for (int j = 0; j < C::FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-    bf16x8 b0[C::FN], b1[C::FN], lo0[FH], lo1[FH], hi[FH];
-    const int nk = p.K / C::BKS;
-
-    auto read_b_lo = [&](int st, bf16x8 (&b)[C::FN], bf16x8 (&lo)[FH]) {
-        const char* S = stage_ptr(st);
-#pragma unroll
-        for (int j = 0; j < C::FN; ++j) b[j] = *reinterpret_cast<const bf16x8*>(S + boff[j]);
-#pragma unroll
-        for (int i = 0; i < FH; ++i) lo[i] = *reinterpret_cast<const bf16x8*>(S + aoff[i]);
-    };
-    auto step = [&](int t, bf16x8 (&bc)[C::FN], bf16x8 (&lc)[FH], bf16x8 (&bnx)[C::FN], bf16x8 (&lnx)[FH]) {
-        const char* S = stage_ptr(t);
-#pragma unroll
-        for (int i = 0; i < FH; ++i) hi[i] = *reinterpret_cast<const bf16x8*>(S + aoff[FH + i]);
-        __builtin_amdgcn_sched_barrier(0);
-        __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-        for (int i = 0; i < FH; ++i)
-#pragma unroll
-            for (int j = 0; j < C::FN; ++j)
-                acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bc[j], lc[i], acc[i][j], 0, 0, 0);
-        __builtin_amdgcn_s_setprio(0);
-        __builtin_amdgcn_sched_barrier(0);
-        if (t + 1 < nk) {
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-            pipe_wait<C>(min(2, nk - 2 - t));
-            __builtin_amdgcn_s_barrier();
-            if (t + 4 < nk) issue(t + 4);
-            read_b_lo(t + 1, bnx, lnx);
-        }
-        __builtin_amdgcn_sched_barrier(0);
-        __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-        for (int i = 0; i < FH; ++i)
-#pragma unroll
-            for (int j = 0; j < C::FN; ++j)
-                acc[FH + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bc[j], hi[i], acc[FH + i][j], 0, 0, 0);
-        __builtin_amdgcn_s_setprio(0);
-        __builtin_amdgcn_sched_barrier(0);
-    };
-
-    for (int st = 0; st < 3 && st < nk; ++st) issue(st);
-    pipe_wait<C>(min(2, nk - 1));
-    __builtin_amdgcn_s_barrier();
-    if (3 < nk) issue(3);
-    read_b_lo(0, b0, lo0);
-    for (int t = 0; t < nk; t += 2) {
-        step(t, b0, lo0, b1, lo1);
-        if (t + 1 < nk) step(t + 1, b1, lo1, b0, lo0);
-    }
-
-    __syncthreads();
-#pragma unroll
-    for (int j = 0; j < C::FN; ++j) {
-        const int nl = wn * C::TN + j * 16 + 4 * g;
-        float bv[4] = {0.f, 0.f, 0.f, 0.f};
-        if (p.bias) {
-#pragma unroll
-            for (int r = 0; r < 4; ++r) bv[r] = bf2f(p.bias[min(n0 + nl + r, p.N - 1)]);
-        }
-#pragma unroll
-        for (int i = 0; i < C::FM; ++i) {
-            const int ml = wm * C::TM + i * 16 + li;
-            bf16x4 o;
-#pragma unroll
-            for (int r = 0; r < 4; ++r) o[r] = f2bf(apply_act(acc[i][j][r] + bv[r], ACT));
-            *reinterpret_cast<bf16x4*>(lds + ml * C::OUT_LD + nl * 2) = o;
-        }
-    }
-    __syncthreads();
-    constexpr int CPR = C::BN / 8;
-    bf16* Cout = reinterpret_cast<bf16*>(p.C);
-    for (int c = tid; c < C::BM * CPR; c += C::NT) {
-        const int row = c / CPR, cc = c % CPR;
-        const int gr = m0 + row, gc = n0 + cc * 8;
-        if (gr >= p.M || gc >= p.N) continue;
-        u16x8 v = *reinterpret_cast<const u16x8*>(lds + row * C::OUT_LD + cc * 16);
-        if (p.res) {
-            const int rr = p.res_period ? gr % p.res_period : gr;
-            const u16x8 rv = *reinterpret_cast<const u16x8*>(p.res + (size_t)rr * p.ldr + gc);
-            bf16x8 o;
-#pragma unroll
-            for (int e = 0; e < 8; ++e) o[e] = f2bf(bits2f(v[e]) + bits2f(rv[e]));
-            *reinterpret_cast<bf16x8*>(Cout + (size_t)gr * p.ldc + gc) = o;
-        } else {
-            *reinterpret_cast<u16x8*>(Cout + (size_t)gr * p.ldc + gc) = v;
-        }
-    }
-}
-
-template <class C, int GROUP_M>
-int launch_pipe2(const GemmArgs& a, hipStream_t s) {
-    const int nbm = (a.M + C::BM - 1) / C::BM, nbn = (a.N + C::BN - 1) / C::BN;
-    const dim3 grid(nbm * nbn), block(C::NT);
-    switch (a.act) {
-        case MME_ACT_GELU_TANH:
-            hipLaunchKernelGGL((gemm_pipe2_kernel<C, GROUP_M, MME_ACT_GELU_TANH>), grid, block, 0, s, a);
-            break;
-        case MME_ACT_QUICK_GELU:
-            hipLaunchKernelGGL((gemm_pipe2_kernel<C, GROUP_M, MME_ACT_QUICK_GELU>), grid, block, 0, s, a);
-            break;
-        case MME_ACT_GELU_ERF:
-            hipLaunchKernelGGL((gemm_pipe2_kernel<C, GROUP_M, MME_ACT_GELU_ERF>), grid, block, 0, s, a);
-            break;
-        default:
-            hipLaunchKernelGGL((gemm_pipe2_kernel<C, GROUP_M, MME_ACT_NONE>), grid, block, 0, s, a);
-            break;
-    }
-    return mme_check_launch("mme_gemm");
-}
-
-// Variant 3: same schedule as pipe2 with the fragment loads as inline-asm
-// ds_read_b128 and hand-counted lgkmcnt waits (hipcc's waitcnt pass drains
-// lgkmcnt(0) at the loop head otherwise, serialising reads and MFMAs).
+// pipe3 / pipe4 helpers: counted lgkm waits and inline-asm fragment reads.
 template <int N>
 __device__ __forceinline__ void lgkm_wait() {
     asm volatile("s_waitcnt lgkmcnt(%0)" ::"n"(N) : "memory");
@@ -446,8 +157,10 @@ __device__ __forceinline__ void ds_read16(bf16x8& r, unsigned addr) {
     asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(r) : "v"(addr), "n"(OFF));
 }
 
-template <class C, int GROUP_M, int ACT, int PRIO = 0>
+template <class C, int GROUP_M, int ACT, int DIAG = 0>
 __global__ __launch_bounds__(C::NT, 2) void gemm_pipe3_kernel(GemmArgs p) {
+    // DIAG (diagnostic builds only, wrong results): 1 = no LDS-DMA at all,
+    // 2 = no MFMA (loads/reads/barriers only)
     __shared__ __attribute__((aligned(16))) char lds[C::LDS];
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -481,6 +194,7 @@ __global__ __launch_bounds__(C::NT, 2) void gemm_pipe3_kernel(GemmArgs p) {
     auto issue = [&](int st) {
         char* base = lds + (st % C::NSTAGE) * C::STAGE;
         const int k0 = st * C::BKS;
+        if (DIAG == 1) return;
 #pragma unroll
         for (int q = 0; q < C::PPW; ++q) glds16(src[q] + k0, base + dst[q]);
     };
@@ -518,16 +232,19 @@ __global__ __launch_bounds__(C::NT, 2) void gemm_pipe3_kernel(GemmArgs p) {
         ds_read16<7168>(hi[3], aa);
     };
     auto mma = [&](bf16x8 (&b)[4], bf16x8 (&a)[4], int ib) {
-        if (PRIO == 0) __builtin_amdgcn_s_setprio(1);
+        __builtin_amdgcn_s_setprio(1);
 #pragma unroll
         for (int i = 0; i < 4; ++i)
 #pragma unroll
-            for (int j = 0; j < 4; ++j)
-                acc[ib + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b[j], a[i], acc[ib + i][j], 0, 0, 0);
-        if (PRIO == 0) __builtin_amdgcn_s_setprio(0);
+            for (int j = 0; j < 4; ++j) {
+                if (DIAG == 2)
+                    asm volatile("" ::"v"(b[j]), "v"(a[i]));
+                else
+                    acc[ib + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b[j], a[i], acc[ib + i][j], 0, 0, 0);
+            }
+        __builtin_amdgcn_s_setprio(0);
         __builtin_amdgcn_sched_barrier(0);
     };
-    if (PRIO == 1 && __builtin_amdgcn_readfirstlane(tid) >= C::NT / 2) __builtin_amdgcn_s_setprio(1);
     // one stage; `full` = a next stage exists and stage t+NSTAGE must be issued
     auto step = [&](int t, bf16x8 (&bc)[4], bf16x8 (&lc)[4], bf16x8 (&bnx)[4], bf16x8 (&lnx)[4], bool full) {
         read_hi(t);
@@ -614,52 +331,217 @@ __global__ __launch_bounds__(C::NT, 2) void gemm_pipe3_kernel(GemmArgs p) {
     }
 }
 
-template <class C, int GROUP_M, int PRIO = 0>
+template <class C, int GROUP_M, int DIAG = 0>
 int launch_pipe3(const GemmArgs& a, hipStream_t s) {
     const int nbm = (a.M + C::BM - 1) / C::BM, nbn = (a.N + C::BN - 1) / C::BN;
     const dim3 grid(nbm * nbn), block(C::NT);
     switch (a.act) {
         case MME_ACT_GELU_TANH:
-            hipLaunchKernelGGL((gemm_pipe3_kernel<C, GROUP_M, MME_ACT_GELU_TANH, PRIO>), grid, block, 0, s, a);
+            hipLaunchKernelGGL((gemm_pipe3_kernel<C, GROUP_M, MME_ACT_GELU_TANH, DIAG>), grid, block, 0, s, a);
             break;
         case MME_ACT_QUICK_GELU:
-            hipLaunchKernelGGL((gemm_pipe3_kernel<C, GROUP_M, MME_ACT_QUICK_GELU, PRIO>), grid, block, 0, s, a);
+            hipLaunchKernelGGL((gemm_pipe3_kernel<C, GROUP_M, MME_ACT_QUICK_GELU, DIAG>), grid, block, 0, s, a);
             break;
         case MME_ACT_GELU_ERF:
-            hipLaunchKernelGGL((gemm_pipe3_kernel<C, GROUP_M, MME_ACT_GELU_ERF, PRIO>), grid, block, 0, s, a);
+            hipLaunchKernelGGL((gemm_pipe3_kernel<C, GROUP_M, MME_ACT_GELU_ERF, DIAG>), grid, block, 0, s, a);
             break;
         default:
-            hipLaunchKernelGGL((gemm_pipe3_kernel<C, GROUP_M, MME_ACT_NONE, PRIO>), grid, block, 0, s, a);
+            hipLaunchKernelGGL((gemm_pipe3_kernel<C, GROUP_M, MME_ACT_NONE, DIAG>), grid, block, 0, s, a);
             break;
     }
     return mme_check_launch("mme_gemm");
 }
 
-template <class C, int GROUP_M>
-int launch_pipe(const GemmArgs& a, hipStream_t s) {
+// ---------------------------------------------------------------------------
+// Variant 4: 64-deep K stages (128-B LDS rows = whole cache lines per DMA row),
+// 2 stages of 64 KB, one barrier per stage; inside a stage four quarter-steps
+// (k-substep x A half) with the next quarter's fragments read while the
+// current quarter's 16 MFMAs run.
+// ---------------------------------------------------------------------------
+template <int BM_, int BN_, int WM_, int WN_>
+struct QCfg {
+    static constexpr int BM = BM_, BN = BN_, WM = WM_, WN = WN_;
+    static constexpr int NW = WM * WN, NT = NW * 64;
+    static constexpr int TM = BM / WM, TN = BN / WN, FM = TM / 16, FN = TN / 16;
+    static constexpr int BKS = 64;
+    static constexpr int A_ST = BM * BKS * 2, B_ST = BN * BKS * 2, STAGE = A_ST + B_ST;
+    static constexpr int A_PIECES = A_ST / 1024, PIECES = STAGE / 1024;
+    static constexpr int PPW = PIECES / NW;
+    static constexpr int OUT_LD = BN * 2 + 16;
+    static constexpr int LDS_MAIN = 2 * STAGE, LDS_OUT = BM * OUT_LD;
+    static constexpr int LDS = LDS_MAIN > LDS_OUT ? LDS_MAIN : LDS_OUT;
+    static_assert(PPW * NW == PIECES, "stage must split evenly into 1 KiB pieces per wave");
+};
+
+template <class C, int GROUP_M, int ACT, int DIAG = 0>
+__global__ __launch_bounds__(C::NT, 2) void gemm_pipe4_kernel(GemmArgs p) {
+    __shared__ __attribute__((aligned(16))) char lds[C::LDS];
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wm = wave / C::WN, wn = wave % C::WN;
+    const int g = lane >> 4, li = lane & 15;
+    static_assert(C::FN == 4 && C::FM == 8, "pipe4 is written for 128 x 64 wave tiles");
+
+    const int nbm = (p.M + C::BM - 1) / C::BM;
+    const int nbn = (p.N + C::BN - 1) / C::BN;
+    const int tile = xcd_remap(blockIdx.x, gridDim.x);
+    int bm, bn;
+    tile_coords<GROUP_M>(tile, nbm, nbn, bm, bn);
+    const int m0 = bm * C::BM, n0 = bn * C::BN;
+
+    // DMA: a 1 KiB piece = 8 rows x 128 B; lane -> row piece*8 + lane/8, chunk lane%8
+    const bf16* src[C::PPW];
+    int dst[C::PPW];
+#pragma unroll
+    for (int q = 0; q < C::PPW; ++q) {
+        const int piece = wave * C::PPW + q;
+        const bool isA = piece < C::A_PIECES;
+        const int prow = (isA ? piece : piece - C::A_PIECES) * 8 + (lane >> 3);
+        const int logical = swz(prow, lane & 7);
+        if (isA)
+            src[q] = p.A + (size_t)min(m0 + prow, p.M - 1) * p.lda + logical * 8;
+        else
+            src[q] = p.B + (size_t)min(n0 + prow, p.N - 1) * p.ldb + logical * 8;
+        dst[q] = piece * 1024;
+    }
+    auto issue = [&](int st) {
+        if (DIAG == 1) return;
+        char* base = lds + (st & 1) * C::STAGE;
+        const int k0 = st * C::BKS;
+#pragma unroll
+        for (int q = 0; q < C::PPW; ++q) glds16(src[q] + k0, base + dst[q]);
+    };
+    // fragment addresses: row r, logical chunk c -> r*128 + ((c ^ ((r>>1)&7)) << 4);
+    // rows of one wave's fragments differ by multiples of 16 -> (r>>1)&7 depends only on li
+    const unsigned lds0 = (unsigned)(uintptr_t)(LDS_AS char*)lds;
+    const int sw = (li >> 1) & 7;
+    const unsigned a_row = lds0 + (wm * C::TM + li) * 128;
+    const unsigned b_row = lds0 + C::A_ST + (wn * C::TN + li) * 128;
+    // per k-substep ks the chunk is ks*4 + g
+    const unsigned ca0 = ((0 * 4 + g) ^ sw) << 4, ca1 = ((1 * 4 + g) ^ sw) << 4;
+
+    f32x4 acc[C::FM][C::FN];
+#pragma unroll
+    for (int i = 0; i < C::FM; ++i)
+#pragma unroll
+        for (int j = 0; j < C::FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    bf16x8 bq0[4], bq1[4], aq0[4], aq1[4];
+    const int nk = p.K / C::BKS;
+
+    auto rd_b = [&](bf16x8 (&b)[4], unsigned base) {
+        ds_read16<0>(b[0], base);
+        ds_read16<16 * 128>(b[1], base);
+        ds_read16<32 * 128>(b[2], base);
+        ds_read16<48 * 128>(b[3], base);
+    };
+    auto rd_a = [&](bf16x8 (&a)[4], unsigned base) {  // 4 m-frags, 16 rows apart
+        ds_read16<0>(a[0], base);
+        ds_read16<16 * 128>(a[1], base);
+        ds_read16<32 * 128>(a[2], base);
+        ds_read16<48 * 128>(a[3], base);
+    };
+    auto mma = [&](bf16x8 (&b)[4], bf16x8 (&a)[4], int ib) {
+        __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                if (DIAG == 2)
+                    asm volatile("" ::"v"(b[j]), "v"(a[i]));
+                else
+                    acc[ib + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b[j], a[i], acc[ib + i][j], 0, 0, 0);
+            }
+        __builtin_amdgcn_s_setprio(0);
+        __builtin_amdgcn_sched_barrier(0);
+    };
+
+    issue(0);
+    for (int t = 0; t < nk; ++t) {
+        vm_wait<0>();
+        __builtin_amdgcn_s_barrier();
+        if (t + 1 < nk) issue(t + 1);
+        const unsigned so = (t & 1) * C::STAGE;
+        const unsigned ab = a_row + so, bb = b_row + so;
+        // quarter 0: B(ks0), A lo(ks0)
+        rd_b(bq0, bb + ca0);
+        rd_a(aq0, ab + ca0);
+        rd_a(aq1, ab + 64 * 128 + ca0);  // A hi (ks0)
+        lgkm_wait<4>();
+        mma(bq0, aq0, 0);
+        rd_b(bq1, bb + ca1);
+        rd_a(aq0, ab + ca1);             // A lo (ks1)
+        lgkm_wait<8>();
+        mma(bq0, aq1, 4);
+        rd_a(aq1, ab + 64 * 128 + ca1);  // A hi (ks1)
+        lgkm_wait<4>();
+        mma(bq1, aq0, 0);
+        lgkm_wait<0>();
+        mma(bq1, aq1, 4);
+    }
+
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < C::FN; ++j) {
+        const int nl = wn * C::TN + j * 16 + 4 * g;
+        float bv[4] = {0.f, 0.f, 0.f, 0.f};
+        if (p.bias) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) bv[r] = bf2f(p.bias[min(n0 + nl + r, p.N - 1)]);
+        }
+#pragma unroll
+        for (int i = 0; i < C::FM; ++i) {
+            const int ml = wm * C::TM + i * 16 + li;
+            bf16x4 o;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) o[r] = f2bf(apply_act(acc[i][j][r] + bv[r], ACT));
+            *reinterpret_cast<bf16x4*>(lds + ml * C::OUT_LD + nl * 2) = o;
+        }
+    }
+    __syncthreads();
+    constexpr int CPR = C::BN / 8;
+    bf16* Cout = reinterpret_cast<bf16*>(p.C);
+    for (int c = tid; c < C::BM * CPR; c += C::NT) {
+        const int row = c / CPR, cc = c % CPR;
+        const int gr = m0 + row, gc = n0 + cc * 8;
+        if (gr >= p.M || gc >= p.N) continue;
+        u16x8 v = *reinterpret_cast<const u16x8*>(lds + row * C::OUT_LD + cc * 16);
+        if (p.res) {
+            const int rr = p.res_period ? gr % p.res_period : gr;
+            const u16x8 rv = *reinterpret_cast<const u16x8*>(p.res + (size_t)rr * p.ldr + gc);
+            bf16x8 o;
+#pragma unroll
+            for (int e = 0; e < 8; ++e) o[e] = f2bf(bits2f(v[e]) + bits2f(rv[e]));
+            *reinterpret_cast<bf16x8*>(Cout + (size_t)gr * p.ldc + gc) = o;
+        } else {
+            *reinterpret_cast<u16x8*>(Cout + (size_t)gr * p.ldc + gc) = v;
+        }
+    }
+}
+
+template <class C, int GROUP_M, int DIAG = 0>
+int launch_pipe4(const GemmArgs& a, hipStream_t s) {
     const int nbm = (a.M + C::BM - 1) / C::BM, nbn = (a.N + C::BN - 1) / C::BN;
     const dim3 grid(nbm * nbn), block(C::NT);
     switch (a.act) {
         case MME_ACT_GELU_TANH:
-            hipLaunchKernelGGL((gemm_pipe_kernel<C, GROUP_M, MME_ACT_GELU_TANH>), grid, block, 0, s, a);
+            hipLaunchKernelGGL((gemm_pipe4_kernel<C, GROUP_M, MME_ACT_GELU_TANH, DIAG>), grid, block, 0, s, a);
             break;
         case MME_ACT_QUICK_GELU:
-            hipLaunchKernelGGL((gemm_pipe_kernel<C, GROUP_M, MME_ACT_QUICK_GELU>), grid, block, 0, s, a);
+            hipLaunchKernelGGL((gemm_pipe4_kernel<C, GROUP_M, MME_ACT_QUICK_GELU, DIAG>), grid, block, 0, s, a);
             break;
         case MME_ACT_GELU_ERF:
-            hipLaunchKernelGGL((gemm_pipe_kernel<C, GROUP_M, MME_ACT_GELU_ERF>), grid, block, 0, s, a);
+            hipLaunchKernelGGL((gemm_pipe4_kernel<C, GROUP_M, MME_ACT_GELU_ERF, DIAG>), grid, block, 0, s, a);
             break;
         default:
-            hipLaunchKernelGGL((gemm_pipe_kernel<C, GROUP_M, MME_ACT_NONE>), grid, block, 0, s, a);
+            hipLaunchKernelGGL((gemm_pipe4_kernel<C, GROUP_M, MME_ACT_NONE, DIAG>), grid, block, 0, s, a);
             break;
     }
     return mme_check_launch("mme_gemm");
 }
 
 using Pipe256 = PCfg<256, 256, 2, 4>;
-using Pipe256s5 = PCfg<256, 256, 2, 4, 5>;
-using Pipe128x256 = PCfg<128, 256, 1, 4, 3>;  // 4 waves, 72 KB LDS: two workgroups per CU
-using Pipe128 = PCfg<256, 128, 4, 2>;
+using Pipe256q = QCfg<256, 256, 2, 4>;
 
 template <class C, int GROUP_M>
 int launch(const GemmArgs& a, hipStream_t s) {
@@ -704,21 +586,14 @@ extern "C" int mme_gemm(const void* A, int lda, const void* B, int ldb, void* Cp
         case 4: return launch<SqCfg, 4>(a, s);
         case 5: return launch<SqCfg, 8>(a, s);
         case 6: return launch<SmallCfg, 8>(a, s);
-        case 7: return launch_pipe<Pipe256, 4>(a, s);
-        case 8: return launch_pipe<Pipe128, 4>(a, s);
-        case 9: return launch_pipe<Pipe256, 8>(a, s);
-        case 10: return launch_pipe<Pipe128, 8>(a, s);
-        case 11: return launch_pipe<Pipe256, 1>(a, s);
-        case 12: return launch_pipe2<Pipe256, 8>(a, s);
-        case 13: return launch_pipe2<Pipe256, 4>(a, s);
         case 14: return launch_pipe3<Pipe256, 8>(a, s);
         case 15: return launch_pipe3<Pipe256, 4>(a, s);
-        case 16: return launch_pipe3<Pipe256s5, 4>(a, s);
-        case 17: return launch_pipe3<Pipe256s5, 8>(a, s);
-        case 18: return launch_pipe3<Pipe128x256, 4>(a, s);
-        case 19: return launch_pipe3<Pipe128x256, 8>(a, s);
-        case 20: return launch_pipe3<Pipe256, 4, 1>(a, s);
-        case 21: return launch_pipe3<Pipe256, 4, 2>(a, s);
+        case 22: return launch_pipe3<Pipe256, 4, 1>(a, s);  // diagnostic: no DMA
+        case 23: return launch_pipe3<Pipe256, 4, 2>(a, s);  // diagnostic: no MFMA
+        case 24: return launch_pipe4<Pipe256q, 4>(a, s);
+        case 25: return launch_pipe4<Pipe256q, 8>(a, s);
+        case 26: return launch_pipe4<Pipe256q, 4, 1>(a, s);  // diagnostic: no DMA
+        case 27: return launch_pipe4<Pipe256q, 4, 2>(a, s);  // diagnostic: no MFMA
         default: break;
     }
     // production dispatch: the pipelined 256x256 kernel whenever its 16-byte
@@ -726,7 +601,7 @@ extern "C" int mme_gemm(const void* A, int lda, const void* B, int ldb, void* Cp
     const bool vec_ok = !out_f32 && ldc % 8 == 0 && ((uintptr_t)Cp & 15) == 0 &&
                         (!residual || (ldr % 8 == 0 && ((uintptr_t)residual & 15) == 0)) && N % 8 == 0;
     if (vec_ok && (long)M * N >= 1024L * 1024) {
-        return launch_pipe3<Pipe256, 4>(a, s);
+        return launch_pipe4<Pipe256q, 4>(a, s);
     }
     if ((long)M * N >= 2048L * 1024) return launch<BigCfg, 1>(a, s);
     return launch<SmallCfg, 8>(a, s);

@@ -25,7 +25,7 @@ def load(d, counter):
 
 
 def family(name):
-    for k in ("gemm_pipe3_kernel", "gemm_tn_kernel", "attn_fwd_kernel", "layernorm_kernel", "sim_topk_kernel",
+    for k in ("gemm_pipe4_kernel", "gemm_pipe3_kernel", "gemm_tn_kernel", "attn_fwd_kernel", "layernorm_kernel", "sim_topk_kernel",
               "resample_v_patch_kernel", "probe_attn_kernel"):
         if k in name:
             return k
@@ -48,6 +48,12 @@ def main(d):
                   "hbm_bytes_per_launch": (2 * f["fetch_kb"] + f["write_kb"]) * 1024 / n,
                   "fetch_bytes_per_launch_corrected": 2 * f["fetch_kb"] * 1024 / n,
                   "write_bytes_per_launch": f["write_kb"] * 1024 / n}
+    # the mme_gemm entry point as bench.py's KernelTimer sees it: every GEMM kernel together
+    fams = [f for k, f in fam.items() if k.startswith("gemm_")]
+    n = sum(f["launches"] for f in fams)
+    if n:
+        out["mme_gemm"] = {"launches": n,
+                           "hbm_bytes_per_launch": sum(2 * f["fetch_kb"] + f["write_kb"] for f in fams) * 1024 / n}
     print(json.dumps(out, indent=1))
 
 
