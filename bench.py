@@ -157,13 +157,13 @@ def main():
 
     roofline = None
     if "gemm" in kt:
-        # dominant kernel family: mme_gemm (gemm_pipe4_kernel; gemm_tn_kernel for the few small shapes).
+        # dominant kernel family: mme_gemm (gemm_pipe6_kernel; gemm_tn_kernel for the few small shapes).
         # achieved = algorithmic FLOPs per launch (2*M*N*K, zero-padding excluded) / average launch time
         # from HIP events recorded on the launch stream over the timed region.
         g = kt["gemm"]
         avg_ms = g["ms"] / g["launches"]
         achieved = g["flops"] / (g["ms"] / 1e3) / 1e12
-        roofline = {"bound": "mfma", "kernel": "mme_gemm (gemm_pipe4_kernel)", "achieved": round(achieved, 1),
+        roofline = {"bound": "mfma", "kernel": "mme_gemm (gemm_pipe6_kernel)", "achieved": round(achieved, 1),
                     "peak": MFMA_BF16_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": round(achieved / MFMA_BF16_PEAK_TFLOPS, 4),
                     "traffic": None, "launches": g["launches"], "avg_launch_ms": round(avg_ms, 4),
                     "algorithmic_bytes_per_launch": round(g["bytes"] / g["launches"]),

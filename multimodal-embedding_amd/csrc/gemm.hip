@@ -118,11 +118,16 @@ __global__ __launch_bounds__(C::NT) void gemm_tn_kernel(GemmArgs p) {
 //     coalesced stores with the residual / position-table add fused.
 //
 // pipe3: K stages of 32 (64-B LDS rows) in a 4-deep ring, half-stage register
-// pipeline. pipe4 (production): K stages of 64 (whole 128-B cache lines per
-// DMA row), 2 stages, one barrier per stage -- 5-7 % faster on the SigLIP
-// shapes (tools/gemm_bench.py). The diagnostic builds (DIAG) show the loop at
-// ~1.55 PF without the DMA and ~1.45 PF without the MFMAs: the overlap of the
-// two, not either alone, sets the ~1.08 PF it reaches.
+// pipeline. pipe4: K stages of 64 (whole 128-B cache lines per DMA row), 2
+// stages, one barrier per stage (+5-7 % over pipe3). pipe6 (production):
+// pipe3's ring with a ping-pong schedule between the two wave rows (+3-6 %
+// over pipe4; +15-20 % over the same kernel without the stagger).
+// Diagnostic builds (DIAG, tools/gemm_bench.py) of pipe6 on the fc1 shape:
+// without the DMA 1.54 PF/s, with DMA + barriers only (no ds_read, no MFMA)
+// 1.35 PF/s-equivalent -- the LDS-DMA path moves ~13 TB/s of L2->LDS traffic
+// (about 50 GB/s per CU, the same with every tile L2-resident) and a 256^2
+// tile needs 1 KiB per 128 KFLOP, so the staging path, overlapped with the
+// MFMAs, sets the ~1.1 PF/s these kernels reach; ring depth 3/4/5 is neutral.
 // ---------------------------------------------------------------------------
 template <int N>
 __device__ __forceinline__ void vm_wait() {
@@ -155,6 +160,51 @@ __device__ __forceinline__ void lgkm_wait() {
 template <int OFF>
 __device__ __forceinline__ void ds_read16(bf16x8& r, unsigned addr) {
     asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(r) : "v"(addr), "n"(OFF));
+}
+
+// Shared epilogue of the pipelined kernels: bias + activation in registers,
+// bf16 tile staged in LDS (row pitch BN*2+16 B), 16-B stores with the
+// residual / position-table add fused. Starts with a barrier (LDS reuse).
+template <class C, int ACT>
+__device__ __forceinline__ void gemm_epilogue_lds(const GemmArgs& p, char* lds, f32x4 (&acc)[C::FM][C::FN], int m0,
+                                                  int n0, int wm, int wn, int g, int li, int tid) {
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < C::FN; ++j) {
+        const int nl = wn * C::TN + j * 16 + 4 * g;
+        float bv[4] = {0.f, 0.f, 0.f, 0.f};
+        if (p.bias) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) bv[r] = bf2f(p.bias[min(n0 + nl + r, p.N - 1)]);
+        }
+#pragma unroll
+        for (int i = 0; i < C::FM; ++i) {
+            const int ml = wm * C::TM + i * 16 + li;
+            bf16x4 o;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) o[r] = f2bf(apply_act(acc[i][j][r] + bv[r], ACT));
+            *reinterpret_cast<bf16x4*>(lds + ml * C::OUT_LD + nl * 2) = o;
+        }
+    }
+    __syncthreads();
+    constexpr int CPR = C::BN / 8;
+    bf16* Cout = reinterpret_cast<bf16*>(p.C);
+    for (int c = tid; c < C::BM * CPR; c += C::NT) {
+        const int row = c / CPR, cc = c % CPR;
+        const int gr = m0 + row, gc = n0 + cc * 8;
+        if (gr >= p.M || gc >= p.N) continue;
+        u16x8 v = *reinterpret_cast<const u16x8*>(lds + row * C::OUT_LD + cc * 16);
+        if (p.res) {
+            const int rr = p.res_period ? gr % p.res_period : gr;
+            const u16x8 rv = *reinterpret_cast<const u16x8*>(p.res + (size_t)rr * p.ldr + gc);
+            bf16x8 o;
+#pragma unroll
+            for (int e = 0; e < 8; ++e) o[e] = f2bf(bits2f(v[e]) + bits2f(rv[e]));
+            *reinterpret_cast<bf16x8*>(Cout + (size_t)gr * p.ldc + gc) = o;
+        } else {
+            *reinterpret_cast<u16x8*>(Cout + (size_t)gr * p.ldc + gc) = v;
+        }
+    }
 }
 
 template <class C, int GROUP_M, int ACT, int DIAG = 0>
@@ -292,43 +342,7 @@ __global__ __launch_bounds__(C::NT, 2) void gemm_pipe3_kernel(GemmArgs p) {
         if (t + 1 < nk) step(t + 1, b1, l1, b0, l0, t + 1 + C::NSTAGE < nk);
     }
 
-    __syncthreads();
-#pragma unroll
-    for (int j = 0; j < C::FN; ++j) {
-        const int nl = wn * C::TN + j * 16 + 4 * g;
-        float bv[4] = {0.f, 0.f, 0.f, 0.f};
-        if (p.bias) {
-#pragma unroll
-            for (int r = 0; r < 4; ++r) bv[r] = bf2f(p.bias[min(n0 + nl + r, p.N - 1)]);
-        }
-#pragma unroll
-        for (int i = 0; i < C::FM; ++i) {
-            const int ml = wm * C::TM + i * 16 + li;
-            bf16x4 o;
-#pragma unroll
-            for (int r = 0; r < 4; ++r) o[r] = f2bf(apply_act(acc[i][j][r] + bv[r], ACT));
-            *reinterpret_cast<bf16x4*>(lds + ml * C::OUT_LD + nl * 2) = o;
-        }
-    }
-    __syncthreads();
-    constexpr int CPR = C::BN / 8;
-    bf16* Cout = reinterpret_cast<bf16*>(p.C);
-    for (int c = tid; c < C::BM * CPR; c += C::NT) {
-        const int row = c / CPR, cc = c % CPR;
-        const int gr = m0 + row, gc = n0 + cc * 8;
-        if (gr >= p.M || gc >= p.N) continue;
-        u16x8 v = *reinterpret_cast<const u16x8*>(lds + row * C::OUT_LD + cc * 16);
-        if (p.res) {
-            const int rr = p.res_period ? gr % p.res_period : gr;
-            const u16x8 rv = *reinterpret_cast<const u16x8*>(p.res + (size_t)rr * p.ldr + gc);
-            bf16x8 o;
-#pragma unroll
-            for (int e = 0; e < 8; ++e) o[e] = f2bf(bits2f(v[e]) + bits2f(rv[e]));
-            *reinterpret_cast<bf16x8*>(Cout + (size_t)gr * p.ldc + gc) = o;
-        } else {
-            *reinterpret_cast<u16x8*>(Cout + (size_t)gr * p.ldc + gc) = v;
-        }
-    }
+    gemm_epilogue_lds<C, ACT>(p, lds, acc, m0, n0, wm, wn, g, li, tid);
 }
 
 template <class C, int GROUP_M, int DIAG = 0>
@@ -480,43 +494,7 @@ __global__ __launch_bounds__(C::NT, 2) void gemm_pipe4_kernel(GemmArgs p) {
         mma(bq1, aq1, 4);
     }
 
-    __syncthreads();
-#pragma unroll
-    for (int j = 0; j < C::FN; ++j) {
-        const int nl = wn * C::TN + j * 16 + 4 * g;
-        float bv[4] = {0.f, 0.f, 0.f, 0.f};
-        if (p.bias) {
-#pragma unroll
-            for (int r = 0; r < 4; ++r) bv[r] = bf2f(p.bias[min(n0 + nl + r, p.N - 1)]);
-        }
-#pragma unroll
-        for (int i = 0; i < C::FM; ++i) {
-            const int ml = wm * C::TM + i * 16 + li;
-            bf16x4 o;
-#pragma unroll
-            for (int r = 0; r < 4; ++r) o[r] = f2bf(apply_act(acc[i][j][r] + bv[r], ACT));
-            *reinterpret_cast<bf16x4*>(lds + ml * C::OUT_LD + nl * 2) = o;
-        }
-    }
-    __syncthreads();
-    constexpr int CPR = C::BN / 8;
-    bf16* Cout = reinterpret_cast<bf16*>(p.C);
-    for (int c = tid; c < C::BM * CPR; c += C::NT) {
-        const int row = c / CPR, cc = c % CPR;
-        const int gr = m0 + row, gc = n0 + cc * 8;
-        if (gr >= p.M || gc >= p.N) continue;
-        u16x8 v = *reinterpret_cast<const u16x8*>(lds + row * C::OUT_LD + cc * 16);
-        if (p.res) {
-            const int rr = p.res_period ? gr % p.res_period : gr;
-            const u16x8 rv = *reinterpret_cast<const u16x8*>(p.res + (size_t)rr * p.ldr + gc);
-            bf16x8 o;
-#pragma unroll
-            for (int e = 0; e < 8; ++e) o[e] = f2bf(bits2f(v[e]) + bits2f(rv[e]));
-            *reinterpret_cast<bf16x8*>(Cout + (size_t)gr * p.ldc + gc) = o;
-        } else {
-            *reinterpret_cast<u16x8*>(Cout + (size_t)gr * p.ldc + gc) = v;
-        }
-    }
+    gemm_epilogue_lds<C, ACT>(p, lds, acc, m0, n0, wm, wn, g, li, tid);
 }
 
 template <class C, int GROUP_M, int DIAG = 0>
@@ -535,6 +513,151 @@ int launch_pipe4(const GemmArgs& a, hipStream_t s) {
             break;
         default:
             hipLaunchKernelGGL((gemm_pipe4_kernel<C, GROUP_M, MME_ACT_NONE, DIAG>), grid, block, 0, s, a);
+            break;
+    }
+    return mme_check_launch("mme_gemm");
+}
+
+// ---------------------------------------------------------------------------
+// pipe6: "ping-pong" schedule. Same 256x256 tile, 32-deep stages and 4-deep
+// LDS ring as pipe3, but each stage is split into a memory phase (12
+// ds_read_b128 + the DMA issue of stage t+3 + counted waits) and a compute
+// phase (32 MFMAs), separated by raw barriers; with STAG the second wave row
+// (wm = 1) runs one barrier behind the first, so on every SIMD (one wave of
+// each row) one wave computes while the other reads: the MFMA pipe is fed by
+// alternating waves instead of both waves stalling on LDS at the same time.
+// Ordering: stage s is read after barrier B(2s) (row 0) / B(2s+1) (row 1);
+// every wave retires its own stage-s DMA (vmcnt) before the barrier that
+// closes its memory phase s-1, i.e. before B(2s) -> RAW safe; the buffer of
+// stage t+3 was last read in memory phase t-1, whose reads every wave retired
+// (lgkmcnt(0)) before that phase's closing barrier -> WAR safe.
+// ---------------------------------------------------------------------------
+template <class C, int GROUP_M, int ACT, int STAG, int DIAG = 0>
+__global__ __launch_bounds__(C::NT, 2) void gemm_pipe6_kernel(GemmArgs p) {
+    __shared__ __attribute__((aligned(16))) char lds[C::LDS];
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wm = wave / C::WN, wn = wave % C::WN;
+    const int g = lane >> 4, li = lane & 15;
+    static_assert(C::FN == 4 && C::FM == 8 && C::WM == 2, "pipe6 geometry");
+    constexpr int PF = C::NSTAGE - 1;  // stages issued ahead of the one being read
+    static_assert(PF >= 2 && PF <= 4, "pipe6 is written for 3- to 5-deep rings");
+
+    const int nbm = (p.M + C::BM - 1) / C::BM;
+    const int nbn = (p.N + C::BN - 1) / C::BN;
+    const int tile = xcd_remap(blockIdx.x, gridDim.x);
+    int bm, bn;
+    tile_coords<GROUP_M>(tile, nbm, nbn, bm, bn);
+    const int m0 = bm * C::BM, n0 = bn * C::BN;
+
+    const bf16* src[C::PPW];
+    int dst[C::PPW];
+#pragma unroll
+    for (int q = 0; q < C::PPW; ++q) {
+        const int piece = wave * C::PPW + q;
+        const bool isA = piece < C::A_PIECES;
+        const int prow = (isA ? piece : piece - C::A_PIECES) * 16 + (lane >> 2);
+        const int logical = pswz(prow, lane & 3);
+        const int lm0 = DIAG == 5 ? 0 : m0, ln0 = DIAG == 5 ? 0 : n0;
+        if (isA)
+            src[q] = p.A + (size_t)min(lm0 + prow, p.M - 1) * p.lda + logical * 8;
+        else
+            src[q] = p.B + (size_t)min(ln0 + prow, p.N - 1) * p.ldb + logical * 8;
+        dst[q] = piece * 1024;
+    }
+    auto issue = [&](int st) {
+        char* base = lds + (st % C::NSTAGE) * C::STAGE;
+        const int k0 = st * C::BKS;
+        if (DIAG == 1) return;
+#pragma unroll
+        for (int q = 0; q < C::PPW; ++q) glds16(src[q] + k0, base + dst[q]);
+    };
+    const unsigned lds0 = (unsigned)(uintptr_t)(LDS_AS char*)lds;
+    const unsigned b_lane = lds0 + C::A_ST + (wn * C::TN + li) * 64 + (pswz(li, g) << 4);
+    const unsigned a_lane = lds0 + (wm * C::TM + li) * 64 + (pswz(li, g) << 4);
+
+    f32x4 acc[C::FM][C::FN];
+#pragma unroll
+    for (int i = 0; i < C::FM; ++i)
+#pragma unroll
+        for (int j = 0; j < C::FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    bf16x8 b[4], a[8];
+    const int nk = p.K / C::BKS;
+
+    // own DMA of stage s retired while `rem` later stages may stay in flight
+    auto wait_rem = [&](int rem) {
+        if (rem >= 3) vm_wait<3 * C::PPW>();
+        else if (rem == 2) vm_wait<2 * C::PPW>();
+        else if (rem == 1) vm_wait<C::PPW>();
+        else vm_wait<0>();
+    };
+    for (int st = 0; st < PF && st < nk; ++st) issue(st);
+    wait_rem(min(PF - 1, nk - 1));
+    __builtin_amdgcn_s_barrier();
+    if (STAG && wm == 1) __builtin_amdgcn_s_barrier();
+
+    for (int t = 0; t < nk; ++t) {
+        // ---- memory phase
+        const unsigned so = (t % C::NSTAGE) * C::STAGE;
+        const unsigned bb = b_lane + so, aa = a_lane + so;
+        if (DIAG != 3 && DIAG != 4 && DIAG != 5) {
+        ds_read16<0>(b[0], bb);
+        ds_read16<1024>(b[1], bb);
+        ds_read16<2048>(b[2], bb);
+        ds_read16<3072>(b[3], bb);
+        ds_read16<0>(a[0], aa);
+        ds_read16<1024>(a[1], aa);
+        ds_read16<2048>(a[2], aa);
+        ds_read16<3072>(a[3], aa);
+        ds_read16<4096>(a[4], aa);
+        ds_read16<5120>(a[5], aa);
+        ds_read16<6144>(a[6], aa);
+        ds_read16<7168>(a[7], aa);
+        }
+        if (t + PF < nk) {
+            issue(t + PF);
+            wait_rem(PF - 1);  // own stage t+1 landed; t+2 .. t+PF in flight
+        } else {
+            wait_rem(max(0, nk - 2 - t));
+        }
+        lgkm_wait<0>();
+        __builtin_amdgcn_s_barrier();
+        // ---- compute phase
+        __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+                if (DIAG == 2 || DIAG == 4 || DIAG == 5)
+                    asm volatile("" ::"v"(b[j]), "v"(a[i]));
+                else
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b[j], a[i], acc[i][j], 0, 0, 0);
+        __builtin_amdgcn_s_setprio(0);
+        __builtin_amdgcn_sched_barrier(0);
+        __builtin_amdgcn_s_barrier();
+    }
+    if (STAG && wm == 0) __builtin_amdgcn_s_barrier();
+
+    gemm_epilogue_lds<C, ACT>(p, lds, acc, m0, n0, wm, wn, g, li, tid);
+}
+
+template <class C, int GROUP_M, int STAG, int DIAG = 0>
+int launch_pipe6(const GemmArgs& a, hipStream_t s) {
+    const int nbm = (a.M + C::BM - 1) / C::BM, nbn = (a.N + C::BN - 1) / C::BN;
+    const dim3 grid(nbm * nbn), block(C::NT);
+    switch (a.act) {
+        case MME_ACT_GELU_TANH:
+            hipLaunchKernelGGL((gemm_pipe6_kernel<C, GROUP_M, MME_ACT_GELU_TANH, STAG, DIAG>), grid, block, 0, s, a);
+            break;
+        case MME_ACT_QUICK_GELU:
+            hipLaunchKernelGGL((gemm_pipe6_kernel<C, GROUP_M, MME_ACT_QUICK_GELU, STAG, DIAG>), grid, block, 0, s, a);
+            break;
+        case MME_ACT_GELU_ERF:
+            hipLaunchKernelGGL((gemm_pipe6_kernel<C, GROUP_M, MME_ACT_GELU_ERF, STAG, DIAG>), grid, block, 0, s, a);
+            break;
+        default:
+            hipLaunchKernelGGL((gemm_pipe6_kernel<C, GROUP_M, MME_ACT_NONE, STAG, DIAG>), grid, block, 0, s, a);
             break;
     }
     return mme_check_launch("mme_gemm");
@@ -594,6 +717,14 @@ extern "C" int mme_gemm(const void* A, int lda, const void* B, int ldb, void* Cp
         case 25: return launch_pipe4<Pipe256q, 8>(a, s);
         case 26: return launch_pipe4<Pipe256q, 4, 1>(a, s);  // diagnostic: no DMA
         case 27: return launch_pipe4<Pipe256q, 4, 2>(a, s);  // diagnostic: no MFMA
+        case 30: return launch_pipe6<Pipe256, 4, 1>(a, s);
+        case 31: return launch_pipe6<Pipe256, 4, 0>(a, s);
+        case 32: return launch_pipe6<Pipe256, 8, 1>(a, s);
+        case 33: return launch_pipe6<Pipe256, 4, 1, 1>(a, s);  // diagnostic: no DMA
+        case 34: return launch_pipe6<Pipe256, 4, 1, 2>(a, s);  // diagnostic: no MFMA
+        case 35: return launch_pipe6<Pipe256, 4, 1, 3>(a, s);  // diagnostic: no ds_read
+        case 36: return launch_pipe6<Pipe256, 4, 1, 4>(a, s);  // diagnostic: DMA + barriers only
+        case 37: return launch_pipe6<Pipe256, 4, 1, 5>(a, s);  // diagnostic: DMA of one L2-resident tile
         default: break;
     }
     // production dispatch: the pipelined 256x256 kernel whenever its 16-byte
@@ -601,7 +732,7 @@ extern "C" int mme_gemm(const void* A, int lda, const void* B, int ldb, void* Cp
     const bool vec_ok = !out_f32 && ldc % 8 == 0 && ((uintptr_t)Cp & 15) == 0 &&
                         (!residual || (ldr % 8 == 0 && ((uintptr_t)residual & 15) == 0)) && N % 8 == 0;
     if (vec_ok && (long)M * N >= 1024L * 1024) {
-        return launch_pipe4<Pipe256q, 4>(a, s);
+        return launch_pipe6<Pipe256, 4, 1>(a, s);
     }
     if ((long)M * N >= 2048L * 1024) return launch<BigCfg, 1>(a, s);
     return launch<SmallCfg, 8>(a, s);
