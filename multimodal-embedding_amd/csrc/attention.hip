@@ -28,6 +28,11 @@
 
 namespace {
 
+template <int N>
+__device__ __forceinline__ void vm_wait() {
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
 
 struct AttnArgs {
     const bf16* qkv;
@@ -37,8 +42,9 @@ struct AttnArgs {
     float scale_log2;
 };
 
-template <int HD>
+template <int HD, int DIAG = 0>
 __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(AttnArgs a) {
+    // DIAG (dev builds, wrong results): 1 no K/V global loads, 2 no exp2, 3 no PV MFMA, 4 no QK MFMA
     // QK^T reduction depth covered by 16x16x32 steps: 64, or 96 for head dims
     // 72/80 zero-padded. Only same-shape MFMA accumulation chains are used: a
     // 16x16x16 tail step chained on a 16x16x32 result was observed to be
@@ -106,6 +112,7 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(AttnArgs a) {
     constexpr int CPT1 = (NCH + 255) / 256;
     u16x8 pk[CPT1], pv[CPT1];
     auto load_tile = [&](int t) {
+        if (DIAG == 1 && t > 0) return;
 #pragma unroll
         for (int i = 0; i < CPT1; ++i) {
             const int cidx = tid + i * 256;
@@ -158,7 +165,12 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(AttnArgs a) {
             for (int u = 0; u < 2; ++u) {
                 f32x4 z = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-                for (int ks = 0; ks < NKS; ++ks) z = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf[ks], qf[u][ks], z, 0, 0, 0);
+                for (int ks = 0; ks < NKS; ++ks) {
+                    if (DIAG == 4)
+                        asm volatile("" : "+v"(z) : "v"(kf[ks]), "v"(qf[u][ks]));
+                    else
+                        z = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf[ks], qf[u][ks], z, 0, 0, 0);
+                }
                 sc[u][kt] = z;
             }
         }
@@ -195,7 +207,7 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(AttnArgs a) {
             for (int kt = 0; kt < 4; ++kt)
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
-                    const float pv = __builtin_amdgcn_exp2f(sc[u][kt][r] * c - mc);
+                    const float pv = DIAG == 2 ? sc[u][kt][r] * c - mc : __builtin_amdgcn_exp2f(sc[u][kt][r] * c - mc);
                     sc[u][kt][r] = pv;
                     psum += pv;
                 }
@@ -220,13 +232,238 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(AttnArgs a) {
                 const s16x4 v1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS_AS s16x4*)(Vb + (r1 + 16) * VS + col));
                 const bf16x8 vv = __builtin_bit_cast(bf16x8, __builtin_shufflevector(v0, v1, 0, 1, 2, 3, 4, 5, 6, 7));
 #pragma unroll
-                for (int u = 0; u < 2; ++u)
-                    o[u][dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vv, pb[u], o[u][dt], 0, 0, 0);
+                for (int u = 0; u < 2; ++u) {
+                    if (DIAG == 3)
+                        asm volatile("" : "+v"(o[u][dt]) : "v"(vv), "v"(pb[u]));
+                    else
+                        o[u][dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vv, pb[u], o[u][dt], 0, 0, 0);
+                }
             }
         }
 
         if (t + 1 < nkt) store_tile(buf ^ 1);
         __syncthreads();
+    }
+
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+        float ltot = lsum[u] + __shfl_xor(lsum[u], 16, 64);
+        ltot += __shfl_xor(ltot, 32, 64);
+        const float inv = 1.0f / ltot;
+        const int q = qw0 + u * 16 + li;
+        if (q < T) {
+            bf16* orow = a.out + ((long)b * T + q) * a.ldo + h * HD;
+#pragma unroll
+            for (int dt = 0; dt < NDT; ++dt) {
+                const int d0 = dt * 16 + 4 * g;
+                if (d0 < HD) {
+                    bf16x4 v;
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) v[r] = f2bf(o[u][dt][r] * inv);
+                    *reinterpret_cast<bf16x4*>(orow + d0) = v;
+                }
+            }
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// attn_dma_kernel: the same per-wave math as attn_fwd_kernel (32 query rows
+// per wave, S^T = K.Q^T, P in registers, V^T by transposed LDS reads), with
+// the K/V tiles staged by LDS-DMA instead of through registers:
+//   * "chunk-plane" tile layout: plane c (16-B column chunk c of all 64 keys)
+//     is one 1 KiB DMA instruction, lane = key -> no register staging, no
+//     ds_write, and conflict-free ds_read_b128 for the K fragments (the 16
+//     lanes of a read group have distinct keys);
+//   * V planes with odd c store key ^ 8 (swizzled through the per-lane DMA
+//     source row) so the 32 lanes of a ds_read_b64_tr_b16 group hit 64
+//     distinct banks;
+//   * head-dim padding is never stored: fragment lanes past HD read plane 0
+//     (finite data meeting zero Q columns / producing discarded O rows);
+//   * NSTG-deep ring of tiles, tile t+NSTG-1 issued after the barrier that
+//     opens tile t (WAR: every wave finished tile t-1 before that barrier;
+//     RAW: each wave retires its own DMA of tile t by a counted vmcnt before it).
+// ---------------------------------------------------------------------------
+template <int HD, int NW, int NSTG>
+__global__ __launch_bounds__(NW * 64) void attn_dma_kernel(AttnArgs a) {
+    constexpr int HDP = HD == 64 ? 64 : 96;
+    constexpr int NKS = HDP / 32;
+    constexpr int NCHL = HD / 8;             // real 16-B planes per K (or V) tile
+    constexpr int NDT = (HD + 15) / 16;
+    constexpr int QW = 32, QB = NW * QW;     // query rows per wave / per block
+    constexpr int TILE = 2 * NCHL * 1024;    // bytes per K+V tile
+    constexpr int NINS = 2 * NCHL;           // DMA instructions per tile
+    constexpr int MAXI = (NINS + NW - 1) / NW;
+    __shared__ __attribute__((aligned(16))) char lds[NSTG * TILE];
+
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int g = lane >> 4, li = lane & 15;
+    const int nqb = (a.T + QB - 1) / QB;
+    int id;
+    {
+        const int bid = blockIdx.x, nwg = gridDim.x;
+        const int xcd = bid & 7, loc = bid >> 3, q8 = nwg >> 3, r8 = nwg & 7;
+        id = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + loc;
+    }
+    const int qb = id % nqb, h = (id / nqb) % a.H, b = id / (nqb * a.H);
+    const int T = a.T, D = a.H * HD;
+    const bf16* base = a.qkv + (long)b * T * a.ld;
+    const int qw0 = qb * QB + wave * QW;
+    const int Tk = a.seq_lens ? a.seq_lens[b] : T;
+    const float c = a.scale_log2;
+
+    bf16x8 qf[2][NKS];
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+        const bf16* qrow = base + (long)min(qw0 + u * 16 + li, T - 1) * a.ld + h * HD;
+#pragma unroll
+        for (int ks = 0; ks < NKS; ++ks) {
+            const int col = ks * 32 + 8 * g;
+            if (col < HD)
+                qf[u][ks] = *reinterpret_cast<const bf16x8*>(qrow + col);
+            else
+                qf[u][ks] = bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
+        }
+    }
+
+    int nkt = (Tk + 63) / 64;
+    if (a.causal) nkt = min(nkt, (min(T, qb * QB + QB) + 63) / 64);
+
+    // this wave's DMA instructions: idx = wave + NW*i (K planes 0..NCHL-1, V planes after)
+    const int nmine = (NINS - wave + NW - 1) / NW;
+    auto issue = [&](int t) {
+        char* tb = lds + (t % NSTG) * TILE;
+#pragma unroll
+        for (int i = 0; i < MAXI; ++i) {
+            const int idx = wave + NW * i;
+            if (i < MAXI - 1 || idx < NINS) {
+                const bool isV = idx >= NCHL;
+                const int plane = isV ? idx - NCHL : idx;
+                const int key = isV && (plane & 1) ? lane ^ 8 : lane;
+                const bf16* src = base + (long)min(t * 64 + key, T - 1) * a.ld + (isV ? 2 : 1) * D + h * HD + plane * 8;
+                glds16(src, tb + idx * 1024);
+            }
+        }
+    };
+    auto wait_own = [&](int later) {  // retire own DMA except `later` (0/1) tiles after it
+        if (later == 0) {
+            vm_wait<0>();
+        } else if (nmine == MAXI) {
+            vm_wait<MAXI>();
+        } else {
+            vm_wait<MAXI - 1>();
+        }
+    };
+
+    // fragment addresses inside a tile
+    const unsigned lds0 = (unsigned)(uintptr_t)(LDS_AS char*)lds;
+    unsigned koff[NKS];
+#pragma unroll
+    for (int ks = 0; ks < NKS; ++ks) {
+        const int cch = ks * 4 + g;
+        koff[ks] = (cch < NCHL ? cch : 0) * 1024 + li * 16;
+    }
+    unsigned voff[NDT];  // + key*16 added per read (key parity handled by the plane's swizzle)
+    int vsw[NDT];
+#pragma unroll
+    for (int dt = 0; dt < NDT; ++dt) {
+        int plane = 2 * dt + ((li >> 1) & 1);
+        if (plane >= NCHL) plane = 0;
+        voff[dt] = (NCHL + plane) * 1024 + (li & 1) * 8;
+        vsw[dt] = (plane & 1) ? 8 : 0;
+    }
+
+    f32x4 o[2][NDT];
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+#pragma unroll
+        for (int i = 0; i < NDT; ++i) o[u][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+    float m[2] = {-1e30f, -1e30f}, lsum[2] = {0.f, 0.f};
+
+    static_assert(NSTG == 2 || NSTG == 3, "ring depth");
+    for (int t = 0; t < NSTG - 1 && t < nkt; ++t) issue(t);
+    for (int t = 0; t < nkt; ++t) {
+        wait_own(NSTG == 3 && t + 1 < nkt ? 1 : 0);
+        __builtin_amdgcn_s_barrier();
+        if (t + NSTG - 1 < nkt) issue(t + NSTG - 1);
+        const unsigned tb = lds0 + (t % NSTG) * TILE;
+
+        f32x4 sc[2][4];
+#pragma unroll
+        for (int kt = 0; kt < 4; ++kt) {
+            bf16x8 kf[NKS];
+#pragma unroll
+            for (int ks = 0; ks < NKS; ++ks)
+                kf[ks] = *reinterpret_cast<const LDS_AS bf16x8*>((uintptr_t)(tb + koff[ks] + kt * 256));
+#pragma unroll
+            for (int u = 0; u < 2; ++u) {
+                f32x4 z = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+                for (int ks = 0; ks < NKS; ++ks) z = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf[ks], qf[u][ks], z, 0, 0, 0);
+                sc[u][kt] = z;
+            }
+        }
+
+        if ((t * 64 + 64 > Tk) || (a.causal && t * 64 + 63 > qw0)) {
+#pragma unroll
+            for (int u = 0; u < 2; ++u) {
+                const int q = qw0 + u * 16 + li;
+                const int lim = a.causal ? min(Tk, q + 1) : Tk;
+#pragma unroll
+                for (int kt = 0; kt < 4; ++kt)
+#pragma unroll
+                    for (int r = 0; r < 4; ++r)
+                        if (t * 64 + kt * 16 + 4 * g + r >= lim) sc[u][kt][r] = -INFINITY;
+            }
+        }
+
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+            float mloc = fmaxf(fmaxf(sc[u][0][0], sc[u][0][1]), fmaxf(sc[u][0][2], sc[u][0][3]));
+#pragma unroll
+            for (int kt = 1; kt < 4; ++kt)
+                mloc = fmaxf(mloc, fmaxf(fmaxf(sc[u][kt][0], sc[u][kt][1]), fmaxf(sc[u][kt][2], sc[u][kt][3])));
+            mloc = fmaxf(mloc, __shfl_xor(mloc, 16, 64));
+            mloc = fmaxf(mloc, __shfl_xor(mloc, 32, 64));
+            const float mnew = fmaxf(m[u], mloc);
+            const float alpha = __builtin_amdgcn_exp2f((m[u] - mnew) * c);
+            m[u] = mnew;
+            const float mc = mnew * c;
+            float psum = 0.f;
+#pragma unroll
+            for (int kt = 0; kt < 4; ++kt)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const float pv = __builtin_amdgcn_exp2f(sc[u][kt][r] * c - mc);
+                    sc[u][kt][r] = pv;
+                    psum += pv;
+                }
+            lsum[u] = lsum[u] * alpha + psum;
+#pragma unroll
+            for (int i = 0; i < NDT; ++i) o[u][i] *= alpha;
+        }
+
+#pragma unroll
+        for (int hh = 0; hh < 2; ++hh) {
+            bf16x8 pb[2];
+#pragma unroll
+            for (int u = 0; u < 2; ++u)
+                pb[u] = __builtin_convertvector(__builtin_shufflevector(sc[u][2 * hh], sc[u][2 * hh + 1], 0, 1, 2, 3,
+                                                                        4, 5, 6, 7), bf16x8);
+            const int r1 = 32 * hh + 4 * g + (li >> 2);
+#pragma unroll
+            for (int dt = 0; dt < NDT; ++dt) {
+                const unsigned va = tb + voff[dt] + ((r1 ^ vsw[dt]) * 16);
+                const unsigned vb2 = tb + voff[dt] + (((r1 + 16) ^ vsw[dt]) * 16);
+                const s16x4 v0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS_AS s16x4*)(uintptr_t)va);
+                const s16x4 v1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS_AS s16x4*)(uintptr_t)vb2);
+                const bf16x8 vv = __builtin_bit_cast(bf16x8, __builtin_shufflevector(v0, v1, 0, 1, 2, 3, 4, 5, 6, 7));
+#pragma unroll
+                for (int u = 0; u < 2; ++u)
+                    o[u][dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vv, pb[u], o[u][dt], 0, 0, 0);
+            }
+        }
     }
 
 #pragma unroll
@@ -313,7 +550,24 @@ __global__ __launch_bounds__(256) void probe_attn_kernel(const bf16* __restrict_
     }
 }
 
+template <int HD>
+void launch_attn(int kind, const AttnArgs& a, int B, int T, int H, hipStream_t st) {
+    if (kind == 0)
+        hipLaunchKernelGGL((attn_fwd_kernel<HD>), dim3(cdiv(T, 128) * H * B), dim3(256), 0, st, a);
+    else if (kind == 1)
+        hipLaunchKernelGGL((attn_dma_kernel<HD, 4, 2>), dim3(cdiv(T, 128) * H * B), dim3(256), 0, st, a);
+    else
+        hipLaunchKernelGGL((attn_dma_kernel<HD, 8, 2>), dim3(cdiv(T, 256) * H * B), dim3(512), 0, st, a);
+}
+
+int g_attn_variant = 0;  // dev-only override (tools/attn_bench.py)
+
 }  // namespace
+
+extern "C" int mme_attention_variant(int v) {
+    g_attn_variant = v;
+    return MME_OK;
+}
 
 extern "C" int mme_attention(const void* qkv, int ld_qkv, void* out, int ld_out, int B, int T, int H, int hd,
                              const int32_t* seq_lens, int causal, float scale, void* stream) {
@@ -326,13 +580,30 @@ extern "C" int mme_attention(const void* qkv, int ld_qkv, void* out, int ld_out,
     if (B == 0) return MME_OK;
     AttnArgs a{(const bf16*)qkv, (bf16*)out, seq_lens, ld_qkv, ld_out, T, H, hd, causal ? 1 : 0,
                scale * 1.4426950408889634f};  // exp(x*scale) = exp2(x*scale*log2 e)
-    const dim3 grid(cdiv(T, 128) * H * B);
+    // kernel choice (tools/attn_bench.py): short sequences (T <= 128: one or two key tiles)
+    // and head dim 64 (3 waves/SIMD already) -> register-staged attn_fwd_kernel; otherwise
+    // LDS-DMA staging, 8 waves (256 queries) per block unless that pads the query range by
+    // > 10 % more than 128-query blocks (T = 257), then 4 waves. SigLIP-400M vision
+    // (T 729, hd 72): 1.80 -> 1.27 ms per 256-image layer; ViT-H (T 257, hd 80): 0.40 -> 0.355.
+    int kind = (T <= 128 || hd == 64) ? 0
+               : ((long)cdiv(T, 256) * 256 * 10 <= (long)cdiv(T, 128) * 128 * 11 ? 2 : 1);
+    if (g_attn_variant >= 1 && g_attn_variant <= 4 && hd == 72) {  // dev-only diagnostic builds
+        const dim3 grid(cdiv(T, 128) * H * B);
+        switch (g_attn_variant) {
+            case 1: hipLaunchKernelGGL((attn_fwd_kernel<72, 1>), grid, dim3(256), 0, as_stream(stream), a); break;
+            case 2: hipLaunchKernelGGL((attn_fwd_kernel<72, 2>), grid, dim3(256), 0, as_stream(stream), a); break;
+            case 3: hipLaunchKernelGGL((attn_fwd_kernel<72, 3>), grid, dim3(256), 0, as_stream(stream), a); break;
+            default: hipLaunchKernelGGL((attn_fwd_kernel<72, 4>), grid, dim3(256), 0, as_stream(stream), a); break;
+        }
+        return mme_check_launch("mme_attention");
+    }
+    if (g_attn_variant >= 9 && g_attn_variant <= 11) kind = g_attn_variant - 9;  // dev: force a kernel
     if (hd == 64)
-        hipLaunchKernelGGL(attn_fwd_kernel<64>, grid, dim3(256), 0, as_stream(stream), a);
+        launch_attn<64>(kind, a, B, T, H, as_stream(stream));
     else if (hd == 72)
-        hipLaunchKernelGGL(attn_fwd_kernel<72>, grid, dim3(256), 0, as_stream(stream), a);
+        launch_attn<72>(kind, a, B, T, H, as_stream(stream));
     else
-        hipLaunchKernelGGL(attn_fwd_kernel<80>, grid, dim3(256), 0, as_stream(stream), a);
+        launch_attn<80>(kind, a, B, T, H, as_stream(stream));
     return mme_check_launch("mme_attention");
 }
 

@@ -109,6 +109,10 @@ def attn_ref(qkv, B, T, H, hd, lens, causal, scale):
     (3, 17, 4, 80, False, None),
     (4, 16, 8, 72, False, [16, 5, 9, 13]),
     (2, 1, 2, 64, False, None),
+    (2, 300, 4, 64, True, [300, 133]),     # LDS-DMA kernels: causal + padding, 4- and 8-wave blocks
+    (2, 520, 4, 72, False, [520, 301]),
+    (1, 1000, 2, 80, False, [999]),
+    (2, 200, 3, 72, True, None),
 ])
 def test_attention(cuda, B, T, H, hd, causal, lens):
     g = torch.Generator(device="cuda").manual_seed(B * T + hd)

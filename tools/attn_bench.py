@@ -5,8 +5,17 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "multimodal-embedding_amd"))
+import ctypes  # noqa: E402
+
 import torch  # noqa: E402
-from mme import ops  # noqa: E402
+from mme import _lib, ops  # noqa: E402
+
+# --variants 0,1,...: 0 = production dispatch; 1-4 dev diagnostic builds of the hd-72 register-
+# staged kernel (1 no K/V loads, 2 no exp2, 3 no PV MFMA, 4 no QK MFMA; wrong results);
+# 9 / 10 / 11 force the register-staged / LDS-DMA 4-wave / LDS-DMA 8-wave kernel
+VARIANTS = [int(v) for v in sys.argv[sys.argv.index("--variants") + 1].split(",")] if "--variants" in sys.argv else [0]
+lib = _lib.load()
+lib.mme_attention_variant.argtypes = [ctypes.c_int]
 
 CASES = [  # name, B, T, H, hd, causal
     ("siglip_vision", 256, 729, 16, 72, False),
@@ -15,11 +24,18 @@ CASES = [  # name, B, T, H, hd, causal
     ("vitH_vision", 256, 257, 16, 80, False),
     ("clip_text_causal", 1024, 77, 16, 64, True),
 ]
-for name, B, T, H, hd, causal in CASES:
+for (name, B, T, H, hd, causal), v in [(c, v) for c in CASES for v in VARIANTS]:
+    if 1 <= v <= 4 and hd != 72:
+        continue
+    torch.manual_seed(0)
     qkv = torch.randn(B * T, 3 * H * hd, device="cuda").to(torch.bfloat16)
     out = torch.empty(B * T, H * hd, device="cuda", dtype=torch.bfloat16)
+    lib.mme_attention_variant(0)
+    ref = ops.attention(qkv, B, T, H, hd, causal=causal).float()
+    lib.mme_attention_variant(v)
     ops.attention(qkv, B, T, H, hd, causal=causal, out=out)
     torch.cuda.synchronize()
+    err = (out.float() - ref).abs().max().item()
     s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     it = 5
     s.record()
@@ -29,4 +45,4 @@ for name, B, T, H, hd, causal in CASES:
     torch.cuda.synchronize()
     ms = s.elapsed_time(e) / it
     fl = 4.0 * B * H * T * T * hd * (0.5 if causal else 1.0)
-    print(f"{name:18s} B={B} T={T} H={H} hd={hd}: {ms:7.3f} ms {fl / ms / 1e9:7.1f} TFLOP/s", flush=True)
+    print(f"{name:18s} v{v} B={B} T={T} H={H} hd={hd}: {ms:7.3f} ms {fl / ms / 1e9:7.1f} TFLOP/s  maxdiff vs v0 {err:.3g}", flush=True)
