@@ -35,6 +35,7 @@ import torch.distributed as dist  # noqa: E402
 
 A40_PUBLISHED_IMG_S = 47.1  # SigLIP-400M end-to-end img/s, A40 bf16 bs32
 MFMA_BF16_PEAK_TFLOPS = 2500.0  # MI355X_MICROARCH.md: dense bf16 MFMA
+MFMA_FP8_PEAK_TFLOPS = 5000.0  # dense fp8 (block-scaled f8f6f4 MFMA)
 HBM_PEAK_GBS = 8000.0
 
 
@@ -51,6 +52,8 @@ def parse():
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline sample duration")
     p.add_argument("--no-kernel-timer", action="store_true")
+    p.add_argument("--fp8", action="store_true",
+                   help="mx8 encoder GEMMs (BASELINE configs[4]: DFN5B-H fp8 weights on the fp8 MFMA)")
     return p.parse_args()
 
 
@@ -116,7 +119,7 @@ def main():
     from mme.models import load_model
 
     spec = get_spec(args.model)
-    model, _ = load_model(args.model, seed=0, device=dev)
+    model, _ = load_model(args.model, seed=0, device=dev, fp8=args.fp8)
     n, caps = args.n_images, args.caps
     imgs, ids = synth_inputs(spec, n, caps, dev)
     lo, hi = shard_range(n, rank, world)
@@ -156,22 +159,30 @@ def main():
     kt = ops.KernelTimer.summary() if not args.no_kernel_timer else {}
 
     roofline = None
-    if "gemm" in kt:
-        # dominant kernel family: mme_gemm (gemm_pipe6_kernel; gemm_tn_kernel for the few small shapes).
+    fam = "gemm_mx" if args.fp8 else "gemm"
+    if fam in kt:
+        # dominant kernel family: mme_gemm (gemm_pipe6_kernel; gemm_tn_kernel for the few small shapes),
+        # or with --fp8 mme_gemm_mx (gemm_mx_kernel, block-scaled fp8 MFMA; dense fp8 peak).
         # achieved = algorithmic FLOPs per launch (2*M*N*K, zero-padding excluded) / average launch time
         # from HIP events recorded on the launch stream over the timed region.
-        g = kt["gemm"]
+        g = kt[fam]
         avg_ms = g["ms"] / g["launches"]
         achieved = g["flops"] / (g["ms"] / 1e3) / 1e12
-        roofline = {"bound": "mfma", "kernel": "mme_gemm (gemm_pipe6_kernel)", "achieved": round(achieved, 1),
-                    "peak": MFMA_BF16_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": round(achieved / MFMA_BF16_PEAK_TFLOPS, 4),
+        peak = MFMA_FP8_PEAK_TFLOPS if args.fp8 else MFMA_BF16_PEAK_TFLOPS
+        roofline = {"bound": "mfma",
+                    "kernel": "mme_gemm_mx (gemm_mx_kernel)" if args.fp8 else "mme_gemm (gemm_pipe6_kernel)",
+                    "achieved": round(achieved, 1), "peak": peak, "unit": "TFLOP/s", "frac": round(achieved / peak, 4),
                     "traffic": None, "launches": g["launches"], "avg_launch_ms": round(avg_ms, 4),
                     "algorithmic_bytes_per_launch": round(g["bytes"] / g["launches"]),
                     "share_of_step_time": round(g["ms"] / 1e3 / dt, 3)}
+        if args.fp8 and "gemm" in kt:
+            b = kt["gemm"]
+            roofline["bf16_gemm_tflops"] = round(b["flops"] / (b["ms"] / 1e3) / 1e12, 1)
+            roofline["bf16_gemm_share"] = round(b["ms"] / 1e3 / dt, 3)
         # HBM bytes per launch from the rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes (tools/pmc_gemm.sh,
         # gfx950-corrected by tools/pmc_summary.py) of the same launch shapes
         pmc = os.path.join(ROOT, "profiles", "gemm_traffic.json")
-        if os.path.exists(pmc):
+        if os.path.exists(pmc) and not args.fp8:
             try:
                 roofline["traffic"] = round(json.load(open(pmc))["mme_gemm"]["hbm_bytes_per_launch"])
             except (KeyError, ValueError, TypeError):
@@ -193,7 +204,7 @@ def main():
         "higher_is_better": True,
         "scaling": "strong",  # total job fixed (5k images) as N grows
         "vs_baseline": round(value / A40_PUBLISHED_IMG_S, 2) if (args.model == "SigLIP-400M" and n == 5000) else None,
-        "dtype": "bf16",
+        "dtype": "mx-fp8 (e4m3 + e8m0/32) QKV/MLP GEMMs, bf16 elsewhere" if args.fp8 else "bf16",
         "data": "synthetic (u8 224x224x3 images, token-id captions L=%d; seeded random weights)" % spec.text.max_pos,
         "config": {"workload": f"{args.model}: {n} images x {caps * n} captions (+{n} T2I), encode + sim + top-10 "
                                f"recall", "n_images": n, "n_captions": caps * n, "image_in": "224x224x3 u8",

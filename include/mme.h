@@ -35,7 +35,7 @@ extern "C" {
 #define MME_ERR_HIP 2         /* HIP runtime error at launch               */
 #define MME_ERR_UNSUPPORTED 3 /* valid request this build does not handle  */
 
-#define MME_ABI_VERSION 1
+#define MME_ABI_VERSION 2
 
 /* activation codes for mme_gemm (HF config.hidden_act) */
 #define MME_ACT_NONE 0
@@ -166,6 +166,32 @@ size_t mme_maxsim_workspace_bytes(int nq, int Lq, int nd);
 int mme_maxsim(const void* Q, const int32_t* q_lens, int nq, int Lq, const void* D, const int32_t* d_lens,
                const uint8_t* d_zero, int nd, int Ld, int dim, float* out, void* workspace, size_t ws_bytes,
                void* stream);
+
+/* ------------------------------------------------------- config 5: fp8 ----
+ * MX-fp8 encoder GEMMs ("Apple-DFN5B-H fp8 weights on CDNA4 fp8 MFMA",
+ * BASELINE.json configs[4]; the reference runs the same CLIP layers in bf16,
+ * TF:models/clip/modeling_clip.py CLIPAttention q/k/v + CLIPMLP fc1/fc2).
+ * mx8 tensor: values u8 [rows][k] e4m3fn (row stride ld bytes) + E8M0 scale
+ * bytes [k/32][rows_pad] (block-major planes, rows_pad % 256 == 0);
+ * element (r,c) = e4m3(q[r][c]) * 2^(S[c/32][r] - 127). Block rule: absmax a,
+ * S = clamp(expfield(a) - 8 + (mantissa(a) > 0x600000), 1, 254) (127 when a == 0),
+ * q = RNE_e4m3(clamp(x * 2^(127-S), +-448)).  */
+
+/* bf16 rows [rows, k] (k % 32 == 0) -> mx8. */
+int mme_mx_quant(const void* x, int ldx, int rows, int k, void* q, int ldq, void* scales, int rows_pad, void* stream);
+
+/* mme_layernorm (same statistics, output rounded to bf16) -> mx8 (d % 32 == 0). */
+int mme_layernorm_mx(const void* x, int ldx, const void* gamma, const void* beta, int rows, int d, float eps,
+                     const int32_t* rows_idx, void* q, int ldq, void* scales, int rows_pad, void* stream);
+
+/* C = act(A . B^T + bias) (+ residual[row % res_period or row]) with A [M,K], B [N,K] in mx8
+ * (sa_rows / sb_rows = their planes' rows_pad), fp32 accumulation on the block-scaled
+ * MFMA. out_mx == 0: C bf16 [M, ldc elements]; out_mx == 1: C re-quantised to mx8
+ * (values [M, ldc bytes], scale planes c_scales with c_rows_pad rows; N % 32 == 0, no
+ * residual) -- fc1's output as fc2's operand. K % 64 == 0, lda/ldb % 16 == 0. */
+int mme_gemm_mx(const void* A, int lda, const void* sa, int sa_rows, const void* B, int ldb, const void* sb,
+                int sb_rows, void* C, int ldc, void* c_scales, int c_rows_pad, int M, int N, int K, const void* bias,
+                const void* residual, int ldr, int res_period, int act, int out_mx, void* stream);
 
 #ifdef __cplusplus
 }

@@ -37,26 +37,6 @@ struct GemmArgs {
     int res_period, act, out_f32;
 };
 
-// Tile order: XCD remap (each XCD gets a contiguous range of tile ids), then
-// GROUP_M-row bands walked column-major inside the band, so the 32 tiles an
-// XCD runs concurrently form a GROUP_M x (32/GROUP_M) patch that shares A row
-// panels and B column panels in that XCD's L2.
-template <int GROUP_M>
-__device__ __forceinline__ void tile_coords(int tile, int nbm, int nbn, int& bm, int& bn) {
-    if (GROUP_M <= 1) {
-        bm = tile / nbn;
-        bn = tile % nbn;
-        return;
-    }
-    const int per_group = GROUP_M * nbn;
-    const int gid = tile / per_group;
-    const int first_m = gid * GROUP_M;
-    const int gsz = min(nbm - first_m, GROUP_M);
-    const int r = tile % per_group;
-    bm = first_m + r % gsz;
-    bn = r / gsz;
-}
-
 template <class C, int GROUP_M>
 __global__ __launch_bounds__(C::NT) void gemm_tn_kernel(GemmArgs p) {
     __shared__ __attribute__((aligned(16))) char lds[C::LDS];
@@ -129,10 +109,6 @@ __global__ __launch_bounds__(C::NT) void gemm_tn_kernel(GemmArgs p) {
 // tile needs 1 KiB per 128 KFLOP, so the staging path, overlapped with the
 // MFMAs, sets the ~1.1 PF/s these kernels reach; ring depth 3/4/5 is neutral.
 // ---------------------------------------------------------------------------
-template <int N>
-__device__ __forceinline__ void vm_wait() {
-    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
-}
 
 __device__ __forceinline__ int pswz(int row, int chunk) { return chunk ^ (3 * ((row >> 3) & 1)); }
 
@@ -151,16 +127,6 @@ struct PCfg {
     static_assert(PPW * NW == PIECES, "stage must split evenly into 1 KiB pieces per wave");
 };
 
-// pipe3 / pipe4 helpers: counted lgkm waits and inline-asm fragment reads.
-template <int N>
-__device__ __forceinline__ void lgkm_wait() {
-    asm volatile("s_waitcnt lgkmcnt(%0)" ::"n"(N) : "memory");
-    __builtin_amdgcn_sched_barrier(0);
-}
-template <int OFF>
-__device__ __forceinline__ void ds_read16(bf16x8& r, unsigned addr) {
-    asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(r) : "v"(addr), "n"(OFF));
-}
 
 // Shared epilogue of the pipelined kernels: bias + activation in registers,
 // bf16 tile staged in LDS (row pitch BN*2+16 B), 16-B stores with the

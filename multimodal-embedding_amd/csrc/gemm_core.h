@@ -32,6 +32,43 @@ __device__ __forceinline__ int xcd_remap(int bid, int nwg) {
     return start + loc;
 }
 
+// Tile order: XCD remap (each XCD gets a contiguous range of tile ids), then
+// GROUP_M-row bands walked column-major inside the band, so the 32 tiles an
+// XCD runs concurrently form a GROUP_M x (32/GROUP_M) patch that shares A row
+// panels and B column panels in that XCD's L2.
+template <int GROUP_M>
+__device__ __forceinline__ void tile_coords(int tile, int nbm, int nbn, int& bm, int& bn) {
+    if (GROUP_M <= 1) {
+        bm = tile / nbn;
+        bn = tile % nbn;
+        return;
+    }
+    const int per_group = GROUP_M * nbn;
+    const int gid = tile / per_group;
+    const int first_m = gid * GROUP_M;
+    const int gsz = min(nbm - first_m, GROUP_M);
+    const int r = tile % per_group;
+    bm = first_m + r % gsz;
+    bn = r / gsz;
+}
+
+// Pipelined-kernel helpers: counted vmcnt / lgkmcnt waits (immediates) and
+// inline-asm fragment reads (hipcc's waitcnt pass would otherwise drain
+// lgkmcnt(0) at loop heads).
+template <int N>
+__device__ __forceinline__ void vm_wait() {
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+template <int N>
+__device__ __forceinline__ void lgkm_wait() {
+    asm volatile("s_waitcnt lgkmcnt(%0)" ::"n"(N) : "memory");
+    __builtin_amdgcn_sched_barrier(0);
+}
+template <int OFF>
+__device__ __forceinline__ void ds_read16(bf16x8& r, unsigned addr) {
+    asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(r) : "v"(addr), "n"(OFF));
+}
+
 template <class C>
 __device__ __forceinline__ void stage_tile(const bf16* __restrict__ A, int lda, int M, int m0,
                                            const bf16* __restrict__ B, int ldb, int N, int n0, int k0,

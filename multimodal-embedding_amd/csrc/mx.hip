@@ -1,0 +1,478 @@
+// MX-fp8 (OCP e4m3 values + E8M0 scales per 32-element block) path for the
+// encoder GEMMs: quantisers and the block-scaled fp8 MFMA GEMM.
+//
+// This is the "fp8 weights on CDNA4 fp8 MFMA" configuration of BASELINE.json
+// (Apple-DFN5B-H, config 5): the reference runs these layers in bf16
+// (TF:models/clip/modeling_clip.py CLIPMLP / CLIPAttention q,k,v projections);
+// here the QKV, fc1 and fc2 products of every encoder layer run on
+// v_mfma_scale_f32_32x32x64_f8f6f4 (2x the bf16 MFMA rate) with both operands
+// in MX-fp8 and the block scales applied by the MFMA itself.
+//
+// MX tensor format ("mx8"), shared with the host (mme/mx.py) and the oracle
+// (oracle/mx.py): values u8 [R][K] (row stride ld bytes, e4m3fn), scales u8
+// [K/32][rows_pad] block-major "scale planes" (rows_pad a multiple of 256,
+// so one 256-row GEMM tile's scales of one block are 256 contiguous bytes).
+// Element (r, k) = e4m3(q[r][k]) * 2^(S[k/32][r] - 127).
+//
+// Quantisation of a block with absmax a (bf16 inputs, exact in fp32):
+//   a == 0          -> scale byte 127, all values 0
+//   otherwise       -> scale byte e = clamp(expfield(a) - 8 + (mantissa(a) > 0x600000), 1, 254),
+//                      the smallest power of two with a * 2^-(e-127) <= 448;
+//                      q = RNE_e4m3(clamp(x * 2^-(e-127), -448, 448))
+// (v_cvt_pk_fp8_f32 is RNE once the input is clamped: tools/probes/fp8_probe.hip).
+#include "gemm_core.h"
+
+namespace {
+using namespace gemmcore;
+
+typedef int i32x8 __attribute__((ext_vector_type(8)));
+
+__device__ __forceinline__ int mx_scale_byte(float amax) {
+    if (amax == 0.f) return 127;
+    const unsigned u = __float_as_uint(amax);
+    const int e = (int)((u >> 23) & 255) - 8 + ((u & 0x7fffff) > 0x600000 ? 1 : 0);
+    return min(254, max(1, e));
+}
+
+// 8 values -> 8 e4m3 bytes (as two dwords) after scaling by 2^(127 - sb)
+__device__ __forceinline__ uint2 mx_pack8(const float (&v)[8], int sb) {
+    float s[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) s[e] = fminf(448.f, fmaxf(-448.f, __builtin_amdgcn_ldexpf(v[e], 127 - sb)));
+    unsigned lo = 0, hi = 0;
+    lo = __builtin_amdgcn_cvt_pk_fp8_f32(s[0], s[1], lo, false);
+    lo = __builtin_amdgcn_cvt_pk_fp8_f32(s[2], s[3], lo, true);
+    hi = __builtin_amdgcn_cvt_pk_fp8_f32(s[4], s[5], hi, false);
+    hi = __builtin_amdgcn_cvt_pk_fp8_f32(s[6], s[7], hi, true);
+    return make_uint2(lo, hi);
+}
+
+// absmax over the 4 consecutive lanes holding one 32-element block
+__device__ __forceinline__ float block_amax(float a) {
+    a = fmaxf(a, __shfl_xor(a, 1, 64));
+    a = fmaxf(a, __shfl_xor(a, 2, 64));
+    return a;
+}
+
+// ---------------------------------------------------------------------------
+// bf16 rows -> mx8. One 256-thread block per row; thread t handles 16-B
+// chunks t, t+256, ...: four consecutive threads = one 32-element block.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void mx_quant_kernel(const bf16* __restrict__ x, int ldx, int k,
+                                                       uint8_t* __restrict__ q, int ldq, uint8_t* __restrict__ sc,
+                                                       int rows_pad) {
+    const int row = blockIdx.x;
+    const int nch = k >> 3;
+    const bf16* xr = x + (long)row * ldx;
+    for (int c0 = 0; c0 < nch; c0 += 256) {  // uniform trip count: shuffles see whole groups
+        const int ch = c0 + threadIdx.x;
+        float v[8];
+        float a = 0.f;
+        if (ch < nch) {
+            const u16x8 u = *reinterpret_cast<const u16x8*>(xr + ch * 8);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+                v[e] = bits2f(u[e]);
+                a = fmaxf(a, fabsf(v[e]));
+            }
+        } else {
+#pragma unroll
+            for (int e = 0; e < 8; ++e) v[e] = 0.f;
+        }
+        const int sb = mx_scale_byte(block_amax(a));
+        if (ch < nch) {
+            *reinterpret_cast<uint2*>(q + (long)row * ldq + ch * 8) = mx_pack8(v, sb);
+            if ((ch & 3) == 0) sc[(long)(ch >> 2) * rows_pad + row] = (uint8_t)sb;
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// LayerNorm -> mx8 (the QKV / fc1 operand straight from the norm): same
+// statistics as layernorm_kernel (norm.hip), the output rounded to bf16 (the
+// value the bf16 path would feed the GEMM) and then block-quantised.
+// One wave per row; lane chunks ch = lane + 64c, so 4 consecutive lanes hold
+// one 32-element block.
+// ---------------------------------------------------------------------------
+constexpr int LN_MAXC = 4;
+__global__ __launch_bounds__(256) void layernorm_mx_kernel(const bf16* __restrict__ x, int ldx,
+                                                           const bf16* __restrict__ g, const bf16* __restrict__ b,
+                                                           int rows, int d, float eps, const int32_t* __restrict__ idx,
+                                                           uint8_t* __restrict__ q, int ldq, uint8_t* __restrict__ sc,
+                                                           int rows_pad) {
+    const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    if (row >= rows) return;  // whole wave exits together
+    const long src = idx ? idx[row] : row;
+    const int nch = d >> 3;
+    const bf16* xr = x + src * ldx;
+    float v[LN_MAXC][8];
+#pragma unroll
+    for (int c = 0; c < LN_MAXC; ++c) {
+        const int ch = lane + c * 64;
+        if (ch < nch) {
+            const u16x8 u = *reinterpret_cast<const u16x8*>(xr + ch * 8);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) v[c][e] = bits2f(u[e]);
+        } else {
+#pragma unroll
+            for (int e = 0; e < 8; ++e) v[c][e] = 0.f;
+        }
+    }
+    float s = 0.f;
+#pragma unroll
+    for (int c = 0; c < LN_MAXC; ++c)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) s += v[c][e];
+    const float mean = wave_sum(s) / d;
+    float s2 = 0.f;
+#pragma unroll
+    for (int c = 0; c < LN_MAXC; ++c) {
+        if (lane + c * 64 < nch) {
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+                const float t = v[c][e] - mean;
+                s2 += t * t;
+            }
+        }
+    }
+    const float rstd = rsqrtf(wave_sum(s2) / d + eps);
+#pragma unroll
+    for (int c = 0; c < LN_MAXC; ++c) {
+        const int ch = lane + c * 64;
+        if (c * 64 >= nch) break;  // wave-uniform
+        float o[8];
+        float a = 0.f;
+        if (ch < nch) {
+            const u16x8 gu = *reinterpret_cast<const u16x8*>(g + ch * 8);
+            const u16x8 bu = *reinterpret_cast<const u16x8*>(b + ch * 8);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+                o[e] = bf2f(f2bf((v[c][e] - mean) * rstd * bits2f(gu[e]) + bits2f(bu[e])));
+                a = fmaxf(a, fabsf(o[e]));
+            }
+        } else {
+#pragma unroll
+            for (int e = 0; e < 8; ++e) o[e] = 0.f;
+        }
+        const int sb = mx_scale_byte(block_amax(a));
+        if (ch < nch) {
+            *reinterpret_cast<uint2*>(q + (long)row * ldq + ch * 8) = mx_pack8(o, sb);
+            if ((ch & 3) == 0) sc[(long)(ch >> 2) * rows_pad + row] = (uint8_t)sb;
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Block-scaled fp8 GEMM: C[m][n] = act(sum_k A[m][k] B[n][k] + bias[n]) (+ residual),
+// A, B in mx8. Same schedule as gemm_pipe6_kernel (gemm.hip): 256 x 256 tile,
+// 8 waves in two ping-pong rows, 4-deep LDS ring of 64-deep K stages (64-B
+// rows: the same byte geometry as the bf16 kernel's 32-deep stages), one
+// memory and one compute phase per stage. Per stage each wave issues 8
+// v_mfma_scale_f32_32x32x64_f8f6f4 (128 x 64 outputs as 4 x 2 tiles of 32 x 32)
+// fed by 12 ds_read_b128 + 6 scale-byte reads.
+//   * operand k-layout (probe-verified): lane (r, h = lane >> 5) holds bytes
+//     k = 16h .. 16h+15 then 32+16h .. 32+16h+15 of row r -> LDS chunks h and
+//     2 + h of the 64-B row; its scale operand is row r's block h;
+//   * LDS swizzle chunk ^ ((row >> 2) & 3): the 16 lanes of each ds_read_b128
+//     group (rows {0-3, 12-15, 20-27} / {4-11, 16-19, 28-31} of a 32-row
+//     fragment) land in 16 distinct bank quads;
+//   * per stage a 1 KiB scale piece ([A blk0][A blk1][B blk0][B blk1], 256 B
+//     each) rides along, DMA'd by 8 lanes of every wave (uniform vmcnt).
+// Epilogue: bf16 output through LDS as in gemm.hip, or (out_mx) the bf16
+// value re-quantised to mx8 per 32-column block -- fc1's output is fc2's
+// A operand with no extra pass.
+// ---------------------------------------------------------------------------
+struct MxArgs {
+    const uint8_t* A;
+    const uint8_t* B;
+    const uint8_t* sa;
+    const uint8_t* sb;
+    void* C;
+    uint8_t* sc;
+    const bf16* bias;
+    const bf16* res;
+    int lda, ldb, ldc, ldr;
+    int sa_rows, sb_rows, sc_rows;
+    int M, N, K;
+    int res_period, act, out_mx;
+};
+
+struct MxCfg {
+    static constexpr int BM = 256, BN = 256, WM = 2, WN = 4, NW = WM * WN, NT = NW * 64;
+    static constexpr int TM = 128, TN = 64, FM = 4, FN = 2;  // 32 x 32 tiles per wave
+    static constexpr int BK = 64;                            // fp8 elements (bytes) per stage
+    static constexpr int A_ST = BM * BK, B_ST = BN * BK, SC_ST = 1024;
+    static constexpr int STAGE = A_ST + B_ST + SC_ST, NSTAGE = 4;
+    static constexpr int A_PIECES = A_ST / 1024, PIECES = (A_ST + B_ST) / 1024, PPW = PIECES / NW;  // data
+    static constexpr int OUT_LD = BN * 2 + 16;
+    static constexpr int LDS_MAIN = NSTAGE * STAGE, LDS_OUT = BM * OUT_LD;
+    static constexpr int LDS = LDS_MAIN > LDS_OUT ? LDS_MAIN : LDS_OUT;
+};
+
+__device__ __forceinline__ int mxswz(int row, int chunk) { return chunk ^ ((row >> 2) & 3); }
+
+template <int GROUP_M, int ACT>
+__global__ __launch_bounds__(512, 2) void gemm_mx_kernel(MxArgs p) {
+    using C = MxCfg;
+    __shared__ __attribute__((aligned(16))) char lds[C::LDS];
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wm = wave / C::WN, wn = wave % C::WN;
+    const int h = lane >> 5, r32 = lane & 31;
+
+    const int nbm = (p.M + C::BM - 1) / C::BM;
+    const int nbn = (p.N + C::BN - 1) / C::BN;
+    const int tile = xcd_remap(blockIdx.x, gridDim.x);
+    int bm, bn;
+    tile_coords<GROUP_M>(tile, nbm, nbn, bm, bn);
+    const int m0 = bm * C::BM, n0 = bn * C::BN;
+
+    // data pieces: 16 rows x 64 B; lane -> row piece*16 + lane/4, physical chunk lane&3
+    const uint8_t* src[C::PPW];
+#pragma unroll
+    for (int q = 0; q < C::PPW; ++q) {
+        const int piece = wave * C::PPW + q;
+        const bool isA = piece < C::A_PIECES;
+        const int prow = (isA ? piece : piece - C::A_PIECES) * 16 + (lane >> 2);
+        const int logical = mxswz(prow, lane & 3);
+        src[q] = isA ? p.A + (size_t)min(m0 + prow, p.M - 1) * p.lda + logical * 16
+                     : p.B + (size_t)min(n0 + prow, p.N - 1) * p.ldb + logical * 16;
+    }
+    // scale piece: lane L -> part L/16 (A b0, A b1, B b0, B b1), 16 rows (L%16)*16..; this wave owns lanes 8w..8w+7
+    const bool sc_mine = (lane >> 3) == wave;
+    const int part = lane >> 4, srow = (lane & 15) * 16;
+    const uint8_t* sc_src = part < 2 ? p.sa + (size_t)part * p.sa_rows + m0 + srow
+                                     : p.sb + (size_t)(part - 2) * p.sb_rows + n0 + srow;
+    const size_t sc_step = part < 2 ? (size_t)2 * p.sa_rows : (size_t)2 * p.sb_rows;  // per stage (2 blocks)
+
+    auto issue = [&](int st) {
+        char* base = lds + (st & 3) * C::STAGE;
+        const int k0 = st * C::BK;
+#pragma unroll
+        for (int q = 0; q < C::PPW; ++q) glds16(src[q] + k0, base + (wave * C::PPW + q) * 1024);
+        if (sc_mine) glds16(sc_src + st * sc_step, base + C::A_ST + C::B_ST);
+    };
+
+    const unsigned lds0 = (unsigned)(uintptr_t)(LDS_AS char*)lds;
+    const int sw = (lane >> 2) & 3;
+    const unsigned c0 = (unsigned)((h ^ sw) << 4), c1 = (unsigned)(((2 + h) ^ sw) << 4);
+    const unsigned a_row = lds0 + (wm * C::TM + r32) * 64;
+    const unsigned b_row = lds0 + C::A_ST + (wn * C::TN + r32) * 64;
+    const unsigned sa_l = lds0 + C::A_ST + C::B_ST + h * 256 + wm * C::TM + r32;
+    const unsigned sb_l = lds0 + C::A_ST + C::B_ST + 512 + h * 256 + wn * C::TN + r32;
+
+    f32x16 acc[C::FM][C::FN];
+#pragma unroll
+    for (int i = 0; i < C::FM; ++i)
+#pragma unroll
+        for (int j = 0; j < C::FN; ++j)
+#pragma unroll
+            for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
+
+    const int nk = p.K / C::BK;
+    auto wait_rem = [&](int rem) {  // own DMA (PPW + 1 per stage) retired except `rem` later stages
+        if (rem >= 2) vm_wait<2 * (C::PPW + 1)>();
+        else if (rem == 1) vm_wait<C::PPW + 1>();
+        else vm_wait<0>();
+    };
+    // every wave issues PPW + 1 DMA instructions per stage (EXEC-masked scale piece included)
+    for (int st = 0; st < 3 && st < nk; ++st) issue(st);
+    wait_rem(min(2, nk - 1));
+    __builtin_amdgcn_s_barrier();
+    if (wm == 1) __builtin_amdgcn_s_barrier();
+
+    for (int t = 0; t < nk; ++t) {
+        const unsigned so = (t & 3) * C::STAGE;
+        bf16x8 a[C::FM][2], b[C::FN][2];
+        unsigned sa[C::FM], sbv[C::FN];
+#pragma unroll
+        for (int j = 0; j < C::FN; ++j) {
+            ds_read16<0>(b[j][0], b_row + so + j * 32 * 64 + c0);
+            ds_read16<0>(b[j][1], b_row + so + j * 32 * 64 + c1);
+        }
+#pragma unroll
+        for (int i = 0; i < C::FM; ++i) {
+            ds_read16<0>(a[i][0], a_row + so + i * 32 * 64 + c0);
+            ds_read16<0>(a[i][1], a_row + so + i * 32 * 64 + c1);
+        }
+        asm volatile("ds_read_u8 %0, %1 offset:0" : "=v"(sbv[0]) : "v"(sb_l + so) : "memory");
+        asm volatile("ds_read_u8 %0, %1 offset:32" : "=v"(sbv[1]) : "v"(sb_l + so) : "memory");
+#pragma unroll
+        for (int i = 0; i < C::FM; ++i) {
+            // offsets i*32 (A) / j*32 (B) as immediates
+            if (i == 0) asm volatile("ds_read_u8 %0, %1 offset:0" : "=v"(sa[0]) : "v"(sa_l + so) : "memory");
+            if (i == 1) asm volatile("ds_read_u8 %0, %1 offset:32" : "=v"(sa[1]) : "v"(sa_l + so) : "memory");
+            if (i == 2) asm volatile("ds_read_u8 %0, %1 offset:64" : "=v"(sa[2]) : "v"(sa_l + so) : "memory");
+            if (i == 3) asm volatile("ds_read_u8 %0, %1 offset:96" : "=v"(sa[3]) : "v"(sa_l + so) : "memory");
+        }
+        if (t + 3 < nk) {
+            issue(t + 3);
+            wait_rem(2);
+        } else {
+            wait_rem(max(0, nk - 2 - t));
+        }
+        lgkm_wait<0>();
+        __builtin_amdgcn_s_barrier();
+        __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+        for (int i = 0; i < C::FM; ++i)
+#pragma unroll
+            for (int j = 0; j < C::FN; ++j) {
+                const i32x8 bo = __builtin_bit_cast(i32x8, __builtin_shufflevector(b[j][0], b[j][1], 0, 1, 2, 3, 4,
+                                                                                  5, 6, 7, 8, 9, 10, 11, 12, 13,
+                                                                                  14, 15));
+                const i32x8 ao = __builtin_bit_cast(i32x8, __builtin_shufflevector(a[i][0], a[i][1], 0, 1, 2, 3, 4,
+                                                                                  5, 6, 7, 8, 9, 10, 11, 12, 13,
+                                                                                  14, 15));
+                acc[i][j] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(bo, ao, acc[i][j], 0, 0, 0,
+                                                                             (int)sbv[j], 0,
+                                                                             (int)sa[i]);
+            }
+        __builtin_amdgcn_s_setprio(0);
+        __builtin_amdgcn_sched_barrier(0);
+        __builtin_amdgcn_s_barrier();
+    }
+    if (wm == 0) __builtin_amdgcn_s_barrier();
+
+    // ---- epilogue: bias + act -> bf16 tile in LDS; lane holds m = i*32 + r32, n = j*32 + 8q + 4h + (0..3)
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < C::FN; ++j)
+#pragma unroll
+        for (int qd = 0; qd < 4; ++qd) {
+            const int nl = wn * C::TN + j * 32 + 8 * qd + 4 * h;
+            float bv[4] = {0.f, 0.f, 0.f, 0.f};
+            if (p.bias) {
+#pragma unroll
+                for (int r = 0; r < 4; ++r) bv[r] = bf2f(p.bias[min(n0 + nl + r, p.N - 1)]);
+            }
+#pragma unroll
+            for (int i = 0; i < C::FM; ++i) {
+                const int ml = wm * C::TM + i * 32 + r32;
+                bf16x4 o;
+#pragma unroll
+                for (int r = 0; r < 4; ++r) o[r] = f2bf(apply_act(acc[i][j][4 * qd + r] + bv[r], ACT));
+                *reinterpret_cast<bf16x4*>(lds + ml * C::OUT_LD + nl * 2) = o;
+            }
+        }
+    __syncthreads();
+    constexpr int CPR = C::BN / 8;
+    if (!p.out_mx) {
+        bf16* Cout = reinterpret_cast<bf16*>(p.C);
+        for (int c = tid; c < C::BM * CPR; c += C::NT) {
+            const int row = c / CPR, cc = c % CPR;
+            const int gr = m0 + row, gc = n0 + cc * 8;
+            if (gr >= p.M || gc >= p.N) continue;
+            u16x8 v = *reinterpret_cast<const u16x8*>(lds + row * C::OUT_LD + cc * 16);
+            if (p.res) {
+                const int rr = p.res_period ? gr % p.res_period : gr;
+                const u16x8 rv = *reinterpret_cast<const u16x8*>(p.res + (size_t)rr * p.ldr + gc);
+                bf16x8 o;
+#pragma unroll
+                for (int e = 0; e < 8; ++e) o[e] = f2bf(bits2f(v[e]) + bits2f(rv[e]));
+                *reinterpret_cast<bf16x8*>(Cout + (size_t)gr * p.ldc + gc) = o;
+            } else {
+                *reinterpret_cast<u16x8*>(Cout + (size_t)gr * p.ldc + gc) = v;
+            }
+        }
+    } else {
+        // mx8 output: 4 consecutive threads = one 32-column block of one row (CPR % 4 == 0, NT % 4 == 0)
+        uint8_t* Cq = reinterpret_cast<uint8_t*>(p.C);
+        for (int c = tid; c < C::BM * CPR; c += C::NT) {  // same trip count for every thread
+            const int row = c / CPR, cc = c % CPR;
+            const int gr = m0 + row, gc = n0 + cc * 8;
+            const u16x8 v = *reinterpret_cast<const u16x8*>(lds + row * C::OUT_LD + cc * 16);
+            float f[8];
+            float a = 0.f;
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+                f[e] = bits2f(v[e]);
+                a = fmaxf(a, fabsf(f[e]));
+            }
+            const int sbyte = mx_scale_byte(block_amax(a));
+            if (gr < p.M && gc < p.N) {
+                *reinterpret_cast<uint2*>(Cq + (size_t)gr * p.ldc + gc) = mx_pack8(f, sbyte);
+                if ((cc & 3) == 0) p.sc[(size_t)(gc >> 5) * p.sc_rows + gr] = (uint8_t)sbyte;
+            }
+        }
+    }
+}
+
+template <int GROUP_M>
+int launch_mx(const MxArgs& a, hipStream_t s) {
+    const int nbm = (a.M + 255) / 256, nbn = (a.N + 255) / 256;
+    const dim3 grid(nbm * nbn), block(512);
+    switch (a.act) {
+        case MME_ACT_GELU_TANH:
+            hipLaunchKernelGGL((gemm_mx_kernel<GROUP_M, MME_ACT_GELU_TANH>), grid, block, 0, s, a);
+            break;
+        case MME_ACT_QUICK_GELU:
+            hipLaunchKernelGGL((gemm_mx_kernel<GROUP_M, MME_ACT_QUICK_GELU>), grid, block, 0, s, a);
+            break;
+        case MME_ACT_GELU_ERF:
+            hipLaunchKernelGGL((gemm_mx_kernel<GROUP_M, MME_ACT_GELU_ERF>), grid, block, 0, s, a);
+            break;
+        default:
+            hipLaunchKernelGGL((gemm_mx_kernel<GROUP_M, MME_ACT_NONE>), grid, block, 0, s, a);
+            break;
+    }
+    return mme_check_launch("mme_gemm_mx");
+}
+
+}  // namespace
+
+extern "C" int mme_mx_quant(const void* x, int ldx, int rows, int k, void* q, int ldq, void* scales, int rows_pad,
+                            void* stream) {
+    MME_REQUIRE(x && q && scales, "mme_mx_quant: null pointer");
+    MME_REQUIRE(rows >= 0 && k > 0 && k % 32 == 0, "mme_mx_quant: k=%d must be a positive multiple of 32", k);
+    MME_REQUIRE(ldx % 8 == 0 && ldx >= k && ldq % 16 == 0 && ldq >= k, "mme_mx_quant: bad leading dims");
+    MME_REQUIRE(rows_pad >= rows && rows_pad % 256 == 0, "mme_mx_quant: rows_pad must be >= rows, multiple of 256");
+    MME_REQUIRE(((uintptr_t)x & 15) == 0 && ((uintptr_t)q & 15) == 0, "mme_mx_quant: misaligned");
+    if (rows == 0) return MME_OK;
+    hipLaunchKernelGGL(mx_quant_kernel, dim3(rows), dim3(256), 0, as_stream(stream), (const bf16*)x, ldx, k,
+                       (uint8_t*)q, ldq, (uint8_t*)scales, rows_pad);
+    return mme_check_launch("mme_mx_quant");
+}
+
+extern "C" int mme_layernorm_mx(const void* x, int ldx, const void* gamma, const void* beta, int rows, int d,
+                                float eps, const int32_t* rows_idx, void* q, int ldq, void* scales, int rows_pad,
+                                void* stream) {
+    MME_REQUIRE(x && gamma && beta && q && scales, "mme_layernorm_mx: null pointer");
+    MME_REQUIRE(rows >= 0 && d > 0 && d % 32 == 0 && d <= 8 * 64 * LN_MAXC, "mme_layernorm_mx: d=%d unsupported", d);
+    MME_REQUIRE(ldx % 8 == 0 && ldx >= d && ldq % 16 == 0 && ldq >= d, "mme_layernorm_mx: bad leading dims");
+    MME_REQUIRE(rows_pad >= rows && rows_pad % 256 == 0, "mme_layernorm_mx: rows_pad must be >= rows, multiple of 256");
+    if (rows == 0) return MME_OK;
+    hipLaunchKernelGGL(layernorm_mx_kernel, dim3(cdiv(rows, 4)), dim3(256), 0, as_stream(stream), (const bf16*)x, ldx,
+                       (const bf16*)gamma, (const bf16*)beta, rows, d, eps, rows_idx, (uint8_t*)q, ldq,
+                       (uint8_t*)scales, rows_pad);
+    return mme_check_launch("mme_layernorm_mx");
+}
+
+extern "C" int mme_gemm_mx(const void* A, int lda, const void* sa, int sa_rows, const void* B, int ldb,
+                           const void* sb, int sb_rows, void* Cp, int ldc, void* c_scales, int c_rows_pad, int M,
+                           int N, int K, const void* bias, const void* residual, int ldr, int res_period, int act,
+                           int out_mx, void* stream) {
+    MME_REQUIRE(A && B && sa && sb && Cp, "mme_gemm_mx: null operand");
+    MME_REQUIRE(M >= 0 && N > 0 && K > 0 && K % 64 == 0, "mme_gemm_mx: K=%d must be a positive multiple of 64", K);
+    MME_REQUIRE(lda % 16 == 0 && ldb % 16 == 0 && lda >= K && ldb >= K, "mme_gemm_mx: lda/ldb must be >= K, % 16");
+    MME_REQUIRE(((uintptr_t)A & 15) == 0 && ((uintptr_t)B & 15) == 0 && ((uintptr_t)sa & 15) == 0 &&
+                    ((uintptr_t)sb & 15) == 0 && ((uintptr_t)Cp & 15) == 0,
+                "mme_gemm_mx: operands must be 16-byte aligned");
+    MME_REQUIRE(sa_rows % 256 == 0 && sa_rows >= M && sb_rows % 256 == 0 && sb_rows >= N,
+                "mme_gemm_mx: scale planes must cover round_up(rows, 256)");
+    MME_REQUIRE(act >= MME_ACT_NONE && act <= MME_ACT_GELU_ERF, "mme_gemm_mx: bad activation %d", act);
+    if (out_mx) {
+        MME_REQUIRE(c_scales && N % 32 == 0 && ldc % 16 == 0 && ldc >= N && c_rows_pad % 256 == 0 && c_rows_pad >= M,
+                    "mme_gemm_mx: mx8 output needs N %% 32 == 0, ldc %% 16 == 0 and a covering scale plane");
+        MME_REQUIRE(!residual, "mme_gemm_mx: residual add is not supported with mx8 output");
+    } else {
+        MME_REQUIRE(N % 8 == 0 && ldc % 8 == 0 && ldc >= N, "mme_gemm_mx: bf16 output needs N, ldc %% 8 == 0");
+        MME_REQUIRE(!residual || (ldr % 8 == 0 && ((uintptr_t)residual & 15) == 0), "mme_gemm_mx: bad residual");
+    }
+    if (M == 0) return MME_OK;
+    MxArgs a{(const uint8_t*)A, (const uint8_t*)B, (const uint8_t*)sa, (const uint8_t*)sb, Cp, (uint8_t*)c_scales,
+             (const bf16*)bias, (const bf16*)residual, lda, ldb, ldc, ldr, sa_rows, sb_rows, c_rows_pad, M, N, K,
+             res_period, act, out_mx};
+    return launch_mx<4>(a, as_stream(stream));
+}

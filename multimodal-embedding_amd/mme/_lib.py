@@ -16,7 +16,7 @@ LIB_PATH = os.environ.get("MME_LIB", os.path.join(_HERE, "libmme.so"))
 # MME_ACT_* / MME_PIX_* from include/mme.h
 ACT_NONE, ACT_GELU_TANH, ACT_QUICK_GELU, ACT_GELU_ERF = 0, 1, 2, 3
 PIX_F32_NCHW, PIX_PATCHES = 0, 1
-ABI_VERSION = 1
+ABI_VERSION = 2
 
 # name -> (restype, argtypes)
 _P = c_void_p
@@ -42,6 +42,10 @@ SIGNATURES = {
     "mme_recall_hits": (c_int, [_P, c_int, c_int, _P, c_int, c_int, _P, c_int, _P, _P]),
     "mme_maxsim_workspace_bytes": (c_size_t, [c_int, c_int, c_int]),
     "mme_maxsim": (c_int, [_P, _P, c_int, c_int, _P, _P, _P, c_int, c_int, c_int, _P, _P, c_size_t, _P]),
+    "mme_mx_quant": (c_int, [_P, c_int, c_int, c_int, _P, c_int, _P, c_int, _P]),
+    "mme_layernorm_mx": (c_int, [_P, c_int, _P, _P, c_int, c_int, c_float, _P, _P, c_int, _P, c_int, _P]),
+    "mme_gemm_mx": (c_int, [_P, c_int, _P, c_int, _P, c_int, _P, c_int, _P, c_int, _P, c_int, c_int, c_int, c_int,
+                            _P, _P, c_int, c_int, c_int, c_int, _P]),
 }
 
 

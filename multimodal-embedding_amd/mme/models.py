@@ -18,7 +18,7 @@ from typing import List, Optional, Sequence, Tuple
 
 import torch
 
-from . import ops
+from . import mx, ops
 from .config import ACTS, ModelSpec, TowerConfig, get_spec
 from .weights import LayerW, ModelW, TextW, VisionW, from_hf_state_dict, random_state_dict
 
@@ -29,11 +29,14 @@ class _Bufs:
     """Per-forward activation buffers: x (residual stream), h (LN / attention
     output) and one wide buffer shared by QKV and the MLP hidden."""
 
-    def __init__(self, rows: int, cfg: TowerConfig, device):
+    def __init__(self, rows: int, cfg: TowerConfig, device, fp8: bool = False):
         d = cfg.hidden
         wide = max(3 * d, cfg.inter_pad)
         self.h = torch.empty(rows, d, dtype=BF16, device=device)
         self.wide = torch.empty(rows, wide, dtype=BF16, device=device)
+        # fp8 mode: mx8 LayerNorm output and mx8 MLP hidden (fc1 -> fc2 operand)
+        self.hq = mx.MXTensor.empty(rows, d, device) if fp8 else None
+        self.midq = mx.MXTensor.empty(rows, cfg.inter_pad, device) if fp8 else None
 
 
 def encoder_layer(x: torch.Tensor, L: LayerW, cfg: TowerConfig, B: int, T: int, bufs: _Bufs, *,
@@ -41,6 +44,16 @@ def encoder_layer(x: torch.Tensor, L: LayerW, cfg: TowerConfig, B: int, T: int, 
     """Pre-LN transformer block, in place on x (SiglipEncoderLayer.forward, TF:…siglip.py:341-357)."""
     d, H, hd = cfg.hidden, cfg.heads, cfg.head_dim
     act = ACTS[cfg.act]
+    if L.mx is not None:  # fp8 mode: QKV / fc1 / fc2 on the block-scaled fp8 MFMA (mme/mx.py)
+        mlp_flops = 2.0 * x.shape[0] * d * cfg.intermediate
+        hq = mx.layernorm(x, L.ln1_g, L.ln1_b, cfg.eps, out=bufs.hq)
+        qkv = mx.gemm(hq, L.mx.qkv, L.qkv_b, out=bufs.wide[:, : 3 * d])
+        a = ops.attention(qkv, B, T, H, hd, seq_lens=seq_lens, causal=causal, out=bufs.h)
+        ops.gemm(a, L.o_w, L.o_b, residual=x, out=x)
+        hq = mx.layernorm(x, L.ln2_g, L.ln2_b, cfg.eps, out=bufs.hq)
+        midq = mx.gemm(hq, L.mx.fc1, L.fc1_b, act=act, out_mx=bufs.midq, algo_flops=mlp_flops)
+        mx.gemm(midq, L.mx.fc2, L.fc2_b, residual=x, out=x, algo_flops=mlp_flops)
+        return
     h = ops.layernorm(x, L.ln1_g, L.ln1_b, cfg.eps, out=bufs.h)
     qkv = ops.gemm(h, L.qkv_w, L.qkv_b, out=bufs.wide[:, : 3 * d])
     a = ops.attention(qkv, B, T, H, hd, seq_lens=seq_lens, causal=causal, out=bufs.h)
@@ -69,7 +82,7 @@ class VisionTower:
             pe = ops.gemm(patches, w.patch_w, algo_flops=2.0 * B * P * d * 3 * cfg.patch ** 2)
             x = ops.clip_embed_ln(pe, w.cls, w.pos, w.pre_ln_g, w.pre_ln_b, cfg.eps, B, P)
             del pe
-        bufs = _Bufs(B * T, cfg, dev)
+        bufs = _Bufs(B * T, cfg, dev, fp8=w.layers[0].mx is not None)
         for L in w.layers:
             encoder_layer(x, L, cfg, B, T, bufs)
         if self.spec.family == "siglip":
@@ -100,7 +113,7 @@ class TextTower:
         cfg, w = self.cfg, self.w
         B, L = ids.shape
         x = ops.token_embed(ids, w.tok, w.pos)
-        bufs = _Bufs(B * L, cfg, ids.device)
+        bufs = _Bufs(B * L, cfg, ids.device, fp8=self.w.layers[0].mx is not None)
         for layer in w.layers:
             encoder_layer(x, layer, cfg, B, L, bufs, seq_lens=seq_lens, causal=cfg.causal)
         mode = {"eos": 0, "argmax": 1, "last": 2}[cfg.pool]
@@ -161,6 +174,7 @@ class DualEncoder:
         self.vision = VisionTower(spec, weights.vision)
         self.text = TextTower(spec, weights.text)
         self.dtype = BF16
+        self.precision = "bf16"
 
     # ---- construction
     @classmethod
@@ -168,6 +182,17 @@ class DualEncoder:
         spec = get_spec(spec) if isinstance(spec, str) else spec
         sd = state_dict if state_dict is not None else random_state_dict(spec, seed, device)
         return cls(spec, from_hf_state_dict(spec, sd, device), device)
+
+    def enable_fp8(self) -> "DualEncoder":
+        """Opt-in fp8 precision mode (BASELINE configs[4]): quantise every encoder
+        layer's QKV / fc1 / fc2 weights to mx8 once; forward passes then run those
+        products on the block-scaled fp8 MFMA (mme/mx.py)."""
+        for tower in (self.weights.vision, self.weights.text):
+            for L in tower.layers:
+                if L.mx is None:
+                    L.mx = mx.quantize_layer(L)
+        self.precision = "fp8"
+        return self
 
     # ---- HF-style surface
     def eval(self):
@@ -271,14 +296,17 @@ class CLIPModel(DualEncoder):
     family = "clip"
 
 
-def load_model(name: str, seed: int = 0, device="cuda", state_dict=None, batch_size: Optional[int] = None
-               ) -> Tuple[DualEncoder, "object"]:
+def load_model(name: str, seed: int = 0, device="cuda", state_dict=None, batch_size: Optional[int] = None,
+               fp8: bool = False) -> Tuple[DualEncoder, "object"]:
     """(model, processor) for a registry name — the offline counterpart of
-    from_pretrained(m_info['id']) (main.py:808-820)."""
+    from_pretrained(m_info['id']) (main.py:808-820). fp8=True: the mx8 encoder
+    GEMM mode of BASELINE configs[4] (DualEncoder.enable_fp8)."""
     from .processor import Processor
     spec = get_spec(name)
     if batch_size is not None:
         spec = spec.with_batch_size(batch_size)
     cls = SiglipModel if spec.family == "siglip" else CLIPModel
     model = cls.from_spec(spec, seed=seed, device=device, state_dict=state_dict)
+    if fp8:
+        model.enable_fp8()
     return model, Processor(spec, device=device)

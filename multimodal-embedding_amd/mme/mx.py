@@ -1,0 +1,119 @@
+"""MX-fp8 (e4m3 values + E8M0 block scales) tensors and the fp8 encoder-GEMM
+path (BASELINE.json configs[4]: "Apple-DFN5B-H fp8 weights on CDNA4 fp8 MFMA").
+
+The reference runs every model in bf16 (main.py:808-820 loads with
+torch_dtype=DTYPE); this is an opt-in precision mode of the same towers
+(``load_model(..., fp8=True)``): the QKV, fc1 and fc2 products of each encoder
+layer run on the block-scaled fp8 MFMA with weights quantised once at load and
+activations quantised by the LayerNorm / fc1 kernels that produce them. The
+attention output projection, patch embedding, heads and everything after the
+towers stay bf16. Format and rounding rule: include/mme.h (config 5 section),
+oracle/mx.py restates them on the CPU.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+from typing import Optional
+
+import torch
+
+from . import ops
+from ._lib import ACT_NONE, call
+
+U8 = torch.uint8
+
+
+def rows_pad(rows: int) -> int:
+    return max(256, (rows + 255) // 256 * 256)
+
+
+@dataclass
+class MXTensor:
+    """rows x k matrix in mx8: q u8 [rows, >=k] (row stride = q.stride(0) bytes),
+    scales u8 [k/32, rows_pad] (block-major planes)."""
+    q: torch.Tensor
+    scales: torch.Tensor
+    rows: int
+    k: int
+
+    @property
+    def rows_pad(self) -> int:
+        return self.scales.shape[1]
+
+    @staticmethod
+    def empty(rows: int, k: int, device, rows_alloc: Optional[int] = None) -> "MXTensor":
+        if k % 32:
+            raise ValueError(f"mx8 needs k % 32 == 0 (got {k})")
+        ra = rows_alloc or rows
+        ldq = (k + 15) // 16 * 16
+        q = torch.empty(ra, ldq, dtype=U8, device=device)
+        sc = torch.empty(k // 32, rows_pad(ra), dtype=U8, device=device)
+        return MXTensor(q, sc, rows, k)
+
+    def view_rows(self, rows: int) -> "MXTensor":
+        """The first `rows` rows (same storage; scale planes keep their padding)."""
+        if rows > self.q.shape[0]:
+            raise ValueError("view_rows beyond the allocation")
+        return MXTensor(self.q, self.scales, rows, self.k)
+
+
+def quantize(x: torch.Tensor, out: Optional[MXTensor] = None) -> MXTensor:
+    """bf16 [rows, k] -> mx8 (mme_mx_quant)."""
+    ops._dev(x)
+    rows, k = x.shape
+    if out is None:
+        out = MXTensor.empty(rows, k, x.device)
+    call("mme_mx_quant", x.data_ptr(), ops._rowmajor(x, "x"), rows, k, out.q.data_ptr(), out.q.stride(0),
+         out.scales.data_ptr(), out.rows_pad, ops._stream())
+    return MXTensor(out.q, out.scales, rows, k)
+
+
+def layernorm(x: torch.Tensor, g: torch.Tensor, b: torch.Tensor, eps: float, out: MXTensor,
+              rows_idx: Optional[torch.Tensor] = None) -> MXTensor:
+    """LayerNorm of bf16 rows straight to mx8 (mme_layernorm_mx)."""
+    ops._dev(x, g, b, rows_idx)
+    rows = x.shape[0] if rows_idx is None else rows_idx.numel()
+    d = x.shape[1]
+    call("mme_layernorm_mx", x.data_ptr(), ops._rowmajor(x, "x"), g.data_ptr(), b.data_ptr(), rows, d, float(eps),
+         ops._ptr(rows_idx), out.q.data_ptr(), out.q.stride(0), out.scales.data_ptr(), out.rows_pad, ops._stream())
+    return MXTensor(out.q, out.scales, rows, d)
+
+
+def gemm(a: MXTensor, w: MXTensor, bias: Optional[torch.Tensor] = None, *, residual: Optional[torch.Tensor] = None,
+         res_period: int = 0, act: int = ACT_NONE, out: Optional[torch.Tensor] = None,
+         out_mx: Optional[MXTensor] = None, algo_flops: Optional[float] = None):
+    """act(a @ w.T + bias) (+ residual): bf16 [M, N] into `out`, or mx8 into `out_mx`."""
+    if a.k != w.k:
+        raise ValueError(f"gemm_mx: K mismatch {a.k} vs {w.k}")
+    M, N, K = a.rows, w.rows, a.k
+    ops._dev(a.q, w.q, bias, residual, out)
+    if out_mx is not None:
+        if residual is not None:
+            raise ValueError("gemm_mx: no residual with an mx8 output")
+        cptr, ldc, csc, crows = out_mx.q.data_ptr(), out_mx.q.stride(0), out_mx.scales.data_ptr(), out_mx.rows_pad
+    else:
+        if out is None:
+            out = torch.empty(M, N, dtype=ops.BF16, device=a.q.device)
+        cptr, ldc, csc, crows = out.data_ptr(), ops._rowmajor(out, "out"), None, 0
+    ldr = ops._rowmajor(residual, "residual") if residual is not None else 0
+    ev = ops.KernelTimer.begin()
+    call("mme_gemm_mx", a.q.data_ptr(), a.q.stride(0), a.scales.data_ptr(), a.rows_pad, w.q.data_ptr(),
+         w.q.stride(0), w.scales.data_ptr(), w.rows_pad, cptr, ldc, csc, crows, M, N, K, ops._ptr(bias),
+         ops._ptr(residual), ldr, int(res_period), int(act), int(out_mx is not None), ops._stream())
+    ops.KernelTimer.end(ev, "gemm_mx", algo_flops if algo_flops is not None else 2.0 * M * N * K,
+                        M * K + N * K + (M * N if out_mx is not None else 2.0 * M * N))
+    if out_mx is not None:
+        return MXTensor(out_mx.q, out_mx.scales, M, N)
+    return out
+
+
+@dataclass
+class LayerMX:
+    """mx8 copies of one encoder layer's fp8 weights (quantised once at load)."""
+    qkv: MXTensor
+    fc1: MXTensor
+    fc2: MXTensor
+
+
+def quantize_layer(L) -> LayerMX:
+    return LayerMX(quantize(L.qkv_w), quantize(L.fc1_w), quantize(L.fc2_w))

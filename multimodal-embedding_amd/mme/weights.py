@@ -40,6 +40,7 @@ class LayerW:
     fc1_b: torch.Tensor   # [Ipad]
     fc2_w: torch.Tensor   # [d, Ipad]
     fc2_b: torch.Tensor
+    mx: Optional[object] = None  # mme.mx.LayerMX: fp8 copies of qkv/fc1/fc2 (opt-in precision mode)
 
 
 @dataclass

@@ -1,0 +1,149 @@
+"""MX-fp8 path (BASELINE configs[4]) on the MI355X against oracle/mx.py.
+
+Tolerances: the quantisers are bit-exact; the fp8 GEMM is compared with the fp64
+product of the SAME dequantised operands (only fp32 accumulation order and the
+final bf16 rounding differ: |err| <= 2^-8 |ref| + 1e-3 * rms); the fp8 towers
+against the fp32 oracle at cos >= 0.99 per embedding (fp8 rounding of every
+QKV / MLP operand; the reference has no fp8 mode, so this is parity-unpinned
+against the reference itself).
+"""
+import math
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import mx as omx
+
+pytestmark = pytest.mark.gpu
+
+from mme import _lib, mx, ops  # noqa: E402
+
+
+def rnd(*shape, scale=1.0, gen=None):
+    return (torch.randn(*shape, generator=gen, device="cuda") * scale).to(torch.bfloat16)
+
+
+def mx_host(t: mx.MXTensor):
+    return t.q[: t.rows, : t.k].cpu().numpy(), t.scales.cpu().numpy()
+
+
+@pytest.mark.parametrize("rows,k", [(1, 32), (7, 96), (300, 1280), (513, 5120), (64, 4352)])
+def test_mx_quant_bit_exact(cuda, rows, k):
+    g = torch.Generator(device="cuda").manual_seed(rows + k)
+    x = rnd(rows, k, gen=g) * torch.exp2(torch.randint(-8, 8, (rows, 1), device="cuda", generator=g)).to(torch.bfloat16)
+    x[0, :32] = 0  # an all-zero block
+    t = mx.quantize(x)
+    q, sc = mx_host(t)
+    rq, rsc = omx.quantize(x.float().cpu().numpy(), rows_pad=t.rows_pad)
+    assert np.array_equal(q, rq)
+    assert np.array_equal(sc[:, :rows], rsc[:, :rows])
+
+
+@pytest.mark.parametrize("rows,d,with_idx", [(5, 1280, False), (300, 1024, False), (37, 1152, True)])
+def test_layernorm_mx_bit_exact(cuda, rows, d, with_idx):
+    g = torch.Generator(device="cuda").manual_seed(rows * d)
+    x = rnd(rows, d, scale=2.0, gen=g)
+    gam = rnd(d, gen=g)
+    bet = rnd(d, scale=0.1, gen=g)
+    idx = torch.arange(rows - 1, -1, -1, device="cuda", dtype=torch.int32) if with_idx else None
+    out = mx.MXTensor.empty(rows, d, "cuda")
+    t = mx.layernorm(x, gam, bet, 1e-5, out, rows_idx=idx)
+    # the bf16 LayerNorm kernel's output, quantised by the oracle, must match bit for bit
+    y = ops.layernorm(x, gam, bet, 1e-5, rows_idx=idx)
+    rq, rsc = omx.quantize(y.float().cpu().numpy(), rows_pad=t.rows_pad)
+    q, sc = mx_host(t)
+    assert np.array_equal(q, rq)
+    assert np.array_equal(sc[:, :rows], rsc[:, :rows])
+
+
+@pytest.mark.parametrize("M,N,K", [(1, 64, 64), (300, 256, 128), (1000, 3840, 1280), (777, 1280, 5120),
+                                   (2048, 5120, 1280), (129, 96, 192)])
+@pytest.mark.parametrize("act", [0, 2])
+def test_gemm_mx_vs_dequantised(cuda, M, N, K, act):
+    g = torch.Generator(device="cuda").manual_seed(M + N + K + act)
+    a = mx.quantize(rnd(M, K, gen=g))
+    w = mx.quantize(rnd(N, K, scale=1 / math.sqrt(K), gen=g))
+    b = rnd(N, scale=0.1, gen=g)
+    out = mx.gemm(a, w, b, act=act)
+    aq, asc = mx_host(a)
+    wq, wsc = mx_host(w)
+    ref = omx.gemm_ref(aq, asc, M, wq, wsc, N) + b.float().cpu().numpy()
+    if act == _lib.ACT_QUICK_GELU:
+        ref = ref / (1 + np.exp(-1.702 * ref))
+    got = out.float().cpu().numpy()
+    rms = np.sqrt(np.mean(ref ** 2))
+    assert np.all(np.abs(got - ref) <= np.abs(ref) * 2.0 ** -8 + 1e-3 * rms)
+
+
+def test_gemm_mx_residual_and_mx_output(cuda):
+    M, N, K = 600, 1024, 1280
+    g = torch.Generator(device="cuda").manual_seed(5)
+    a = mx.quantize(rnd(M, K, gen=g))
+    w = mx.quantize(rnd(N, K, scale=1 / math.sqrt(K), gen=g))
+    b = rnd(N, scale=0.1, gen=g)
+    res = rnd(M, N, gen=g)
+    plain = mx.gemm(a, w, b, act=_lib.ACT_GELU_ERF)
+    # residual: bf16(bf16(act(.)) + res) exactly as the bf16 GEMM epilogue
+    x = res.clone()
+    mx.gemm(a, w, b, act=_lib.ACT_GELU_ERF, residual=x, out=x)
+    assert torch.equal(x, (plain.float() + res.float()).to(torch.bfloat16))
+    # mx8 output == oracle quantisation of the bf16 output, bit for bit
+    o = mx.MXTensor.empty(M, N, "cuda")
+    t = mx.gemm(a, w, b, act=_lib.ACT_GELU_ERF, out_mx=o)
+    rq, rsc = omx.quantize(plain.float().cpu().numpy(), rows_pad=t.rows_pad)
+    q, sc = mx_host(t)
+    assert np.array_equal(q, rq)
+    assert np.array_equal(sc[:, :M], rsc[:, :M])
+
+
+def test_gemm_mx_rejects_bad_args(cuda):
+    a = mx.quantize(rnd(64, 96))
+    w = mx.quantize(rnd(64, 96))
+    with pytest.raises(_lib.MMEError):
+        mx.gemm(a, w)  # K % 64 != 0
+
+
+COS_FP8 = 0.99  # per-embedding cosine of the fp8 towers vs the fp32 oracle / reference
+
+
+@pytest.mark.parametrize("name", ["tiny-siglip", "tiny-clip"])
+def test_fp8_towers_tiny_vs_reference(cuda, golden, name):
+    """fp8 mode on the tiny configs vs the reference's fp32 encode_data outputs (golden)."""
+    from helpers import row_cos
+    from mme import encode, get_spec
+    from mme.models import CLIPModel, SiglipModel
+    from mme.processor import Processor
+    from weights_gen import torch_state_dict
+    spec = get_spec(name)
+    g = golden(name)
+    cls = SiglipModel if spec.family == "siglip" else CLIPModel
+    model = cls.from_spec(spec, device="cuda", state_dict=torch_state_dict(spec, 0, torch.bfloat16)).enable_fp8()
+    caps = [g["ids"][i, :l].tolist() for i, l in enumerate(g["lens"])]
+    ie, te = encode.encode_data(model, Processor(spec), spec.m_info, list(g["images"]), caps)
+    assert row_cos(ie, torch.from_numpy(g["img_f32"])).min() >= COS_FP8
+    assert row_cos(te, torch.from_numpy(g["txt_f32"])).min() >= COS_FP8
+
+
+@pytest.mark.slow
+def test_fp8_dfn5b_full_size_vs_oracle(cuda):
+    """BASELINE configs[4] architecture (DFN5B-H, 378 px, quick_gelu) in fp8 vs the fp32 oracle."""
+    from helpers import row_cos
+    from mme import get_spec
+    from mme.models import CLIPModel
+    from mme.processor import synthetic_caption_ids, synthetic_images
+    from mme.weights import random_state_dict
+    from oracle import encoders as oracle_enc
+    spec = get_spec("Apple-DFN5B-H")
+    sd = random_state_dict(spec, seed=0, device="cuda")
+    model = CLIPModel.from_spec(spec, device="cuda", state_dict=sd).enable_fp8()
+    imgs = synthetic_images(1)
+    ids = synthetic_caption_ids(spec, 2)
+    gi = model.encode_images(torch.from_numpy(imgs).cuda()).cpu()
+    gt = model.encode_texts(torch.from_numpy(ids).cuda()).cpu()
+    sd_cpu = {k: v.float().cpu() for k, v in sd.items()}
+    del sd
+    torch.set_num_threads(16)
+    oi, ot = oracle_enc.encode_data(spec, sd_cpu, list(imgs), ids.tolist(), bs=1, out_dtype=torch.float32)
+    assert row_cos(gi, oi).min() >= COS_FP8
+    assert row_cos(gt, ot).min() >= COS_FP8

@@ -19,6 +19,8 @@ from mme import _lib, ops  # noqa: E402
 DIAG_VARIANTS = {22, 23, 26, 27, 33, 34, 35, 36, 37}  # diagnostic builds with deliberately wrong results
 SHAPES = {  # name: (N, K)  with M = rows (SigLIP vision: 256 images x 729 tokens)
     "qkv": (3456, 1152), "o_proj": (1152, 1152), "fc1": (4352, 1152), "fc2": (1152, 4352),
+    # DFN5B-H / ViT-H (d 1280, I 5120): rows 256 x 730
+    "h_qkv": (3840, 1280), "h_fc1": (5120, 1280), "h_fc2": (1280, 5120),
 }
 
 
@@ -27,7 +29,8 @@ def main():
     p.add_argument("--rows", type=int, default=256 * 729)
     p.add_argument("--iters", type=int, default=10)
     p.add_argument("--variants", default="")
-    p.add_argument("--shapes", default=",".join(SHAPES))
+    p.add_argument("--shapes", default="qkv,o_proj,fc1,fc2")
+    p.add_argument("--mx", action="store_true", help="also time the mx8 (block-scaled fp8) GEMM")
     a = p.parse_args()
     lib = _lib.load()
     has_var = hasattr(lib, "mme_gemm_variant")
@@ -65,6 +68,24 @@ def main():
             tf = 2.0 * M * N * K / ms / 1e9
             res[f"{name}/v{v}"] = {"ms": round(ms, 4), "tflops": round(tf, 1)}
             print(f"{name:7s} v{v:<2d} M={M} N={N} K={K}: {ms:8.3f} ms  {tf:7.1f} TFLOP/s", flush=True)
+        if a.mx:
+            from mme import mx
+            Aq, Wq = mx.quantize(A), mx.quantize(W)
+            Cm = mx.gemm(Aq, Wq, out=C)
+            err = (Cm.float() - ref.float()).abs().max().item() if ref is not None else 0.0
+            torch.cuda.synchronize()
+            s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            for rep in range(2):
+                s.record()
+                for _ in range(a.iters):
+                    mx.gemm(Aq, Wq, out=C)
+                e.record()
+                torch.cuda.synchronize()
+                ms = s.elapsed_time(e) / a.iters
+                tf = 2.0 * M * N * K / ms / 1e9
+                res[f"{name}/mx"] = {"ms": round(ms, 4), "tflops": round(tf, 1)}
+                print(f"{name:7s} mx8 M={M} N={N} K={K}: {ms:8.3f} ms  {tf:7.1f} TFLOP/s  (max |mx - bf16| {err:.3g})",
+                      flush=True)
     if has_var:
         lib.mme_gemm_variant(-1)
     print(json.dumps(res))
