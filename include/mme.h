@@ -35,13 +35,14 @@ extern "C" {
 #define MME_ERR_HIP 2         /* HIP runtime error at launch               */
 #define MME_ERR_UNSUPPORTED 3 /* valid request this build does not handle  */
 
-#define MME_ABI_VERSION 2
+#define MME_ABI_VERSION 3
 
 /* activation codes for mme_gemm (HF config.hidden_act) */
 #define MME_ACT_NONE 0
 #define MME_ACT_GELU_TANH 1  /* "gelu_pytorch_tanh" (SigLIP)        */
 #define MME_ACT_QUICK_GELU 2 /* "quick_gelu" (OpenAI CLIP, DFN5B)   */
 #define MME_ACT_GELU_ERF 3   /* "gelu" (LAION ViT-H/14)             */
+#define MME_ACT_GEGLU_TANH 4 /* gated: gelu_tanh(gate) * up (GemmaMLP, ColPali); see mme_gemm */
 
 /* output kinds for mme_preprocess_u8 */
 #define MME_PIX_F32_NCHW 0 /* pixel_values fp32 [n,3,S,S] (HF processor output)   */
@@ -80,7 +81,12 @@ int mme_im2col(const void* pixels, int in_is_f32, int n, int S, int patch, int k
  * Replaces nn.Linear / Conv2d GEMMs of the SigLIP / CLIP towers
  * (TF:models/siglip/modeling_siglip.py:268-322, TF:models/clip/modeling_clip.py).
  * bf16 in, fp32 accumulate (MFMA 16x16x32), bf16 out (or fp32 if out_f32).
- * Requires K % 64 == 0, lda/ldb % 8 == 0 and 16-B aligned A/B rows (C/residual: any ld). */
+ * Requires K % 64 == 0, lda/ldb % 8 == 0 and 16-B aligned A/B rows (C/residual: any ld).
+ * act == MME_ACT_GEGLU_TANH (GemmaMLP act_fn(gate_proj(x)) * up_proj(x),
+ * TF:models/gemma/modeling_gemma.py:95-96): B holds gate and up rows interleaved in
+ * groups of 4 (rows 8k..8k+3 = gate 4k..4k+3, rows 8k+4..8k+7 = up 4k..4k+3), and
+ * C[r, 4k+e] = bf16( bf16(gelu_tanh(bf16 g)) * bf16 u ) is [M, N/2] (N % 8 == 0,
+ * ldc % 4 == 0, no residual, bf16 out). */
 int mme_gemm(const void* A, int lda, const void* B, int ldb, void* C, int ldc, int M, int N, int K,
              const void* bias, const void* residual, int ldr, int res_period, int act, int out_f32,
              void* stream);
@@ -192,6 +198,46 @@ int mme_layernorm_mx(const void* x, int ldx, const void* gamma, const void* beta
 int mme_gemm_mx(const void* A, int lda, const void* sa, int sa_rows, const void* B, int ldb, const void* sb,
                 int sb_rows, void* C, int ldc, void* c_scales, int c_rows_pad, int M, int N, int K, const void* bias,
                 const void* residual, int ldr, int res_period, int act, int out_mx, void* stream);
+
+/* ------------------------------------------------ §8f-1: ColPali encoder ----
+ * ColPali-v1.3 = PaliGemma-3B (SigLIP-448 vision tower + Gemma-2B) + 128-d head,
+ * the model behind the colpali branch of encode_data (main.py:402-405,422-425;
+ * in-container port TF:models/colpali/modeling_colpali.py:107-146). The vision
+ * tower and every GEMM reuse the entry points above; these are the Gemma pieces. */
+
+/* GemmaRMSNorm (TF:models/gemma/modeling_gemma.py:64-78):
+ * y = bf16( x * rsqrt(mean_fp32(x^2) + eps) * (unit_offset + w) ), unit_offset 1 = Gemma's (1 + w).
+ * rows_idx (nullable): output row r reads input row rows_idx[r]. d <= 2048, d % 8 == 0. */
+int mme_rmsnorm(const void* x, int ldx, const void* w, void* y, int ldy, int rows, int d, float eps,
+                int unit_offset, const int32_t* rows_idx, void* stream);
+
+/* Rotary position embedding, in place on heads [0, nheads) of packed rows
+ * (q heads then the k head; GemmaRotaryEmbedding + apply_rotary_pos_emb,
+ * TF:models/gemma/modeling_gemma.py:100-187): position = (row % T) + pos_offset
+ * (PaliGemma: 1, TF:models/paligemma/modeling_paligemma.py:234-237); cos/sin in fp32
+ * rounded to bf16, each product and the sum rounded to bf16 as the bf16 module does. */
+int mme_rope(void* qkv, int ld, int rows, int T, int nheads, int hd, int pos_offset, float theta, void* stream);
+
+/* Gemma decoder input: rows t < P of each length-L sequence take image feature
+ * img[b*P + t] (PaliGemma masked_scatter, the <image> tokens lead a ColPali sequence,
+ * TF:models/paligemma/modeling_paligemma.py:231-246), rows t >= P take
+ * bf16(tok[ids[b,t]] * scale) (GemmaTextScaledWordEmbedding, scale = bf16(sqrt(d))). */
+int mme_gemma_embed(const int64_t* ids, int B, int L, const void* tok, int d, float scale, const void* img,
+                    int ld_img, int P, void* out, int ld_out, void* stream);
+
+/* ColPali head tail: y = bf16( bf16(x / bf16(||x||)) * mask[row] ) (mask: int64
+ * attention_mask rows, nullable = all ones; TF:models/colpali/modeling_colpali.py:136-140). */
+int mme_l2norm_masked(const void* x, int ldx, void* y, int ldy, int rows, int d, const int64_t* mask,
+                      void* stream);
+
+/* Multi-query attention, head dim 256, ONE shared K/V head (Gemma-2B, Hq in {1,2,4,8};
+ * GemmaAttention, TF:models/gemma/modeling_gemma.py:202-292). qkv: bf16 [B*T, ld_qkv],
+ * q head h at column h*256, K at Hq*256, V at (Hq+1)*256. Bidirectional (PaliGemma
+ * prefix attention, use_bidirectional_attention); keys valid in [kstart[b], kend[b])
+ * (nullable -> [0, T); left padding -> kstart = pad count), kend > kstart.
+ * out: bf16 [B*T, ld_out], head h at column h*256. */
+int mme_attention_mqa(const void* qkv, int ld_qkv, void* out, int ld_out, int B, int T, int Hq, int hd,
+                      const int32_t* kstart, const int32_t* kend, float scale, void* stream);
 
 #ifdef __cplusplus
 }

@@ -134,6 +134,12 @@ struct PCfg {
 template <class C, int ACT>
 __device__ __forceinline__ void gemm_epilogue_lds(const GemmArgs& p, char* lds, f32x4 (&acc)[C::FM][C::FN], int m0,
                                                   int n0, int wm, int wn, int g, int li, int tid) {
+    // GeGLU (MME_ACT_GEGLU_TANH): B rows are [gate 4k..4k+3, up 4k..4k+3] per group of 8,
+    // so each 16-B chunk of the bf16 tile holds 4 gate and 4 up outputs of the same
+    // features -> out[:, gc/2 + e] = bf16( bf16(gelu_tanh(bf16 gate)) * bf16 up )
+    // (GemmaMLP.forward act_fn(gate_proj(x)) * up_proj(x), TF:models/gemma/modeling_gemma.py:95-96).
+    constexpr bool GLU = ACT == MME_ACT_GEGLU_TANH;
+    constexpr int RACT = GLU ? MME_ACT_NONE : ACT;
     __syncthreads();
 #pragma unroll
     for (int j = 0; j < C::FN; ++j) {
@@ -148,7 +154,7 @@ __device__ __forceinline__ void gemm_epilogue_lds(const GemmArgs& p, char* lds, 
             const int ml = wm * C::TM + i * 16 + li;
             bf16x4 o;
 #pragma unroll
-            for (int r = 0; r < 4; ++r) o[r] = f2bf(apply_act(acc[i][j][r] + bv[r], ACT));
+            for (int r = 0; r < 4; ++r) o[r] = f2bf(apply_act(acc[i][j][r] + bv[r], RACT));
             *reinterpret_cast<bf16x4*>(lds + ml * C::OUT_LD + nl * 2) = o;
         }
     }
@@ -160,7 +166,13 @@ __device__ __forceinline__ void gemm_epilogue_lds(const GemmArgs& p, char* lds, 
         const int gr = m0 + row, gc = n0 + cc * 8;
         if (gr >= p.M || gc >= p.N) continue;
         u16x8 v = *reinterpret_cast<const u16x8*>(lds + row * C::OUT_LD + cc * 16);
-        if (p.res) {
+        if (GLU) {
+            bf16x4 o;
+#pragma unroll
+            for (int e = 0; e < 4; ++e)
+                o[e] = f2bf(bf2f(f2bf(apply_act(bits2f(v[e]), MME_ACT_GELU_TANH))) * bits2f(v[4 + e]));
+            *reinterpret_cast<bf16x4*>(Cout + (size_t)gr * p.ldc + gc / 2) = o;
+        } else if (p.res) {
             const int rr = p.res_period ? gr % p.res_period : gr;
             const u16x8 rv = *reinterpret_cast<const u16x8*>(p.res + (size_t)rr * p.ldr + gc);
             bf16x8 o;
@@ -622,6 +634,9 @@ int launch_pipe6(const GemmArgs& a, hipStream_t s) {
         case MME_ACT_GELU_ERF:
             hipLaunchKernelGGL((gemm_pipe6_kernel<C, GROUP_M, MME_ACT_GELU_ERF, STAG, DIAG>), grid, block, 0, s, a);
             break;
+        case MME_ACT_GEGLU_TANH:
+            hipLaunchKernelGGL((gemm_pipe6_kernel<C, GROUP_M, MME_ACT_GEGLU_TANH, STAG, DIAG>), grid, block, 0, s, a);
+            break;
         default:
             hipLaunchKernelGGL((gemm_pipe6_kernel<C, GROUP_M, MME_ACT_NONE, STAG, DIAG>), grid, block, 0, s, a);
             break;
@@ -659,14 +674,20 @@ extern "C" int mme_gemm(const void* A, int lda, const void* B, int ldb, void* Cp
     MME_REQUIRE(M > 0 && N > 0 && K > 0, "mme_gemm: empty shape M=%d N=%d K=%d", M, N, K);
     MME_REQUIRE(K % BK == 0, "mme_gemm: K=%d must be a multiple of %d (pad weights/activations)", K, BK);
     MME_REQUIRE(lda % 8 == 0 && ldb % 8 == 0, "mme_gemm: lda/ldb must be multiples of 8 (16-B rows)");
-    MME_REQUIRE(lda >= K && ldb >= K && ldc >= N, "mme_gemm: leading dim smaller than the row");
+    MME_REQUIRE(act >= MME_ACT_NONE && act <= MME_ACT_GEGLU_TANH, "mme_gemm: bad act %d", act);
+    const bool glu = act == MME_ACT_GEGLU_TANH;
+    MME_REQUIRE(lda >= K && ldb >= K && ldc >= (glu ? N / 2 : N), "mme_gemm: leading dim smaller than the row");
     MME_REQUIRE(((uintptr_t)A & 15) == 0 && ((uintptr_t)B & 15) == 0, "mme_gemm: A/B must be 16-byte aligned");
     MME_REQUIRE(!residual || ldr >= N, "mme_gemm: ldr < N");
     MME_REQUIRE(res_period >= 0, "mme_gemm: res_period < 0");
-    MME_REQUIRE(act >= MME_ACT_NONE && act <= MME_ACT_GELU_ERF, "mme_gemm: bad act %d", act);
     GemmArgs a{(const bf16*)A, (const bf16*)B, Cp, (const bf16*)bias, (const bf16*)residual,
                lda, ldb, ldc, ldr, M, N, K, res_period, act, out_f32};
     hipStream_t s = as_stream(stream);
+    if (glu) {  // gated epilogue: the pipelined kernel only (its LDS-staged 16-B tile rows pair gate/up)
+        MME_REQUIRE(N % 8 == 0 && ldc % 4 == 0 && !out_f32 && !residual && ((uintptr_t)Cp & 7) == 0,
+                    "mme_gemm: GeGLU needs N %% 8 == 0, ldc %% 4 == 0, 8-B aligned bf16 C, no residual");
+        return launch_pipe6<Pipe256, 4, 1>(a, s);
+    }
     switch (g_variant) {
         case 0: return launch<BigCfg, 1>(a, s);
         case 1: return launch<BigCfg, 4>(a, s);

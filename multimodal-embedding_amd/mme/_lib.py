@@ -14,9 +14,9 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("MME_LIB", os.path.join(_HERE, "libmme.so"))
 
 # MME_ACT_* / MME_PIX_* from include/mme.h
-ACT_NONE, ACT_GELU_TANH, ACT_QUICK_GELU, ACT_GELU_ERF = 0, 1, 2, 3
+ACT_NONE, ACT_GELU_TANH, ACT_QUICK_GELU, ACT_GELU_ERF, ACT_GEGLU_TANH = 0, 1, 2, 3, 4
 PIX_F32_NCHW, PIX_PATCHES = 0, 1
-ABI_VERSION = 2
+ABI_VERSION = 3
 
 # name -> (restype, argtypes)
 _P = c_void_p
@@ -46,6 +46,11 @@ SIGNATURES = {
     "mme_layernorm_mx": (c_int, [_P, c_int, _P, _P, c_int, c_int, c_float, _P, _P, c_int, _P, c_int, _P]),
     "mme_gemm_mx": (c_int, [_P, c_int, _P, c_int, _P, c_int, _P, c_int, _P, c_int, _P, c_int, c_int, c_int, c_int,
                             _P, _P, c_int, c_int, c_int, c_int, _P]),
+    "mme_rmsnorm": (c_int, [_P, c_int, _P, _P, c_int, c_int, c_int, c_float, c_int, _P, _P]),
+    "mme_rope": (c_int, [_P, c_int, c_int, c_int, c_int, c_int, c_int, c_float, _P]),
+    "mme_gemma_embed": (c_int, [_P, c_int, c_int, _P, c_int, c_float, _P, c_int, c_int, _P, c_int, _P]),
+    "mme_l2norm_masked": (c_int, [_P, c_int, _P, c_int, c_int, c_int, _P, _P]),
+    "mme_attention_mqa": (c_int, [_P, c_int, _P, c_int, c_int, c_int, c_int, c_int, _P, _P, c_float, _P]),
 }
 
 

@@ -8,7 +8,7 @@ safetensors / HF state dict (mme.weights).
 from __future__ import annotations
 
 from dataclasses import dataclass, field, replace
-from typing import Dict, Optional, Tuple
+from typing import Dict, Optional, Sequence, Tuple
 
 from ._lib import ACT_GELU_ERF, ACT_GELU_TANH, ACT_QUICK_GELU
 
@@ -151,12 +151,91 @@ TINY: Dict[str, ModelSpec] = {
 }
 
 
-def get_spec(name: str) -> ModelSpec:
+@dataclass(frozen=True)
+class GemmaConfig:
+    """Gemma decoder of PaliGemma (TF:models/gemma/configuration_gemma.py:64-83)."""
+    hidden: int
+    intermediate: int
+    layers: int
+    heads: int            # query heads; ONE key/value head (MQA)
+    head_dim: int
+    vocab: int
+    eps: float = 1e-6
+    theta: float = 10000.0
+
+
+@dataclass(frozen=True)
+class ColPaliSpec:
+    """ColPali = PaliGemma (SigLIP vision tower without head + Gemma) + 128-d head.
+
+    Token layout (TF:models/colpali/processing_colpali.py:113-142): an image is
+    [<image>] * P + [bos] + prompt("Describe the image.") + ["\\n"]; a query is
+    [bos] + prefix("Question: ") + caption + [pad] * 10 (query augmentation) + ["\\n"].
+    The Gemma tokenizer pads on the LEFT (TF:models/gemma/tokenization_gemma.py:55).
+    Vocab files are absent offline: prompt / prefix ids are fixed synthetic ids."""
+    name: str
+    hub_id: str
+    vision: VisionConfig
+    text: GemmaConfig
+    image_proc: ImageProcConfig
+    image_token_id: int
+    bos_id: int = 2
+    eos_id: int = 1
+    pad_id: int = 0
+    newline_id: int = 108
+    prompt_ids: Tuple[int, ...] = (50721, 573, 2416, 235265)   # synthetic "Describe the image."
+    query_prefix_ids: Tuple[int, ...] = (9413, 235292, 235248)  # synthetic "Question: "
+    n_aug: int = 10
+    dim: int = 128
+    batch_size: int = 4   # main.py:130
+    family: str = "colpali"
+
+    @property
+    def image_seq_len(self) -> int:
+        return self.vision.num_patches
+
+    @property
+    def image_tokens(self) -> Tuple[int, ...]:
+        return (self.image_token_id,) * self.image_seq_len + (self.bos_id,) + self.prompt_ids + (self.newline_id,)
+
+    def query_tokens(self, caption: Sequence[int]) -> Tuple[int, ...]:
+        return ((self.bos_id,) + self.query_prefix_ids + tuple(int(c) for c in caption) +
+                (self.pad_id,) * self.n_aug + (self.newline_id,))
+
+    @property
+    def m_info(self) -> dict:
+        return {"name": self.name, "id": self.hub_id, "type": "colpali", "batch_size": self.batch_size}
+
+    def with_batch_size(self, bs: int) -> "ColPaliSpec":
+        return replace(self, batch_size=bs)
+
+
+COLPALI: Dict[str, ColPaliSpec] = {
+    # vidore/colpali-v1.3 on PaliGemma-3B-pt-448 (vision 27 x 1152, Gemma-2B 18 x 2048, MQA 8 x 256)
+    "ColPali-v1.3": ColPaliSpec(
+        "ColPali-v1.3", "vidore/colpali-v1.3",
+        VisionConfig(hidden=1152, intermediate=4304, layers=27, heads=16, act="gelu_pytorch_tanh", eps=1e-6,
+                     image_size=448, patch=14),
+        GemmaConfig(hidden=2048, intermediate=16384, layers=18, heads=8, head_dim=256, vocab=257216),
+        ImageProcConfig(448, "square", IMAGENET_STANDARD_MEAN, IMAGENET_STANDARD_STD), image_token_id=257152),
+    "tiny-colpali": ColPaliSpec(
+        "tiny-colpali", "-",
+        VisionConfig(hidden=576, intermediate=600, layers=2, heads=8, act="gelu_pytorch_tanh", eps=1e-6,
+                     image_size=56, patch=14),
+        GemmaConfig(hidden=512, intermediate=1024, layers=2, heads=2, head_dim=256, vocab=1000),
+        ImageProcConfig(56, "square", IMAGENET_STANDARD_MEAN, IMAGENET_STANDARD_STD), image_token_id=998,
+        prompt_ids=(300, 301, 302, 303), query_prefix_ids=(400, 401)),
+}
+
+
+def get_spec(name: str):
     if name in REGISTRY:
         return REGISTRY[name]
     if name in TINY:
         return TINY[name]
-    raise KeyError(f"unknown model {name!r}; known: {sorted(REGISTRY) + sorted(TINY)}")
+    if name in COLPALI:
+        return COLPALI[name]
+    raise KeyError(f"unknown model {name!r}; known: {sorted(REGISTRY) + sorted(TINY) + sorted(COLPALI)}")
 
 
 def image_flops(spec: ModelSpec) -> float:

@@ -19,6 +19,8 @@ from . import ops
 def encode_data(model, processor, m_info: dict, images: Sequence, texts: Sequence, device="cuda"
                 ) -> Tuple[torch.Tensor, torch.Tensor]:
     bs = m_info["batch_size"]
+    if m_info.get("type") == "colpali":
+        return encode_colpali(model, processor, bs, images, texts, device)
     img_list: List[torch.Tensor] = []
     for i in range(0, len(images), bs):
         inputs = processor(images=images[i:i + bs], return_tensors="pt", padding=True).to(device)
@@ -36,3 +38,22 @@ def encode_data(model, processor, m_info: dict, images: Sequence, texts: Sequenc
     img = torch.cat(img_list) if img_list else torch.empty(0)
     txt = torch.cat(txt_list) if txt_list else torch.empty(0)
     return img, txt
+
+
+@torch.no_grad()
+def encode_colpali(model, processor, bs: int, images: Sequence, texts: Sequence, device="cuda"
+                   ) -> Tuple[List[torch.Tensor], List[torch.Tensor]]:
+    """The colpali branch (main.py:402-405,422-425): process_images / process_queries ->
+    model(**inputs) -> one [T, 128] CPU tensor per item (padding rows included, zero).
+    The per-item lists are returned intact: main.py:416,436 torch.cat them into one
+    [sum T, 128] tensor, which compute_similarity_scores then splits into single rows
+    (SURVEY.md §0.2); mme keeps the list the scorer needs."""
+    img_list: List[torch.Tensor] = []
+    for i in range(0, len(images), bs):
+        out = model(**processor.process_images(images[i:i + bs]).to(device))
+        img_list.extend([o.cpu() for o in out])
+    txt_list: List[torch.Tensor] = []
+    for i in range(0, len(texts), bs):
+        out = model(**processor.process_queries(texts[i:i + bs]).to(device))
+        txt_list.extend([o.cpu() for o in out])
+    return img_list, txt_list

@@ -91,6 +91,18 @@ class VisionTower:
         pooled = ops.layernorm(x, w.post_ln_g, w.post_ln_b, cfg.eps, rows_idx=rows)
         return ops.gemm(pooled, w.proj_w)
 
+    def forward_tokens(self, patches: torch.Tensor, B: int) -> torch.Tensor:
+        """SigLIP tower without pooling head (PaliGemma's vision_tower, vision_use_head=False,
+        TF:models/siglip/modeling_siglip.py:597-619): post-LN hidden states [B*P, d] bf16."""
+        cfg, w = self.cfg, self.w
+        P, d = cfg.num_patches, cfg.hidden
+        x = ops.gemm(patches, w.patch_w, w.patch_b, residual=w.pos, res_period=P,
+                     algo_flops=2.0 * B * P * d * 3 * cfg.patch ** 2)
+        bufs = _Bufs(B * P, cfg, patches.device)
+        for L in w.layers:
+            encoder_layer(x, L, cfg, B, P, bufs)
+        return ops.layernorm(x, w.post_ln_g, w.post_ln_b, cfg.eps, out=bufs.h)
+
     def _map_head(self, x, B, T, bufs) -> torch.Tensor:
         """post_layernorm + SiglipMultiheadAttentionPoolingHead (TF:…siglip.py:611-644)."""
         cfg, w, hw = self.cfg, self.w, self.w.head

@@ -120,8 +120,9 @@ def gemm(a: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None, 
     N = w.shape[0]
     if w.shape[1] != K:
         raise ValueError(f"gemm: a is [*, {K}] but w is {tuple(w.shape)}")
+    n_out = N // 2 if act == _lib.ACT_GEGLU_TANH else N  # gated: gate/up rows interleaved by 4 (mme.h)
     if out is None:
-        out = torch.empty(M, N, dtype=torch.float32 if out_f32 else BF16, device=a.device)
+        out = torch.empty(M, n_out, dtype=torch.float32 if out_f32 else BF16, device=a.device)
     lda, ldb, ldc = _rowmajor(a, "a"), _rowmajor(w, "w"), _rowmajor(out, "out")
     ldr = 0
     if residual is not None:
@@ -131,7 +132,8 @@ def gemm(a: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None, 
     ev = KernelTimer.begin()
     call("mme_gemm", a.data_ptr(), lda, w.data_ptr(), ldb, out.data_ptr(), ldc, M, N, K, _ptr(bias),
          _ptr(residual), ldr, res_period, act, int(out_f32), _stream())
-    KernelTimer.end(ev, "gemm", algo_flops if algo_flops is not None else 2.0 * M * N * K, 2.0 * (M * K + N * K + M * N))
+    KernelTimer.end(ev, "gemm", algo_flops if algo_flops is not None else 2.0 * M * N * K,
+                    2.0 * (M * K + N * K + M * n_out))
     return out
 
 
@@ -187,6 +189,79 @@ def probe_attention(q: torch.Tensor, kv: torch.Tensor, B: int, T: int, H: int, h
     scale = hd ** -0.5 if scale is None else scale
     call("mme_probe_attention", q.data_ptr(), kv.data_ptr(), _rowmajor(kv, "kv"), out.data_ptr(),
          _rowmajor(out, "out"), B, T, H, hd, float(scale), _stream())
+    return out
+
+
+# ---------------------------------------------------------------- Gemma / ColPali pieces
+def rmsnorm(x: torch.Tensor, w: torch.Tensor, eps: float, *, unit_offset: bool = True,
+            out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """GemmaRMSNorm: bf16(x * rsqrt(mean x^2 + eps) * (1 + w)) with fp32 statistics."""
+    _dev(x, w, out)
+    rows, d = x.shape[0], w.numel()
+    if out is None:
+        out = torch.empty(rows, d, dtype=BF16, device=x.device)
+    call("mme_rmsnorm", x.data_ptr(), _rowmajor(x, "x"), w.data_ptr(), out.data_ptr(), _rowmajor(out, "out"), rows, d,
+         float(eps), int(unit_offset), None, _stream())
+    return out
+
+
+def rope_(qkv: torch.Tensor, T: int, nheads: int, hd: int, pos_offset: int, theta: float) -> torch.Tensor:
+    """Rotary embedding in place on heads [0, nheads) of packed rows (position = row % T + pos_offset)."""
+    _dev(qkv)
+    call("mme_rope", qkv.data_ptr(), _rowmajor(qkv, "qkv"), qkv.shape[0], T, nheads, hd, int(pos_offset),
+         float(theta), _stream())
+    return qkv
+
+
+def gemma_embed(ids: torch.Tensor, tok: torch.Tensor, scale: float, *, img: Optional[torch.Tensor] = None,
+                img_prefix: int = 0, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Decoder input rows: image features for t < img_prefix, bf16(tok[id] * scale) otherwise."""
+    _dev(ids, tok, img, out)
+    if ids.dtype != torch.int64 or ids.dim() != 2:
+        raise ValueError("gemma_embed: ids must be int64 [B, L]")
+    ids = ids.contiguous()
+    B, L = ids.shape
+    d = tok.shape[1]
+    if img_prefix and (img is None or img.shape[0] != B * img_prefix):
+        raise ValueError(f"gemma_embed: image features must be [B*{img_prefix}, d]")
+    if out is None:
+        out = torch.empty(B * L, d, dtype=BF16, device=ids.device)
+    call("mme_gemma_embed", ids.data_ptr(), B, L, tok.data_ptr(), d, float(scale), _ptr(img),
+         _rowmajor(img, "img") if img is not None else 0, int(img_prefix), out.data_ptr(), _rowmajor(out, "out"),
+         _stream())
+    return out
+
+
+def l2norm_masked(x: torch.Tensor, mask: Optional[torch.Tensor], out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """bf16(bf16(x / bf16||x||) * mask[row]); mask int64 per row (the flattened attention_mask)."""
+    _dev(x, mask, out)
+    rows, d = x.shape
+    if mask is not None and (mask.dtype != torch.int64 or mask.numel() != rows):
+        raise ValueError("l2norm_masked: mask must be int64 with one entry per row")
+    if out is None:
+        out = torch.empty(rows, d, dtype=BF16, device=x.device)
+    call("mme_l2norm_masked", x.data_ptr(), _rowmajor(x, "x"), out.data_ptr(), _rowmajor(out, "out"), rows, d,
+         _ptr(mask.contiguous() if mask is not None else None), _stream())
+    return out
+
+
+def attention_mqa(qkv: torch.Tensor, B: int, T: int, Hq: int, hd: int, *, kstart: Optional[torch.Tensor] = None,
+                  kend: Optional[torch.Tensor] = None, scale: Optional[float] = None,
+                  out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Bidirectional multi-query attention (one K/V head) over packed [q heads | k | v] rows."""
+    _dev(qkv, kstart, kend, out)
+    if qkv.shape[0] != B * T:
+        raise ValueError(f"attention_mqa: qkv has {qkv.shape[0]} rows, expected B*T={B * T}")
+    for t in (kstart, kend):
+        if t is not None and (t.dtype != torch.int32 or t.numel() != B):
+            raise ValueError("attention_mqa: kstart / kend must be int32 [B]")
+    if out is None:
+        out = torch.empty(B * T, Hq * hd, dtype=BF16, device=qkv.device)
+    scale = hd ** -0.5 if scale is None else scale
+    ev = KernelTimer.begin()
+    call("mme_attention_mqa", qkv.data_ptr(), _rowmajor(qkv, "qkv"), out.data_ptr(), _rowmajor(out, "out"), B, T, Hq,
+         hd, _ptr(kstart), _ptr(kend), float(scale), _stream())
+    KernelTimer.end(ev, "attention", 4.0 * B * Hq * T * T * hd)
     return out
 
 

@@ -285,11 +285,121 @@ def make_l2norm(main):
     print("l2norm.npz", y.shape)
 
 
+# ------------------------------------------------------------------ ColPali encoder
+class ColPaliRefModel:
+    """model(**inputs) -> embeddings tensor [B, L, 128] (colpali_engine's ColPali returns the
+    tensor; transformers' ColPaliForRetrieval wraps it in .embeddings)."""
+
+    def __init__(self, hf):
+        self.hf = hf
+
+    def __call__(self, **kw):
+        return self.hf(**kw).embeddings
+
+
+class ColPaliRefProcessor:
+    """process_images / process_queries with the ColPaliProcessor layout
+    (TF:models/colpali/processing_colpali.py:113-142) over pre-tokenized ids:
+    images [<image>]*P + [bos] + prompt + [\\n]; queries [bos] + prefix + ids + [pad]*10 + [\\n],
+    left-padded (Gemma tokenizer padding_side='left'), token_type_ids all 0."""
+
+    def __init__(self, spec, image_proc):
+        self.spec, self.ip = spec, image_proc
+
+    def _batch(self, rows):
+        from transformers import BatchFeature
+        L = max(len(r) for r in rows)
+        ids = torch.full((len(rows), L), self.spec.pad_id, dtype=torch.int64)
+        mask = torch.zeros((len(rows), L), dtype=torch.int64)
+        for i, r in enumerate(rows):
+            ids[i, L - len(r):] = torch.tensor(r)
+            mask[i, L - len(r):] = 1
+        return BatchFeature({"input_ids": ids, "attention_mask": mask, "token_type_ids": torch.zeros_like(ids)})
+
+    def process_images(self, images):
+        b = self._batch([list(self.spec.image_tokens)] * len(images))
+        b["pixel_values"] = self.ip(images=images, return_tensors="pt")["pixel_values"]
+        return b
+
+    def process_queries(self, queries):
+        return self._batch([list(self.spec.query_tokens(q)) for q in queries])
+
+
+def hf_colpali(spec, dtype):
+    from transformers import ColPaliConfig, ColPaliForRetrieval
+    v, t = spec.vision, spec.text
+    vc = dict(model_type="siglip_vision_model", hidden_size=v.hidden, intermediate_size=v.intermediate,
+              num_hidden_layers=v.layers, num_attention_heads=v.heads, image_size=v.image_size, patch_size=v.patch,
+              hidden_act=v.act, layer_norm_eps=v.eps, vision_use_head=False)
+    tc = dict(model_type="gemma", hidden_size=t.hidden, intermediate_size=t.intermediate, num_hidden_layers=t.layers,
+              num_attention_heads=t.heads, num_key_value_heads=1, head_dim=t.head_dim, vocab_size=t.vocab,
+              rms_norm_eps=t.eps, hidden_act="gelu_pytorch_tanh", pad_token_id=spec.pad_id, bos_token_id=spec.bos_id,
+              eos_token_id=spec.eos_id)
+    cfg = ColPaliConfig(vlm_config=dict(model_type="paligemma", vision_config=vc, text_config=tc,
+                                        image_token_index=spec.image_token_id, vocab_size=t.vocab,
+                                        projection_dim=t.hidden, hidden_size=t.hidden), embedding_dim=spec.dim)
+    m = ColPaliForRetrieval(cfg)
+    sd = torch_state_dict(spec, seed=0)
+    missing, unexpected = m.load_state_dict(sd, strict=False)
+    assert not missing and not unexpected, (missing, unexpected)
+    return m.to(dtype).eval()
+
+
+def make_colpali(main):
+    from PIL import Image
+    from transformers.models.siglip.image_processing_pil_siglip import SiglipImageProcessorPil
+    from mme.config import COLPALI
+
+    spec = COLPALI["tiny-colpali"]
+    S = spec.vision.image_size
+    rng = np.random.default_rng(11)
+    imgs = rng.integers(0, 256, (5, 96, 80, 3), dtype=np.uint8)
+    pil = [Image.fromarray(a) for a in imgs]
+    lens = [7, 3, 12, 5, 9, 4, 10]
+    caps = [rng.integers(3, 990, L).tolist() for L in lens]
+    proc = ColPaliRefProcessor(spec, SiglipImageProcessorPil(size={"height": S, "width": S}))
+    m_info = {"name": "tiny-colpali", "type": "colpali", "batch_size": spec.batch_size}
+    out = {"images": imgs, "cap_lens": np.array(lens, np.int64), "cap_ids": np.concatenate(caps).astype(np.int64)}
+    for tag, dtype in (("bf16", torch.bfloat16), ("f32", torch.float32)):
+        model = ColPaliRefModel(hf_colpali(spec, dtype))
+        main.DEVICE, main.DTYPE = "cpu", dtype
+        with torch.no_grad():
+            # encode_data concatenates the per-item [T, 128] outputs along rows (main.py:416,436;
+            # the flattening defect of SURVEY §0.2): the row counts below split them again
+            cat_i, cat_t = main.encode_data(model, proc, m_info, pil, caps)
+        bs = spec.batch_size
+        img_rows = [len(spec.image_tokens)] * len(pil)
+        txt_rows = []
+        for s in range(0, len(caps), bs):
+            Lb = max(len(spec.query_tokens(c)) for c in caps[s:s + bs])
+            txt_rows += [Lb] * len(caps[s:s + bs])
+        assert cat_i.shape[0] == sum(img_rows) and cat_t.shape[0] == sum(txt_rows)
+        out["img_rows"], out["txt_rows"] = np.array(img_rows, np.int64), np.array(txt_rows, np.int64)
+        if tag == "bf16":
+            out["img_bf16"], out["txt_bf16"] = bf16_bits(cat_i), bf16_bits(cat_t)
+
+            class Scorer:  # colpali_engine score -> transformers' score_retrieval stand-in
+                def score(self, qs, ps):
+                    from transformers.models.colpali.processing_colpali import ColPaliProcessor
+                    return ColPaliProcessor.score_retrieval(None, qs, ps, output_dtype=torch.float32)
+
+            # T2I orientation of run_bootstrap_benchmark with per-item lists kept intact
+            # (the mme semantics, DESIGN §1): queries = captions, docs = images
+            img_l, txt_l = list(cat_i.split(img_rows)), list(cat_t.split(txt_rows))
+            out["t2i_score"] = main.compute_similarity_scores(img_l, txt_l, {"type": "colpali"}, Scorer()).numpy()
+        else:
+            out["img_f32"], out["txt_f32"] = cat_i.numpy(), cat_t.numpy()
+    np.savez_compressed(os.path.join(HERE, "tiny-colpali.npz"), **out)
+    print("tiny-colpali.npz:", {k: v.shape for k, v in out.items()})
+
+
 if __name__ == "__main__":
     torch.manual_seed(0)
     main = import_reference()
-    make_preprocess()
-    make_l2norm(main)
-    make_retrieval(main)
-    make_maxsim(main)
-    make_encoders(main)
+    only = sys.argv[1:]
+    steps = {"preprocess": make_preprocess, "l2norm": lambda: make_l2norm(main),
+             "retrieval": lambda: make_retrieval(main), "maxsim": lambda: make_maxsim(main),
+             "encoders": lambda: make_encoders(main), "colpali": lambda: make_colpali(main)}
+    for name, fn in steps.items():
+        if not only or name in only:
+            fn()

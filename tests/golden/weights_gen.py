@@ -81,7 +81,63 @@ def np_state_dict(spec, seed: int = 0) -> Dict[str, np.ndarray]:
     return sd
 
 
+def np_state_dict_colpali(spec, seed: int = 0) -> Dict[str, np.ndarray]:
+    """transformers ColPaliForRetrieval names/shapes (vlm.vision_tower.*, vlm.multi_modal_projector.*,
+    vlm.language_model.*, embedding_proj_layer.*) for a ColPaliSpec."""
+    rng = np.random.default_rng(seed)
+    sd: Dict[str, np.ndarray] = {}
+
+    def put(name, arr):
+        sd[name] = bf16_round(np.asarray(arr, dtype=np.float32))
+
+    def lin(name, out_f, in_f, bias=True):
+        a = math.sqrt(6.0 / (in_f + out_f))
+        put(name + ".weight", rng.uniform(-a, a, (out_f, in_f)))
+        if bias:
+            put(name + ".bias", rng.normal(0, 0.02, out_f))
+
+    def ln(name, d):
+        put(name + ".weight", 1.0 + rng.normal(0, 0.05, d))
+        put(name + ".bias", rng.normal(0, 0.02, d))
+
+    v, t = spec.vision, spec.text
+    d = v.hidden
+    pre = "vlm.vision_tower."
+    put(pre + "embeddings.patch_embedding.weight", rng.normal(0, 1 / math.sqrt(3 * v.patch * v.patch),
+                                                              (d, 3, v.patch, v.patch)))
+    put(pre + "embeddings.patch_embedding.bias", rng.normal(0, 0.02, d))
+    put(pre + "embeddings.position_embedding.weight", rng.normal(0, 1 / math.sqrt(d), (v.num_patches, d)))
+    for i in range(v.layers):
+        p = f"{pre}encoder.layers.{i}."
+        ln(p + "layer_norm1", d)
+        for n in ("q_proj", "k_proj", "v_proj", "out_proj"):
+            lin(p + "self_attn." + n, d, d)
+        ln(p + "layer_norm2", d)
+        lin(p + "mlp.fc1", v.intermediate, d)
+        lin(p + "mlp.fc2", d, v.intermediate)
+    ln(pre + "post_layernorm", d)
+    lin("vlm.multi_modal_projector.linear", t.hidden, d)
+    D, H, hd = t.hidden, t.heads, t.head_dim
+    lm = "vlm.language_model."
+    put(lm + "embed_tokens.weight", rng.normal(0, 1 / D, (t.vocab, D)))
+    for i in range(t.layers):
+        p = f"{lm}layers.{i}."
+        put(p + "input_layernorm.weight", rng.normal(0, 0.1, D))
+        lin(p + "self_attn.q_proj", H * hd, D, bias=False)
+        lin(p + "self_attn.k_proj", hd, D, bias=False)
+        lin(p + "self_attn.v_proj", hd, D, bias=False)
+        lin(p + "self_attn.o_proj", D, H * hd, bias=False)
+        put(p + "post_attention_layernorm.weight", rng.normal(0, 0.1, D))
+        lin(p + "mlp.gate_proj", t.intermediate, D, bias=False)
+        lin(p + "mlp.up_proj", t.intermediate, D, bias=False)
+        lin(p + "mlp.down_proj", D, t.intermediate, bias=False)
+    put(lm + "norm.weight", rng.normal(0, 0.1, D))
+    lin("embedding_proj_layer", spec.dim, D)
+    return sd
+
+
 def torch_state_dict(spec, seed: int = 0, dtype=None):
     import torch
     dtype = dtype or torch.float32
-    return {k: torch.from_numpy(v.copy()).to(dtype) for k, v in np_state_dict(spec, seed).items()}
+    gen = np_state_dict_colpali if getattr(spec, "family", "") == "colpali" else np_state_dict
+    return {k: torch.from_numpy(v.copy()).to(dtype) for k, v in gen(spec, seed).items()}

@@ -1,0 +1,199 @@
+"""ColPali encoder on the MI355X: Gemma kernels vs fp32 references,
+the tiny model vs the reference's encode_data outputs (tests/golden/tiny-colpali.npz),
+fast paths vs the HF surface, and the full-size ColPali-v1.3 towers vs the CPU oracle.
+
+Tolerances: kernels whose rounding steps are restated exactly (RMSNorm, RoPE,
+embedding assembly, masked L2) are compared bit-exactly against a torch
+restatement of the same bf16 ops, or within one bf16 ulp where fp32 reduction
+order differs; MFMA paths (attention, GeGLU GEMM) against fp32 within bf16
+output rounding; whole towers by per-token cosine >= 0.999.
+"""
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+from helpers import bits_to_f32, row_cos
+from mme import ops
+from mme._lib import ACT_GEGLU_TANH
+from mme.colpali_encoder import ColPaliModel, ColPaliProcessor, interleave_gate_up
+from mme.config import COLPALI
+from weights_gen import torch_state_dict
+
+pytestmark = pytest.mark.gpu
+BF = torch.bfloat16
+SPEC = COLPALI["tiny-colpali"]
+
+
+def _ulps(a, b):
+    ai = a.to(BF).view(torch.int16).int()
+    bi = b.to(BF).view(torch.int16).int()
+    return (ai - bi).abs().max().item()
+
+
+def test_rmsnorm_matches_gemma_module(cuda):
+    g = torch.Generator().manual_seed(0)
+    x = (torch.randn(333, 2048, generator=g) * 3).to(BF)
+    w = (torch.randn(2048, generator=g) * 0.3).to(BF)
+    xf = x.float()
+    ref = ((xf * torch.rsqrt(xf.pow(2).mean(-1, keepdim=True) + 1e-6)) * (1.0 + w.float())).to(BF)
+    got = ops.rmsnorm(x.cuda(), w.cuda(), 1e-6).cpu()
+    assert _ulps(got, ref) <= 1
+
+
+def test_rope_matches_oracle(cuda):
+    from oracle.colpali_encoder import _rope
+    g = torch.Generator().manual_seed(1)
+    B, T, H, hd = 3, 77, 8, 256
+    qkv = torch.randn(B * T, (H + 2) * hd, generator=g).to(BF)
+    got = ops.rope_(qkv.clone().cuda(), T, H + 1, hd, 1, 10000.0).cpu()
+    pos = torch.arange(T, dtype=torch.float) + 1
+    x = qkv.view(B, T, H + 2, hd)[:, :, : H + 1].transpose(1, 2)  # [B, H+1, T, hd]
+    ref = _rope(x, pos, 10000.0).transpose(1, 2).reshape(B * T, (H + 1) * hd)
+    assert _ulps(got[:, : (H + 1) * hd], ref) <= 1
+    frac = (got[:, : (H + 1) * hd].view(torch.int16) == ref.view(torch.int16)).float().mean().item()
+    assert frac > 0.999
+    assert torch.equal(got[:, (H + 1) * hd:], qkv[:, (H + 1) * hd:])  # V untouched
+
+
+@pytest.mark.parametrize("B,T,Hq,left", [(2, 1030, 8, False), (3, 45, 8, True), (5, 33, 2, True), (1, 7, 4, False)])
+def test_attention_mqa_vs_fp32(cuda, B, T, Hq, left):
+    g = torch.Generator().manual_seed(T)
+    hd = 256
+    qkv = (torch.randn(B * T, (Hq + 2) * hd, generator=g) * 0.5).to(BF)
+    lens = torch.randint(max(1, T // 3), T + 1, (B,), generator=g)
+    lens[0] = T
+    ks = (T - lens) if left else torch.zeros(B, dtype=torch.long)
+    ke = ks + lens
+    got = ops.attention_mqa(qkv.cuda(), B, T, Hq, hd, kstart=ks.int().cuda(), kend=ke.int().cuda()).cpu().float()
+    x = qkv.float().view(B, T, Hq + 2, hd)
+    q, k, v = x[:, :, :Hq].transpose(1, 2), x[:, :, Hq:Hq + 1].transpose(1, 2), x[:, :, Hq + 1:].transpose(1, 2)
+    s = q @ k.transpose(-1, -2) * hd ** -0.5
+    keys = torch.arange(T)
+    valid = (keys[None, :] >= ks[:, None]) & (keys[None, :] < ke[:, None])
+    s = s.masked_fill(~valid[:, None, None, :], float("-inf"))
+    ref = (torch.softmax(s, -1) @ v).transpose(1, 2).reshape(B * T, Hq * hd)
+    err = (got - ref).abs().max().item()
+    assert err < 2e-2, err
+    assert row_cos(got, ref).min() > 0.9995
+
+
+def test_geglu_gemm_vs_fp32(cuda):
+    g = torch.Generator().manual_seed(3)
+    M, K, I = 700, 512, 1024
+    a = (torch.randn(M, K, generator=g)).to(BF)
+    gate = (torch.randn(I, K, generator=g) / K ** 0.5).to(BF)
+    up = (torch.randn(I, K, generator=g) / K ** 0.5).to(BF)
+    got = ops.gemm(a.cuda(), interleave_gate_up(gate, up).cuda(), act=ACT_GEGLU_TANH).cpu()
+    assert got.shape == (M, I)
+    gb = (a.float() @ gate.float().T).to(BF)
+    ub = (a.float() @ up.float().T).to(BF)
+    ref = (F.gelu(gb.float(), approximate="tanh").to(BF).float() * ub.float()).to(BF)
+    # fp32 accumulation order may flip the bf16 rounding of gate / up (then propagated): allow
+    # 2 bf16 ulps of the product, and require most outputs to be bit-identical
+    err = (got.float() - ref.float()).abs()
+    bound = 2 * 2.0 ** -7 * ref.float().abs() + 1e-3
+    assert bool((err <= bound).all()), float((err - bound).max())
+    assert (got.view(torch.int16) == ref.view(torch.int16)).float().mean().item() > 0.95
+
+
+def test_gemma_embed_and_masked_l2(cuda):
+    g = torch.Generator().manual_seed(4)
+    B, L, P, d, V = 3, 20, 6, 512, 1000
+    tok = torch.randn(V, d, generator=g).to(BF)
+    ids = torch.randint(0, V, (B, L), generator=g)
+    img = torch.randn(B * P, d, generator=g).to(BF)
+    scale = float(torch.tensor(d ** 0.5).to(BF))
+    got = ops.gemma_embed(ids.cuda(), tok.cuda(), scale, img=img.cuda(), img_prefix=P).cpu().view(B, L, d)
+    ref = tok[ids] * torch.tensor(scale).to(BF)
+    ref[:, :P] = img.view(B, P, d)
+    assert torch.equal(got, ref)
+    x = (torch.randn(B * L, 128, generator=g) * 2).to(BF)
+    mask = torch.randint(0, 2, (B * L,), generator=g)
+    y = ops.l2norm_masked(x.cuda(), mask.cuda()).cpu()
+    ref = (x / x.norm(dim=-1, keepdim=True)) * mask[:, None]
+    assert torch.equal(y.view(torch.int16), ref.view(torch.int16))
+
+
+def _tiny_model():
+    return ColPaliModel.from_spec(SPEC, device="cuda", state_dict=torch_state_dict(SPEC, 0, BF))
+
+
+def _captions(g):
+    return [c.tolist() for c in np.split(g["cap_ids"], np.cumsum(g["cap_lens"])[:-1])]
+
+
+def test_tiny_colpali_vs_reference(cuda, golden):
+    """mme.encode.encode_data's colpali branch over the processor / model duck type vs main.encode_data."""
+    from mme import encode
+    g = golden("tiny-colpali")
+    model, proc = _tiny_model(), ColPaliProcessor(SPEC)
+    ie, te = encode.encode_data(model, proc, SPEC.m_info, list(g["images"]), _captions(g))
+    gi, gt = torch.cat(ie), torch.cat(te)
+    assert [e.shape[0] for e in ie] == g["img_rows"].tolist() and [e.shape[0] for e in te] == g["txt_rows"].tolist()
+    for got, key in ((gi, "img"), (gt, "txt")):
+        r32 = torch.from_numpy(g[key + "_f32"])
+        r16 = torch.from_numpy(bits_to_f32(g[key + "_bf16"]))
+        keep = r32.abs().sum(1) > 0
+        assert torch.equal(got.float().abs().sum(1) > 0, keep), f"{key}: zero (padding) rows differ"
+        assert row_cos(got[keep], r32[keep]).min() >= 0.999, key
+        assert row_cos(got[keep], r16[keep]).min() >= 0.999, key
+
+
+def test_tiny_fast_paths_and_scores(cuda, golden):
+    """encode_images(u8) / encode_queries(ids) == the HF surface rows; MaxSim over them vs the
+    reference chunk loop on the reference's own embeddings (T2I)."""
+    from mme import encode
+    from mme.colpali import maxsim_scores, pack_multivectors
+    g = golden("tiny-colpali")
+    model, proc = _tiny_model(), ColPaliProcessor(SPEC)
+    caps = _captions(g)
+    ie, te = encode.encode_data(model, proc, SPEC.m_info, list(g["images"]), caps)
+    fi = model.encode_images(torch.from_numpy(g["images"]).cuda(), batch=2).cpu()
+    assert torch.equal(fi, torch.stack(ie))
+    Q, ql, qpad = model.encode_queries(caps, exec_batch=2)
+    for i, e in enumerate(te):
+        n = int(ql[i])
+        assert torch.equal(Q[i, :n].cpu(), e[e.shape[0] - n:]), i
+    assert qpad.cpu().tolist() == g["txt_rows"].tolist()
+    D, dl = pack_multivectors(list(fi), device="cuda")  # zero-padded to a multiple of 16 tokens
+    s = maxsim_scores(Q, ql, D, dl, doc_chunk=10).cpu().numpy()
+    ref = g["t2i_score"]
+    assert np.abs(s - ref).max() <= 0.05 + 0.01 * np.abs(ref).max()
+    assert np.array_equal(s.argmax(1), ref.argmax(1))
+
+
+@pytest.mark.slow
+def test_full_size_colpali_vs_oracle(cuda):
+    from oracle import colpali_encoder as oc
+    from mme.colpali_encoder import random_state_dict
+    from mme.processor import synthetic_images
+    spec = COLPALI["ColPali-v1.3"]
+    sd = random_state_dict(spec, seed=0, device="cuda")
+    model = ColPaliModel.from_spec(spec, device="cuda", state_dict=sd)
+    imgs = synthetic_images(1)
+    caps = [list(range(1000, 1012)), list(range(2000, 2005))]
+    gi = model.encode_images(torch.from_numpy(imgs).cuda()).cpu()[0]
+    Q, ql, qpad = model.encode_queries(caps)
+    sd_cpu = {k: v.float().cpu() for k, v in sd.items()}
+    del sd, model
+    torch.cuda.empty_cache()
+    torch.set_num_threads(16)
+    from oracle import pil_bicubic
+    ip = spec.image_proc
+    pv = torch.from_numpy(pil_bicubic.normalize(pil_bicubic.preprocess_u8(imgs[0], ip.size, ip.mode),
+                                                ip.mean, ip.std))[None]
+    ids = torch.tensor([spec.image_tokens])
+    oi = oc.forward(spec, sd_cpu, ids, None, pv)[0]
+    assert row_cos(gi, oi).min() >= 0.99 and row_cos(gi, oi).mean() >= 0.999
+    rows = [list(spec.query_tokens(c)) for c in caps]
+    L = max(len(r) for r in rows)
+    ids = torch.full((2, L), spec.pad_id, dtype=torch.int64)
+    mask = torch.zeros((2, L), dtype=torch.int64)
+    for i, r in enumerate(rows):
+        ids[i, L - len(r):] = torch.tensor(r)
+        mask[i, L - len(r):] = 1
+    ot = oc.forward(spec, sd_cpu, ids, mask)
+    for i, r in enumerate(rows):
+        n = len(r)
+        assert row_cos(Q[i, :n].cpu(), ot[i, L - n:]).min() >= 0.99
