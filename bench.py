@@ -34,6 +34,7 @@ import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
 A40_PUBLISHED_IMG_S = 47.1  # SigLIP-400M end-to-end img/s, A40 bf16 bs32
+A40_COLPALI_IMG_S = 2.9     # ColPali-v1.3 img/s (encoder + MaxSim), A40 bf16 bs4 (5k job)
 MFMA_BF16_PEAK_TFLOPS = 2500.0  # MI355X_MICROARCH.md: dense bf16 MFMA
 MFMA_FP8_PEAK_TFLOPS = 5000.0  # dense fp8 (block-scaled f8f6f4 MFMA)
 HBM_PEAK_GBS = 8000.0
@@ -106,6 +107,162 @@ def cpu_baseline(spec, seconds: float):
                       f"{nc} captions in {tc:.1f}s ({cap_s:.2f} cap/s), extrapolated to n images + 6n captions"}
 
 
+def colpali_captions(n: int, caps: int, seed: int = 1):
+    """Synthetic caption token lists for the ColPali job: 8..14 ids each, so a query is
+    1 + 3 + len + 10 + 1 = 23..29 tokens (Tq ~ 26)."""
+    import numpy as np
+    rng = np.random.default_rng(seed)
+    lens = rng.integers(8, 15, n * caps)
+    return [rng.integers(3, 250000, int(L)).tolist() for L in lens]
+
+
+def cpu_baseline_colpali(spec, seconds: float):
+    """oracle/colpali_encoder.py (bf16 PyTorch-CPU) on a bounded sample: images and
+    queries timed separately, extrapolated to n images + 6n queries."""
+    import numpy as np
+    from oracle import colpali_encoder as oc
+    from oracle import pil_bicubic
+    from mme.colpali_encoder import random_state_dict
+    from mme.processor import synthetic_images
+    sd = {k: v.cpu() for k, v in random_state_dict(spec, seed=0, device="cuda").items()}
+    threads = torch.get_num_threads()
+    ip = spec.image_proc
+    imgs = synthetic_images(4)
+    caps = colpali_captions(64, 1)
+
+    def enc_img(a):
+        pv = torch.from_numpy(pil_bicubic.normalize(pil_bicubic.preprocess_u8(a, ip.size, ip.mode), ip.mean,
+                                                    ip.std))[None]
+        oc.forward(spec, sd, torch.tensor([spec.image_tokens]), None, pv)
+
+    def enc_q(batch):
+        rows = [list(spec.query_tokens(c)) for c in batch]
+        L = max(len(r) for r in rows)
+        ids = torch.full((len(rows), L), spec.pad_id, dtype=torch.int64)
+        m = torch.zeros_like(ids)
+        for i, r in enumerate(rows):
+            ids[i, L - len(r):] = torch.tensor(r)
+            m[i, L - len(r):] = 1
+        oc.forward(spec, sd, ids, m)
+
+    t0, ni = time.time(), 0
+    while ni < len(imgs) and (ni == 0 or time.time() - t0 < seconds * 0.7):
+        enc_img(imgs[ni])
+        ni += 1
+    ti = time.time() - t0
+    t0, nc = time.time(), 0
+    while nc < len(caps) and (nc == 0 or time.time() - t0 < seconds * 0.3):
+        enc_q(caps[nc:nc + 4])
+        nc += 4
+    tc = time.time() - t0
+    per_img = ti / ni + 6.0 * tc / nc
+    return {"value": round(1.0 / per_img, 5), "unit": "images/sec", "cores": threads, "kind": "port",
+            "sample": f"oracle/colpali_encoder.py bf16 CPU: {ni} images in {ti:.1f}s + {nc} queries (bs 4) in "
+                      f"{tc:.1f}s, extrapolated to n images + 6n queries (MaxSim excluded)"}
+
+
+def main_colpali(args, rank, world, dev):
+    """BASELINE configs[3]: ColPali-v1.3, n images x 5n captions: encode (PaliGemma-3B) + MaxSim
+    T2I / I2T / I2T-Sym + top-10 recall. value = images / job second."""
+    from mme import get_spec, ops
+    from mme.colpali_encoder import ColPaliModel
+    from mme.distributed import shard_range, sharded_colpali_recall
+    spec = get_spec(args.model)
+    model = ColPaliModel.from_spec(spec, seed=0, device=dev)
+    n, caps = args.n_images, args.caps
+    g = torch.Generator(device=dev)
+    g.manual_seed(0)
+    imgs = torch.randint(0, 256, (n, 224, 224, 3), generator=g, device=dev, dtype=torch.uint8)
+    all_caps = colpali_captions(n, caps)
+    width = -(-max(len(spec.query_tokens(c)) for c in all_caps) // 16) * 16
+    lo, hi = shard_range(n, rank, world)
+    my_imgs = imgs[lo:hi].contiguous()
+    my_caps = all_caps[caps * lo:caps * hi]
+    my_t2i = my_caps[::caps]
+    del imgs
+    ev = {}
+
+    def mark(name):
+        e = torch.cuda.Event(enable_timing=True)
+        e.record()
+        ev[name] = e
+
+    def step():
+        mark("t0")
+        D = model.encode_images(my_imgs, batch=args.img_batch)
+        dl = torch.full((D.shape[0],), D.shape[1], dtype=torch.int32, device=dev)
+        Dp = torch.zeros(D.shape[0], -(-D.shape[1] // 16) * 16, D.shape[2], dtype=D.dtype, device=dev)
+        Dp[:, : D.shape[1]] = D
+        mark("img")
+        Qt, qtl, _ = model.encode_queries(my_t2i, exec_batch=args.txt_batch, width=width)
+        Qa, qal, qap = model.encode_queries(my_caps, exec_batch=args.txt_batch, width=width)
+        mark("txt")
+        m = sharded_colpali_recall(Dp, dl, Qt, qtl, Qa, qal, qap, rank, world, n, caps)
+        mark("score")
+        return m
+
+    for _ in range(args.warmup):
+        metrics = step()
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+
+    if not args.no_kernel_timer:
+        ops.KernelTimer.start()
+    barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        metrics = step()
+    barrier()
+    dt = time.perf_counter() - t0
+    ops.KernelTimer.stop()
+    phases = {"encode_images_ms": ev["t0"].elapsed_time(ev["img"]), "encode_queries_ms": ev["img"].elapsed_time(ev["txt"]),
+              "maxsim_recall_ms": ev["txt"].elapsed_time(ev["score"])}
+    if world > 1:
+        t = torch.tensor([dt], device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+    kt = ops.KernelTimer.summary() if not args.no_kernel_timer else {}
+    roofline = None
+    if "gemm" in kt:
+        gk = kt["gemm"]
+        achieved = gk["flops"] / (gk["ms"] / 1e3) / 1e12
+        roofline = {"bound": "mfma", "kernel": "mme_gemm (gemm_pipe6_kernel)", "achieved": round(achieved, 1),
+                    "peak": MFMA_BF16_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": round(achieved / MFMA_BF16_PEAK_TFLOPS, 4),
+                    "traffic": None, "launches": gk["launches"], "avg_launch_ms": round(gk["ms"] / gk["launches"], 4),
+                    "algorithmic_bytes_per_launch": round(gk["bytes"] / gk["launches"]),
+                    "share_of_step_time": round(gk["ms"] / 1e3 / dt, 3)}
+        if "attention" in kt:
+            a = kt["attention"]
+            roofline["attention_tflops"] = round(a["flops"] / (a["ms"] / 1e3) / 1e12, 1)
+            roofline["attention_share"] = round(a["ms"] / 1e3 / dt, 3)
+    value = n * args.steps / dt
+    out = {
+        "metric": "images/sec encode + end-to-end retrieval sec, 5k img x 25k cap; R@1 parity",
+        "value": round(value, 2), "unit": "images/sec", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": round(dt / args.steps * 1e3, 2), "higher_is_better": True, "scaling": "strong",
+        "vs_baseline": round(value / A40_COLPALI_IMG_S, 2) if args.model == "ColPali-v1.3" else None, "dtype": "bf16",
+        "data": "synthetic (u8 224x224x3 images, token-id queries of 23-29 tokens; seeded random weights)",
+        "config": {"workload": f"{args.model}: {n} images x {caps * n} captions (+{n} T2I), PaliGemma-3B encode + "
+                               f"MaxSim T2I/I2T/Sym + top-10 recall", "n_images": n, "n_captions": caps * n,
+                   "image_in": "224x224x3 u8", "image_size": spec.vision.image_size,
+                   "image_tokens": len(spec.image_tokens), "img_batch": args.img_batch, "txt_batch": args.txt_batch,
+                   "global_batch": n, "parallelism": f"image-shard x{world}"},
+        "phases_rank0_last_step": {k: round(v, 1) for k, v in phases.items()},
+        "recall": {k: round(v, 2) for k, v in metrics.items()},
+        "roofline": roofline, "cpu_baseline": None,
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        sys.path.insert(0, ROOT)
+        out["cpu_baseline"] = cpu_baseline_colpali(spec, args.cpu_seconds)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
 def main():
     args = parse()
     rank, world, local = (int(os.environ.get(k, d)) for k, d in (("RANK", 0), ("WORLD_SIZE", 1), ("LOCAL_RANK", 0)))
@@ -113,6 +270,12 @@ def main():
     dev = torch.device("cuda", local)
     if world > 1:
         dist.init_process_group("nccl", device_id=dev)
+    if args.model.startswith("ColPali"):
+        if args.n_images == 5000 and "--n-images" not in sys.argv:
+            args.n_images = 1000  # BASELINE configs[3]: 1 000 images x 5 000 captions
+        if "--img-batch" not in sys.argv:
+            args.img_batch = 32
+        return main_colpali(args, rank, world, dev)
 
     from mme import get_spec, ops
     from mme.distributed import shard_range, sharded_recall

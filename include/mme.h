@@ -153,6 +153,12 @@ int mme_sim_topk(const void* Q, int ldq, const void* Db, int ldd, int nq, int nd
 int mme_topk_merge(const int32_t* in_idx, const float* in_score, int rows, int parts, int k, int32_t* out_idx,
                    float* out_score, void* stream);
 
+/* Row top-k of a materialised fp32 score matrix S [rows, ld] (first `cols` columns):
+ * out [rows, k], order (score desc, column asc), indices + col_offset. k <= 16.
+ * Replaces torch.topk at main.py:335,365,375 on the MaxSim (ColPali) score matrices. */
+int mme_topk_rows(const float* scores, int ld, int rows, int cols, int k, int col_offset, int32_t* out_idx,
+                  float* out_score, void* stream);
+
 /* Recall hit counts. For row r the targets are columns
  *   [tgt_start[r], tgt_start[r] + tgt_count)   (tgt_start nullable -> r*tgt_count)
  * hits[j] += #rows whose first kk[j] indices contain a target, j < nk.

@@ -174,6 +174,53 @@ __global__ void recall_kernel(const int32_t* __restrict__ idx, int rows, int k, 
         if (first < min(kk[j], k)) atomicAdd(&hits[j], 1ull);
 }
 
+// Row top-k of a materialised fp32 score matrix (the MaxSim scores of the ColPali
+// branch; main.py:335,365,375 torch.topk per row). One wave per row: each lane
+// scans columns lane, lane+64, ... into a sorted register list (ties keep the
+// lower column: a lane scans its columns in increasing order), then k rounds of
+// a wave-wide (score desc, column asc) arg-max pop the lanes' list heads.
+__global__ __launch_bounds__(256) void topk_rows_kernel(const float* __restrict__ S, int ld, int rows, int cols,
+                                                        int k, int col_offset, int32_t* __restrict__ oi,
+                                                        float* __restrict__ os) {
+    const int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+    if (row >= rows) return;
+    float ts[KMAX];
+    int ti[KMAX];
+#pragma unroll
+    for (int j = 0; j < KMAX; ++j) {
+        ts[j] = -INFINITY;
+        ti[j] = 0x7fffffff;
+    }
+    const float* sr = S + (long)row * ld;
+    for (int c = lane; c < cols; c += 64) topk_insert(ts, ti, sr[c], c);
+    for (int out = 0; out < k; ++out) {
+        float wv = ts[0];
+        int wi = ti[0];
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) {
+            const float ov = __shfl_xor(wv, o, 64);
+            const int ox = __shfl_xor(wi, o, 64);
+            if (ov > wv || (ov == wv && ox < wi)) {
+                wv = ov;
+                wi = ox;
+            }
+        }
+        if (lane == 0) {
+            oi[(long)row * k + out] = wi == 0x7fffffff ? -1 : wi + col_offset;
+            os[(long)row * k + out] = wv;
+        }
+        if (ti[0] == wi && wi != 0x7fffffff) {  // the owner pops its head (column ids are unique)
+#pragma unroll
+            for (int j = 0; j < KMAX - 1; ++j) {
+                ts[j] = ts[j + 1];
+                ti[j] = ti[j + 1];
+            }
+            ts[KMAX - 1] = -INFINITY;
+            ti[KMAX - 1] = 0x7fffffff;
+        }
+    }
+}
+
 size_t sim_splits(int nq, int nd, int k, int* tiles_per_split) {
     const int nqt = (nq + 127) / 128, ntiles = (nd + 127) / 128;
     // aim for >= 1024 workgroups, >= 4 tiles per split, and a candidate list
@@ -225,6 +272,17 @@ extern "C" int mme_topk_merge(const int32_t* in_idx, const float* in_score, int 
     hipLaunchKernelGGL(topk_merge_kernel, dim3(cdiv(rows, 4)), dim3(256), 0, as_stream(stream), in_score, in_idx,
                        rows, parts * k, k, out_idx, out_score);
     return mme_check_launch("mme_topk_merge");
+}
+
+extern "C" int mme_topk_rows(const float* scores, int ld, int rows, int cols, int k, int col_offset,
+                             int32_t* out_idx, float* out_score, void* stream) {
+    MME_REQUIRE(scores && out_idx && out_score, "mme_topk_rows: null pointer");
+    MME_REQUIRE(rows >= 0 && cols >= 1 && ld >= cols, "mme_topk_rows: bad shape");
+    MME_REQUIRE(k >= 1 && k <= KMAX && k <= cols, "mme_topk_rows: k=%d out of range (<= %d, <= cols)", k, KMAX);
+    if (rows == 0) return MME_OK;
+    hipLaunchKernelGGL(topk_rows_kernel, dim3(cdiv(rows, 4)), dim3(256), 0, as_stream(stream), scores, ld, rows, cols,
+                       k, col_offset, out_idx, out_score);
+    return mme_check_launch("mme_topk_rows");
 }
 
 extern "C" int mme_recall_hits(const int32_t* topk_idx, int rows, int k, const int32_t* tgt_start, int tgt_count,

@@ -53,6 +53,19 @@ def maxsim_scores(Q: torch.Tensor, q_lens: torch.Tensor, D: torch.Tensor, d_lens
     return ops.maxsim(Q, q_lens, D, d_lens, flags)
 
 
+KS = (1, 5, 10)
+
+
+def colpali_recall(img_D: torch.Tensor, img_len: torch.Tensor, t2i_Q: torch.Tensor, t2i_len: torch.Tensor,
+                   all_D: torch.Tensor, all_len: torch.Tensor, all_pad: torch.Tensor,
+                   caps_per_image: int = 5, ks: Sequence[int] = KS, chunk: int = 10):
+    """Single-process Recall@k of the colpali branch (mme.distributed.sharded_colpali_recall
+    at world size 1). Returns (hit counters dict, score matrices dict)."""
+    from .distributed import sharded_colpali_recall
+    return sharded_colpali_recall(img_D, img_len, t2i_Q, t2i_len, all_D, all_len, all_pad, 0, 1, img_D.shape[0],
+                                  caps_per_image, ks, chunk, return_scores=True)
+
+
 class ColPaliScorer:
     """The processor.score surface used at main.py:467 (plus a one-call fast path)."""
 

@@ -280,14 +280,16 @@ class ColPaliModel:
 
     @torch.no_grad()
     def encode_queries(self, captions: Sequence[Sequence[int]], ref_batch: Optional[int] = None,
-                       exec_batch: int = 256) -> Tuple[torch.Tensor, torch.Tensor, torch.Tensor]:
+                       exec_batch: int = 256, width: Optional[int] = None
+                       ) -> Tuple[torch.Tensor, torch.Tensor, torch.Tensor]:
         """Caption token lists -> (Q bf16 [n, Lmax, 128] valid rows first then zeros,
         lens int32 [n] (valid rows), padded int32 [n] (the caption's padded length L_b)).
 
         Reproduces processor.process_queries(batch) per reference batch of `ref_batch`
         (main.py:420-424): left padding to the batch-longest, positions 1..L_b over the
         padded row; captions with equal L_b run in one execution batch (their
-        embeddings depend only on L_b)."""
+        embeddings depend only on L_b). width: fixed row count of Q (a multiple of 16 >= the
+        longest query; equal widths let ranks all-gather their tables)."""
         spec = self.spec
         ref_batch = ref_batch or spec.batch_size
         rows = [spec.query_tokens(c) for c in captions]
@@ -297,6 +299,10 @@ class ColPaliModel:
         for s in range(0, n, ref_batch):
             padded[s:s + ref_batch] = lens[s:s + ref_batch].max()
         Lmax = -(-int(lens.max()) // 16) * 16 if n else 16  # zero rows up to a multiple of 16 (mme_maxsim)
+        if width is not None:
+            if width % 16 or width < Lmax:
+                raise ValueError(f"width {width} must be a multiple of 16 >= {Lmax}")
+            Lmax = width
         Q = torch.zeros(n, Lmax, spec.dim, dtype=BF16, device=self.device)
         for Lb in sorted(set(padded.tolist())):
             idx = np.nonzero(padded == Lb)[0]

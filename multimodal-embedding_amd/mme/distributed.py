@@ -100,3 +100,71 @@ def env_rank_world() -> Tuple[int, int, int]:
     """(rank, world_size, local_rank) from torchrun's environment (defaults 0/1/0)."""
     import os
     return int(os.environ.get("RANK", 0)), int(os.environ.get("WORLD_SIZE", 1)), int(os.environ.get("LOCAL_RANK", 0))
+
+
+class MaxSimOps:
+    """Default compute of the ColPali recall: libmme MaxSim, row top-k and recall counters."""
+
+    def maxsim(self, Q, ql, D, dl, flags):
+        from . import ops
+        return ops.maxsim(Q, ql, D, dl, flags)
+
+    def topk(self, s: torch.Tensor, k: int) -> torch.Tensor:
+        from . import ops
+        return ops.topk_rows(s, k)[0]
+
+    def hits(self, idx: torch.Tensor, tgt_count: int, ks: Sequence[int], row_offset: int) -> torch.Tensor:
+        from . import ops
+        return ops.recall_hits(idx, tgt_count, ks, row_offset=row_offset)
+
+
+def sharded_colpali_recall(img_D: torch.Tensor, img_len: torch.Tensor, t2i_Q: torch.Tensor, t2i_len: torch.Tensor,
+                           all_D: torch.Tensor, all_len: torch.Tensor, all_pad: torch.Tensor, rank: int, world: int,
+                           n_img: int, caps_per_image: int = 5, ks: Sequence[int] = KS, chunk: int = 10, group=None,
+                           compute: Optional[object] = None, return_scores: bool = False):
+    """Recall@k of the colpali branch of run_bootstrap_benchmark (main.py:618-624 with the
+    v28 I2T orientation) from per-rank shards of per-item multi-vector tables.
+
+    Rank r holds images [lo, hi) (img_D [n_r, Ld, 128], valid rows img_len), their T2I
+    caption queries (t2i_Q / t2i_len, valid rows first) and their captions (all_D / all_len,
+    all_pad = each caption's padded length L_b in the reference's left-padded batch).
+    Exchange: one all-gather of each table (bf16; 266 MB of image vectors at n = 1000),
+    then every rank scores ITS rows (MaxSim is asymmetric, so I2T-Sym = columns of T2I:
+    all T2I queries against the rank's images, transposed) and one all-reduce of the
+    9 hit counters. Zero-padding semantics of processor.score's pad_sequence are global:
+    doc chunks of `chunk` run over the full, rank-ordered doc lists."""
+    from .colpali import chunk_zero_flags
+    compute = compute or MaxSimOps()
+    lo, hi = shard_range(n_img, rank, world)
+    D_all, dl_all = all_gather_rows(img_D, world, group), all_gather_rows(img_len, world, group)
+    Qt_all, qtl_all = all_gather_rows(t2i_Q, world, group), all_gather_rows(t2i_len, world, group)
+    Qa_all, qal_all = all_gather_rows(all_D, world, group), all_gather_rows(all_len, world, group)
+    qap_all = all_gather_rows(all_pad, world, group)
+    img_flags = chunk_zero_flags(dl_all, chunk)
+    cap_flags = chunk_zero_flags(qap_all, chunk) | (qap_all > qal_all).to(torch.uint8)
+    kmax = max(ks)
+    s_t2i = compute.maxsim(t2i_Q, t2i_len, D_all, dl_all, img_flags)        # [n_r, n]
+    s_i2t = compute.maxsim(img_D, img_len, Qa_all, qal_all, cap_flags)     # [n_r, 5n]
+    if world == 1:
+        s_sym = s_t2i.t().contiguous()
+    else:  # column block [lo, hi) of the global T2I matrix
+        s_sym = compute.maxsim(Qt_all, qtl_all, img_D, img_len, img_flags[lo:hi].contiguous()).t().contiguous()
+    res = []
+    for s, tc in ((s_t2i, 1), (s_i2t, caps_per_image), (s_sym, 1)):
+        k = min(kmax, s.shape[1])
+        kk = [min(x, k) for x in ks]
+        if s.shape[0]:
+            res.append(compute.hits(compute.topk(s, k), tc, kk, lo).to(torch.int64))
+        else:
+            res.append(torch.zeros(len(ks), dtype=torch.int64, device=s.device))
+    counts = torch.cat(res)
+    if world > 1:
+        dist.all_reduce(counts, op=dist.ReduceOp.SUM, group=group)
+    c = counts.tolist()
+    out = {}
+    for j, name in enumerate(("T2I", "I2T", "I2T_Sym")):
+        for i, k in enumerate(ks):
+            out[f"{name}_R@{k}"] = 100.0 * c[j * len(ks) + i] / n_img
+    if return_scores:
+        return out, {"t2i": s_t2i, "i2t": s_i2t}
+    return out

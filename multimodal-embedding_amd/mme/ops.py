@@ -379,6 +379,19 @@ def topk_merge(idx: torch.Tensor, score: torch.Tensor, parts: int, k: int):
     return oi, os_
 
 
+def topk_rows(scores: torch.Tensor, k: int, col_offset: int = 0):
+    """Row top-k of an fp32 score matrix: (idx int32 [rows,k], score fp32 [rows,k]), order (score desc, idx asc)."""
+    _dev(scores)
+    if scores.dtype != torch.float32:
+        raise ValueError("topk_rows: scores must be fp32")
+    rows, cols = scores.shape
+    idx = torch.empty(rows, k, dtype=torch.int32, device=scores.device)
+    sc = torch.empty(rows, k, dtype=torch.float32, device=scores.device)
+    call("mme_topk_rows", scores.data_ptr(), _rowmajor(scores, "scores"), rows, cols, k, col_offset, idx.data_ptr(),
+         sc.data_ptr(), _stream())
+    return idx, sc
+
+
 def recall_hits(topk_idx: torch.Tensor, tgt_count: int, ks: Sequence[int], *, tgt_start: Optional[torch.Tensor] = None,
                 row_offset: int = 0, hits: Optional[torch.Tensor] = None) -> torch.Tensor:
     """int64 [len(ks)] counts of rows whose first ks[j] indices contain a target column."""

@@ -197,3 +197,45 @@ def test_full_size_colpali_vs_oracle(cuda):
     for i, r in enumerate(rows):
         n = len(r)
         assert row_cos(Q[i, :n].cpu(), ot[i, L - n:]).min() >= 0.99
+
+
+def test_colpali_recall_vs_oracle(cuda):
+    """Fast-path encode -> MaxSim (T2I, I2T incl. each caption doc's own left padding) ->
+    device top-k -> hit counters, vs the reference chunk loop (oracle/maxsim.py) over the
+    same per-item embedding lists (left-padded [L_b, 128] caption tensors, as encode_data
+    returns them) and the oracle's top-k / recall."""
+    from mme.colpali import colpali_recall, pack_multivectors
+    from oracle import maxsim as om
+    from oracle import retrieval as orr
+    rng = np.random.default_rng(5)
+    n, caps = 6, 5
+    model = _tiny_model()
+    imgs = rng.integers(0, 256, (n, 64, 64, 3), dtype=np.uint8)
+    all_caps = [rng.integers(3, 990, int(rng.integers(2, 12))).tolist() for _ in range(n * caps)]
+    t2i_caps = all_caps[::caps]
+    fi = model.encode_images(torch.from_numpy(imgs).cuda())
+    D, dl = pack_multivectors(list(fi), device="cuda")
+    Qt, qtl, _ = model.encode_queries(t2i_caps)
+    Qa, qal, qap = model.encode_queries(all_caps)
+    counts, sc = colpali_recall(D, dl, Qt, qtl, Qa, qal, qap, caps_per_image=caps)
+
+    def items(Q, ql, qp):  # per-caption [L_b, 128] with its zero (left) padding rows, as the reference holds it
+        out = []
+        for i in range(Q.shape[0]):
+            e = torch.zeros(int(qp[i]), 128, dtype=BF)
+            e[int(qp[i]) - int(ql[i]):] = Q[i, : int(ql[i])].cpu()
+            out.append(e)
+        return out
+    imgs_l = [e.cpu() for e in fi]
+    t2i_l, all_l = items(Qt, qtl, model.encode_queries(t2i_caps)[2]), items(Qa, qal, qap)
+    ref_t2i = om.score_reference_chunks(t2i_l, imgs_l).numpy()
+    ref_i2t = om.score_reference_chunks(imgs_l, all_l).numpy()
+    for got, ref in ((sc["t2i"].cpu().numpy(), ref_t2i), (sc["i2t"].cpu().numpy(), ref_i2t)):
+        assert np.abs(got - ref).max() <= 2.0 ** -7 * np.abs(ref).max() + 1e-3
+    ks = (1, 5, 10)
+    for name, s, tc in (("T2I", sc["t2i"], 1), ("I2T", sc["i2t"], caps), ("I2T_Sym", sc["t2i"].t(), 1)):
+        s = s.cpu().numpy()
+        k = min(10, s.shape[1])
+        idx, _ = orr.topk(s, k)
+        ref = orr.recall(idx, tc, [min(x, k) for x in ks])
+        assert [counts[f"{name}_R@{x}"] for x in ks] == [100.0 * r / n for r in ref], name
