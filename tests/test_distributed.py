@@ -82,3 +82,106 @@ def test_shard_range_covers():
             assert spans[0][0] == 0 and spans[-1][1] == n
             assert all(a[1] == b[0] for a, b in zip(spans, spans[1:]))
             assert max(h - l for l, h in spans) - min(h - l for l, h in spans) <= 1
+
+
+# ------------------------------------------------------------------ ColPali (MaxSim) sharding
+class MaxSimCPU:
+    """CPU stand-in of the device MaxSim / top-k / hits with processor.score's bf16 semantics."""
+
+    def maxsim(self, Q, ql, D, dl, flags):
+        dots = torch.einsum("qid,njd->qnij", Q.float(), D.float()).to(torch.bfloat16).float()
+        jmask = torch.arange(D.shape[1])[None, :] < dl[:, None].long()          # [n, Ld]
+        dots = dots.masked_fill(~jmask[None, :, None, :], float("-inf"))
+        m = dots.amax(-1)
+        m = torch.where(flags.bool()[None, :, None], m.clamp_min(0.0), m)
+        imask = torch.arange(Q.shape[1])[None, :] < ql[:, None].long()          # [q, Lq]
+        m = m.masked_fill(~imask[:, None, :], 0.0)
+        return m.sum(-1).to(torch.bfloat16).float()
+
+    def topk(self, s, k):
+        from oracle import retrieval as R
+        return torch.from_numpy(R.topk(s.numpy(), k)[0])
+
+    def hits(self, idx, tgt_count, ks, row_offset):
+        from oracle import retrieval as R
+        return torch.from_numpy(R.recall(idx.numpy(), tgt_count, ks, row_offset))
+
+
+def _colpali_tables(n=13, caps=5, Ld=20, seed=0):
+    """Planted per-item multi-vectors: image i tokens ~ base_i, its captions' tokens ~ base_i;
+    captions left-padded per reference batch of 4 (pad = the batch-longest length)."""
+    g = torch.Generator().manual_seed(seed)
+    base = torch.randn(n, 128, generator=g)
+    nrm = lambda x: (x / x.norm(dim=-1, keepdim=True)).to(torch.bfloat16)
+    D = nrm(base[:, None] + 6.0 * torch.randn(n, Ld, 128, generator=g))
+    lens = torch.randint(3, 10, (n * caps,), generator=g)
+    Qa = torch.zeros(n * caps, 16, 128, dtype=torch.bfloat16)
+    for c in range(n * caps):
+        Qa[c, : lens[c]] = nrm(base[c // caps] + 6.0 * torch.randn(int(lens[c]), 128, generator=g))
+    pad = torch.tensor([int(lens[s:s + 4].max()) for s in range(0, n * caps, 4) for _ in range(min(4, n * caps - s))])
+    t2i = Qa[::caps].clone()
+    t2i_len = lens[::caps].clone()
+    return D, torch.full((n,), Ld, dtype=torch.int32), t2i, t2i_len.int(), Qa, lens.int(), pad.int()
+
+
+def _colpali_worker(rank, world, port, q):
+    import sys
+    for p in (ROOT, os.path.join(ROOT, "multimodal-embedding_amd")):
+        sys.path.insert(0, p)
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from mme.distributed import shard_range, sharded_colpali_recall
+    D, dl, Qt, qtl, Qa, qal, qap = _colpali_tables()
+    n, caps = D.shape[0], 5
+    lo, hi = shard_range(n, rank, world)
+    res = sharded_colpali_recall(D[lo:hi], dl[lo:hi], Qt[lo:hi], qtl[lo:hi], Qa[caps * lo:caps * hi],
+                                 qal[caps * lo:caps * hi], qap[caps * lo:caps * hi], rank, world, n, caps,
+                                 compute=MaxSimCPU())
+    if rank == 0:
+        q.put(res)
+    dist.destroy_process_group()
+
+
+def _reference_colpali_metrics():
+    """The reference's colpali scoring (oracle/maxsim.py chunk loop over per-item lists whose
+    caption tensors carry their left zero padding) + compute_metrics_detailed's recall."""
+    from oracle import maxsim as om
+    from oracle import retrieval as R
+    D, dl, Qt, qtl, Qa, qal, qap = _colpali_tables()
+    n, caps = D.shape[0], 5
+
+    def cap_items(Q, ql, qp):
+        out = []
+        for i in range(Q.shape[0]):
+            e = torch.zeros(int(qp[i]), 128, dtype=torch.bfloat16)
+            e[int(qp[i]) - int(ql[i]):] = Q[i, : int(ql[i])]
+            out.append(e)
+        return out
+    t2i_pad = torch.tensor([int(qtl[s:s + 4].max()) for s in range(0, n, 4) for _ in range(min(4, n - s))])
+    imgs = [D[i, : int(dl[i])] for i in range(n)]
+    s_t2i = om.score_reference_chunks(cap_items(Qt, qtl, t2i_pad), imgs).numpy()
+    s_i2t = om.score_reference_chunks(imgs, cap_items(Qa, qal, qap)).numpy()
+    out = {}
+    for name, s, tc in (("T2I", s_t2i, 1), ("I2T", s_i2t, caps), ("I2T_Sym", s_t2i.T.copy(), 1)):
+        idx, _ = R.topk(s, 10)
+        for k, c in zip((1, 5, 10), R.recall(idx, tc, (1, 5, 10))):
+            out[f"{name}_R@{k}"] = 100.0 * c / n
+    return out
+
+
+@pytest.mark.parametrize("world", [1, 2, 3])
+def test_sharded_colpali_recall_equals_reference(world):
+    ref = _reference_colpali_metrics()
+    assert 0 < ref["T2I_R@1"] < 100  # planted data: recall neither trivial nor saturated
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_colpali_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = q.get(timeout=180)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert res == pytest.approx(ref)
