@@ -32,6 +32,7 @@ import torch
 from . import ops
 from ._lib import ACT_GEGLU_TANH
 from .config import ColPaliSpec, get_spec
+from .models import VisionTower, balanced
 from .weights import VisionW, _pad_cols, _sub, pack_layer
 
 BF16 = torch.bfloat16
@@ -183,7 +184,6 @@ class ColPaliModel:
     family = "colpali"
 
     def __init__(self, spec: ColPaliSpec, weights: ColPaliW, device="cuda"):
-        from .models import VisionTower
         self.spec = self.config = spec
         self.device = torch.device(device)
         self.w = weights
@@ -268,6 +268,7 @@ class ColPaliModel:
         toks = torch.tensor(spec.image_tokens, dtype=torch.int64, device=self.device)
         L = toks.numel()
         out = torch.empty(n, L, spec.dim, dtype=BF16, device=self.device)
+        batch = balanced(n, batch)
         for i in range(0, n, batch):
             chunk = images_u8[i:i + batch]
             b = chunk.shape[0]
@@ -306,8 +307,9 @@ class ColPaliModel:
         Q = torch.zeros(n, Lmax, spec.dim, dtype=BF16, device=self.device)
         for Lb in sorted(set(padded.tolist())):
             idx = np.nonzero(padded == Lb)[0]
-            for j in range(0, len(idx), exec_batch):
-                part = idx[j:j + exec_batch]
+            eb = balanced(len(idx), exec_batch)
+            for j in range(0, len(idx), eb):
+                part = idx[j:j + eb]
                 b = len(part)
                 ids = np.full((b, Lb), spec.pad_id, np.int64)
                 for r, i in enumerate(part):
