@@ -159,6 +159,13 @@ int mme_topk_merge(const int32_t* in_idx, const float* in_score, int rows, int p
 int mme_topk_rows(const float* scores, int ld, int rows, int cols, int k, int col_offset, int32_t* out_idx,
                   float* out_score, void* stream);
 
+/* Winoground 2x2 scores (§8f-4; run_winoground, run_benchmark_grand_slam_v28_publication_ready.py:413-461):
+ * text, image: bf16 [n, 2, D] L2-normalised embeddings of (caption_0, caption_1) and (image_0, image_1).
+ * scores: fp32 [n, 4] = bf16(<t_a, i_b>) for (a,b) = 00, 01, 10, 11 (the bf16 torch.matmul);
+ * counts[0..2] += text / image / group successes (strict comparisons of the reference).
+ * counts must be zeroed by the caller. */
+int mme_winoground(const void* text, const void* image, int n, int D, float* scores, int64_t* counts, void* stream);
+
 /* Recall hit counts. For row r the targets are columns
  *   [tgt_start[r], tgt_start[r] + tgt_count)   (tgt_start nullable -> r*tgt_count)
  * hits[j] += #rows whose first kk[j] indices contain a target, j < nk.

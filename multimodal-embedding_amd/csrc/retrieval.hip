@@ -221,6 +221,44 @@ __global__ __launch_bounds__(256) void topk_rows_kernel(const float* __restrict_
     }
 }
 
+// Winoground 2x2 scoring (run_winoground, run_benchmark_grand_slam_v28_publication_ready.py:
+// 413-461): per example s[t][i] = bf16( <text_t, image_i> ) — torch.matmul on the bf16
+// (normalised) embeddings, fp32 accumulation, one rounding — then the strict comparisons
+// text: s00>s01 && s11>s10, image: s00>s10 && s11>s01, group: both. One wave per example.
+__global__ __launch_bounds__(256) void winoground_kernel(const bf16* __restrict__ T, const bf16* __restrict__ I,
+                                                         int n, int D, float* __restrict__ scores,
+                                                         unsigned long long* __restrict__ counts) {
+    const int e = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+    if (e >= n) return;
+    const bf16* t0 = T + (long)e * 2 * D;
+    const bf16* i0 = I + (long)e * 2 * D;
+    float acc[4] = {0.f, 0.f, 0.f, 0.f};
+    for (int c = lane; c < D / 8; c += 64) {
+        const u16x8 a0 = *reinterpret_cast<const u16x8*>(t0 + c * 8);
+        const u16x8 a1 = *reinterpret_cast<const u16x8*>(t0 + D + c * 8);
+        const u16x8 b0 = *reinterpret_cast<const u16x8*>(i0 + c * 8);
+        const u16x8 b1 = *reinterpret_cast<const u16x8*>(i0 + D + c * 8);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            acc[0] += bits2f(a0[j]) * bits2f(b0[j]);
+            acc[1] += bits2f(a0[j]) * bits2f(b1[j]);
+            acc[2] += bits2f(a1[j]) * bits2f(b0[j]);
+            acc[3] += bits2f(a1[j]) * bits2f(b1[j]);
+        }
+    }
+    float s[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) s[j] = bf2f(f2bf(wave_sum(acc[j])));
+    if (lane == 0) {
+        for (int j = 0; j < 4; ++j) scores[(long)e * 4 + j] = s[j];
+        const bool txt = s[0] > s[1] && s[3] > s[2];
+        const bool img = s[0] > s[2] && s[3] > s[1];
+        if (txt) atomicAdd(&counts[0], 1ull);
+        if (img) atomicAdd(&counts[1], 1ull);
+        if (txt && img) atomicAdd(&counts[2], 1ull);
+    }
+}
+
 size_t sim_splits(int nq, int nd, int k, int* tiles_per_split) {
     const int nqt = (nq + 127) / 128, ntiles = (nd + 127) / 128;
     // aim for >= 1024 workgroups, >= 4 tiles per split, and a candidate list
@@ -283,6 +321,16 @@ extern "C" int mme_topk_rows(const float* scores, int ld, int rows, int cols, in
     hipLaunchKernelGGL(topk_rows_kernel, dim3(cdiv(rows, 4)), dim3(256), 0, as_stream(stream), scores, ld, rows, cols,
                        k, col_offset, out_idx, out_score);
     return mme_check_launch("mme_topk_rows");
+}
+
+extern "C" int mme_winoground(const void* text, const void* image, int n, int D, float* scores, int64_t* counts,
+                              void* stream) {
+    MME_REQUIRE(text && image && scores && counts, "mme_winoground: null pointer");
+    MME_REQUIRE(n >= 0 && D > 0 && D % 8 == 0, "mme_winoground: D=%d must be a multiple of 8", D);
+    if (n == 0) return MME_OK;
+    hipLaunchKernelGGL(winoground_kernel, dim3(cdiv(n, 4)), dim3(256), 0, as_stream(stream), (const bf16*)text,
+                       (const bf16*)image, n, D, scores, (unsigned long long*)counts);
+    return mme_check_launch("mme_winoground");
 }
 
 extern "C" int mme_recall_hits(const int32_t* topk_idx, int rows, int k, const int32_t* tgt_start, int tgt_count,

@@ -392,6 +392,19 @@ def topk_rows(scores: torch.Tensor, k: int, col_offset: int = 0):
     return idx, sc
 
 
+def winoground(text: torch.Tensor, image: torch.Tensor):
+    """(scores fp32 [n, 4] = bf16 <t_a, i_b> for ab = 00,01,10,11, counts int64 [3] text/image/group)."""
+    _dev(text, image)
+    if text.shape != image.shape or text.dim() != 3 or text.shape[1] != 2:
+        raise ValueError("winoground: text / image must both be [n, 2, D]")
+    n, _, D = text.shape
+    text, image = text.to(BF16).contiguous(), image.to(BF16).contiguous()
+    scores = torch.empty(n, 4, dtype=torch.float32, device=text.device)
+    counts = torch.zeros(3, dtype=torch.int64, device=text.device)
+    call("mme_winoground", text.data_ptr(), image.data_ptr(), n, D, scores.data_ptr(), counts.data_ptr(), _stream())
+    return scores, counts
+
+
 def recall_hits(topk_idx: torch.Tensor, tgt_count: int, ks: Sequence[int], *, tgt_start: Optional[torch.Tensor] = None,
                 row_offset: int = 0, hits: Optional[torch.Tensor] = None) -> torch.Tensor:
     """int64 [len(ks)] counts of rows whose first ks[j] indices contain a target column."""

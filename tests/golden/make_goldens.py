@@ -393,13 +393,75 @@ def make_colpali(main):
     print("tiny-colpali.npz:", {k: v.shape for k, v in out.items()})
 
 
+# ------------------------------------------------------------------ Winoground
+def make_winoground():
+    """The reference's own run_winoground (run_benchmark_grand_slam_v28_publication_ready.py:413-461)
+    over the tiny models, with its load_dataset patched to return synthetic examples."""
+    from PIL import Image
+    from transformers.models.siglip.image_processing_pil_siglip import SiglipImageProcessorPil
+    from transformers.models.clip.image_processing_pil_clip import CLIPImageProcessorPil
+    cwd = os.getcwd()
+    os.chdir(tempfile.mkdtemp(prefix="mme_ref_"))
+    sys.path.insert(0, REF)
+    import run_benchmark_grand_slam_v28_publication_ready as v28  # noqa: E402
+    os.chdir(cwd)
+    sys.path.insert(0, os.path.join(REPO, "multimodal-embedding_amd"))
+    from mme.winoground import synthetic_examples
+    out = {}
+    for name in ("tiny-siglip", "tiny-clip"):
+        spec = TINY[name]
+        t = spec.text
+        lo, hi = (1, min(t.bos_id, t.eos_id)) if t.bos_id is not None else (2, t.vocab)
+        exs = synthetic_examples(40, seed=3, size=72, vocab=(lo, hi), lens=(3, t.max_pos - 2))
+        for ex in exs:  # the tokenizer's special tokens, as the reference's processor would add them
+            for j in (0, 1):
+                c = ex[f"caption_{j}"]
+                ex[f"caption_{j}"] = ([t.bos_id] + c + [t.eos_id]) if t.bos_id is not None else (c + [t.eos_id])
+        S = spec.vision.image_size
+        ip = (SiglipImageProcessorPil(size={"height": S, "width": S}) if spec.family == "siglip" else
+              CLIPImageProcessorPil(size={"shortest_edge": S}, crop_size={"height": S, "width": S}))
+        proc = RefProcessor(ip, t.pad_id)
+        hf = RefAdapter(hf_model(spec, torch.bfloat16))
+        ds = [{"image_0": Image.fromarray(e["image_0"]), "image_1": Image.fromarray(e["image_1"]),
+               "caption_0": e["caption_0"], "caption_1": e["caption_1"]} for e in exs]
+        v28.DEVICE, v28.DTYPE = "cpu", torch.bfloat16
+        v28.load_dataset = lambda *a, **k: ds
+        m = v28.run_winoground(hf, proc, {"type": spec.m_info["type"]})
+        assert m, "run_winoground returned no metrics"
+        key = name.replace("-", "_")
+        # per-example 2x2 scores through the same modules (run_winoground's dense steps,
+        # restated) so tests can tell decisive decisions from bf16 near-ties
+        sc = []
+        with torch.no_grad():
+            for e in ds:
+                ie = hf.get_image_features(**proc(images=[e["image_0"], e["image_1"]]))
+                te = hf.get_text_features(**proc(text=[e["caption_0"], e["caption_1"]]))
+                ie, te = ie / ie.norm(dim=-1, keepdim=True), te / te.norm(dim=-1, keepdim=True)
+                sc.append(torch.matmul(te.to(torch.bfloat16), ie.to(torch.bfloat16).t()).float().reshape(4).numpy())
+        sc = np.stack(sc)
+        tx = (sc[:, 0] > sc[:, 1]) & (sc[:, 3] > sc[:, 2])
+        im = (sc[:, 0] > sc[:, 2]) & (sc[:, 3] > sc[:, 1])
+        n = len(ds)
+        assert [100.0 * tx.sum() / n, 100.0 * im.sum() / n, 100.0 * (tx & im).sum() / n] == \
+            [m["Wino Text"], m["Wino Image"], m["Wino Group"]], "restated scores disagree with run_winoground"
+        out[f"{key}_scores"] = sc.astype(np.float32)
+        out[f"{key}_metrics"] = np.array([m["Wino Text"], m["Wino Image"], m["Wino Group"]], np.float64)
+        out[f"{key}_images"] = np.stack([np.stack([e["image_0"], e["image_1"]]) for e in exs])
+        caps = [e[f"caption_{j}"] for e in exs for j in (0, 1)]
+        out[f"{key}_cap_lens"] = np.array([len(c) for c in caps], np.int64)
+        out[f"{key}_cap_ids"] = np.concatenate(caps).astype(np.int64)
+    np.savez_compressed(os.path.join(HERE, "winoground.npz"), **out)
+    print("winoground.npz:", {k: v.tolist() for k, v in out.items() if k.endswith("metrics")})
+
+
 if __name__ == "__main__":
     torch.manual_seed(0)
     main = import_reference()
     only = sys.argv[1:]
     steps = {"preprocess": make_preprocess, "l2norm": lambda: make_l2norm(main),
              "retrieval": lambda: make_retrieval(main), "maxsim": lambda: make_maxsim(main),
-             "encoders": lambda: make_encoders(main), "colpali": lambda: make_colpali(main)}
+             "encoders": lambda: make_encoders(main), "colpali": lambda: make_colpali(main),
+             "winoground": make_winoground}
     for name, fn in steps.items():
         if not only or name in only:
             fn()
