@@ -65,15 +65,23 @@ __device__ __forceinline__ void glds16(const void* gsrc, void* lds_base) {
 __device__ __forceinline__ void wait_vmcnt0() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 
 // Activation codes shared by the GEMM epilogue and the host (mme.h MME_ACT_*).
+// The sigmoid forms run on the transcendental unit (v_exp_f32 + v_rcp_f32, ~1 ulp
+// each) instead of the libm tanhf / IEEE division sequences: in a GEMM epilogue the
+// MFMA pipes idle while these run (fc1 with tanhf: ~780 TF/s vs ~1070 for the same
+// shape without an activation). Results round to bf16, so the few-ulp fp32
+// difference is below the output precision.
 __device__ __forceinline__ float apply_act(float x, int act) {
     switch (act) {
-        case MME_ACT_GELU_TANH: {  // gelu_pytorch_tanh
-            const float k0 = 0.7978845608028654f, k1 = 0.044715f;
-            float u = k0 * (x + k1 * x * x * x);
-            return 0.5f * x * (1.0f + tanhf(u));
+        case MME_ACT_GELU_TANH: {  // gelu_pytorch_tanh: 0.5x(1 + tanh(u)) = x * sigmoid(2u)
+            const float k1 = 0.044715f;
+            const float c2 = -2.0f * 0.7978845608028654f * 1.4426950408889634f;  // -2 * sqrt(2/pi) * log2(e)
+            const float e = __builtin_amdgcn_exp2f(c2 * x * (1.0f + k1 * x * x));
+            return x * __builtin_amdgcn_rcpf(1.0f + e);
         }
-        case MME_ACT_QUICK_GELU:  // x * sigmoid(1.702 x)
-            return x / (1.0f + __expf(-1.702f * x));
+        case MME_ACT_QUICK_GELU: {  // x * sigmoid(1.702 x)
+            const float e = __builtin_amdgcn_exp2f(-1.702f * 1.4426950408889634f * x);
+            return x * __builtin_amdgcn_rcpf(1.0f + e);
+        }
         case MME_ACT_GELU_ERF:
             return 0.5f * x * (1.0f + erff(x * 0.7071067811865476f));
         default:
