@@ -140,6 +140,22 @@ __device__ __forceinline__ void gemm_epilogue_lds(const GemmArgs& p, char* lds, 
     // (GemmaMLP.forward act_fn(gate_proj(x)) * up_proj(x), TF:models/gemma/modeling_gemma.py:95-96).
     constexpr bool GLU = ACT == MME_ACT_GEGLU_TANH;
     constexpr int RACT = GLU ? MME_ACT_NONE : ACT;
+    constexpr int CPR = C::BN / 8;                // 16-B chunks per tile row
+    constexpr int NCH = C::BM * CPR / C::NT;      // chunks per thread
+    static_assert(NCH * C::NT == C::BM * CPR, "epilogue chunks must split evenly");
+    // residual / position-table rows: issue this thread's loads first so their latency
+    // overlaps the accumulator staging below (the main loop's counted vmcnt is done;
+    // these are the only loads in flight). o_proj 186624 x 1152 x 1152 + residual: 0.630 -> 0.589 ms.
+    u16x8 rv[NCH];
+    if (!GLU && p.res) {
+#pragma unroll
+        for (int q = 0; q < NCH; ++q) {
+            const int c = tid + q * C::NT;
+            const int gr = min(m0 + c / CPR, p.M - 1), gc = min(n0 + (c % CPR) * 8, p.N - 8);
+            const int rr = p.res_period ? gr % p.res_period : gr;
+            rv[q] = *reinterpret_cast<const u16x8*>(p.res + (size_t)rr * p.ldr + gc);
+        }
+    }
     __syncthreads();
 #pragma unroll
     for (int j = 0; j < C::FN; ++j) {
@@ -159,9 +175,10 @@ __device__ __forceinline__ void gemm_epilogue_lds(const GemmArgs& p, char* lds, 
         }
     }
     __syncthreads();
-    constexpr int CPR = C::BN / 8;
     bf16* Cout = reinterpret_cast<bf16*>(p.C);
-    for (int c = tid; c < C::BM * CPR; c += C::NT) {
+#pragma unroll
+    for (int q = 0; q < NCH; ++q) {
+        const int c = tid + q * C::NT;
         const int row = c / CPR, cc = c % CPR;
         const int gr = m0 + row, gc = n0 + cc * 8;
         if (gr >= p.M || gc >= p.N) continue;
@@ -173,11 +190,9 @@ __device__ __forceinline__ void gemm_epilogue_lds(const GemmArgs& p, char* lds, 
                 o[e] = f2bf(bf2f(f2bf(apply_act(bits2f(v[e]), MME_ACT_GELU_TANH))) * bits2f(v[4 + e]));
             *reinterpret_cast<bf16x4*>(Cout + (size_t)gr * p.ldc + gc / 2) = o;
         } else if (p.res) {
-            const int rr = p.res_period ? gr % p.res_period : gr;
-            const u16x8 rv = *reinterpret_cast<const u16x8*>(p.res + (size_t)rr * p.ldr + gc);
             bf16x8 o;
 #pragma unroll
-            for (int e = 0; e < 8; ++e) o[e] = f2bf(bits2f(v[e]) + bits2f(rv[e]));
+            for (int e = 0; e < 8; ++e) o[e] = f2bf(bits2f(v[e]) + bits2f(rv[q][e]));
             *reinterpret_cast<bf16x8*>(Cout + (size_t)gr * p.ldc + gc) = o;
         } else {
             *reinterpret_cast<u16x8*>(Cout + (size_t)gr * p.ldc + gc) = v;

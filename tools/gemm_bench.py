@@ -31,6 +31,7 @@ def main():
     p.add_argument("--variants", default="")
     p.add_argument("--shapes", default="qkv,o_proj,fc1,fc2")
     p.add_argument("--mx", action="store_true", help="also time the mx8 (block-scaled fp8) GEMM")
+    p.add_argument("--epi", default="none", help="epilogue: none | bias | res (residual in place) | gelu (bias+gelu_tanh)")
     a = p.parse_args()
     lib = _lib.load()
     has_var = hasattr(lib, "mme_gemm_variant")
@@ -45,13 +46,16 @@ def main():
         N, K = SHAPES[name]
         A = (torch.randn(M, K, device="cuda", generator=g)).to(torch.bfloat16)
         W = (torch.randn(N, K, device="cuda", generator=g) / K ** 0.5).to(torch.bfloat16)
-        C = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
+        C = torch.randn(M, N, device="cuda", generator=g).to(torch.bfloat16)
+        bias = (torch.randn(N, device="cuda", generator=g) * 0.1).to(torch.bfloat16)
+        kw = {"none": {}, "bias": {"bias": bias}, "res": {"bias": bias, "residual": C},
+              "gelu": {"bias": bias, "act": _lib.ACT_GELU_TANH}}[a.epi]
         ref = None
         for v in variants:
             if v >= 0:
                 lib.mme_gemm_variant(v)
-            ops.gemm(A, W, out=C)
-            if ref is None:
+            ops.gemm(A, W, out=C, **kw)
+            if ref is None or a.epi == "res":
                 ref = C.clone()
             else:
                 err = (C.float() - ref.float()).abs().max().item()
@@ -61,13 +65,13 @@ def main():
             s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             s.record()
             for _ in range(a.iters):
-                ops.gemm(A, W, out=C)
+                ops.gemm(A, W, out=C, **kw)
             e.record()
             torch.cuda.synchronize()
             ms = s.elapsed_time(e) / a.iters
             tf = 2.0 * M * N * K / ms / 1e9
             res[f"{name}/v{v}"] = {"ms": round(ms, 4), "tflops": round(tf, 1)}
-            print(f"{name:7s} v{v:<2d} M={M} N={N} K={K}: {ms:8.3f} ms  {tf:7.1f} TFLOP/s", flush=True)
+            print(f"{name:7s} v{v:<2d} M={M} N={N} K={K} epi={a.epi}: {ms:8.3f} ms  {tf:7.1f} TFLOP/s", flush=True)
         if a.mx:
             from mme import mx
             Aq, Wq = mx.quantize(A), mx.quantize(W)
