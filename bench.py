@@ -53,6 +53,9 @@ def parse():
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline sample duration")
     p.add_argument("--no-kernel-timer", action="store_true")
+    p.add_argument("--bootstrap", type=int, default=0,
+                   help="also time N bootstrap resamples of the recall on the device (main.py:586-634; untimed "
+                        "by the headline metric, reported separately)")
     p.add_argument("--fp8", action="store_true",
                    help="mx8 encoder GEMMs (BASELINE configs[4]: DFN5B-H fp8 weights on the fp8 MFMA)")
     return p.parse_args()
@@ -292,10 +295,13 @@ def main():
     del imgs, ids
     torch.cuda.synchronize()
 
+    last = {}
+
     def step():
         img = model.encode_images(my_imgs, batch=args.img_batch)
         t2i = model.encode_texts(my_t2i, exec_batch=args.txt_batch)
         allc = model.encode_texts(my_caps, exec_batch=args.txt_batch)
+        last.update(img=img, t2i=t2i, allc=allc)
         return sharded_recall(img, t2i, allc, rank, world, n, caps)
 
     for _ in range(args.warmup):
@@ -377,6 +383,19 @@ def main():
         "roofline": roofline,
         "cpu_baseline": None,
     }
+    if world == 1 and args.bootstrap > 0:
+        from mme import bootstrap as mb
+        torch.cuda.synchronize()
+        tb = time.perf_counter()
+        s_t2i, s_i2t = mb.full_scores(last["img"], last["t2i"], last["allc"])
+        hits = mb.bootstrap_hits(s_t2i, s_i2t, mb.sample_indices(n, args.bootstrap, seed=0, device=dev), caps)
+        torch.cuda.synchronize()
+        tb = time.perf_counter() - tb
+        row = mb.bootstrap_row(hits, n)
+        out["bootstrap"] = {"iterations": args.bootstrap, "seconds": round(tb, 3),
+                            "T2I_R@1_mean": round(row["T2I_R@1_mean"], 3),
+                            "T2I_R@1_ci95": [round(row["T2I_R@1_lower"], 3), round(row["T2I_R@1_upper"], 3)],
+                            "note": "full score matrices once + per-resample gather/top-10/recall on the device"}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         sys.path.insert(0, ROOT)
         out["cpu_baseline"] = cpu_baseline(spec, args.cpu_seconds)

@@ -159,6 +159,19 @@ int mme_topk_merge(const int32_t* in_idx, const float* in_score, int rows, int p
 int mme_topk_rows(const float* scores, int ld, int rows, int cols, int k, int col_offset, int32_t* out_idx,
                   float* out_score, void* stream);
 
+/* Bootstrap resampling (§8f-3; run_bootstrap_benchmark main.py:586-634): the score
+ * matrices of B resamples as index gathers of the full matrices,
+ *   out[b][i][p] = S[rows[b*R + i]][g * cols[b*C + p/g] + p % g],   out fp32 [B*R, C*g]
+ * (T2I: S = full T2I, rows = cols = sample, g = 1; I2T: S = full I2T, g = 5; I2T-Sym:
+ * S = T2I transposed). ld = row stride of S in elements. */
+int mme_gather_scores(const float* S, long ld, const int32_t* rows, const int32_t* cols, int B, int R, int C, int g,
+                      float* out, void* stream);
+
+/* Recall hits per resample: row r (of B groups of R rows) targets columns
+ * [(r % R) * tgt_count, +tgt_count); hits [B, nk] += rows whose first kk[j] indices hold a target. */
+int mme_recall_hits_groups(const int32_t* topk_idx, int rows, int k, int R, int tgt_count, const int32_t* kk, int nk,
+                           int64_t* hits, void* stream);
+
 /* Winoground 2x2 scores (§8f-4; run_winoground, run_benchmark_grand_slam_v28_publication_ready.py:413-461):
  * text, image: bf16 [n, 2, D] L2-normalised embeddings of (caption_0, caption_1) and (image_0, image_1).
  * scores: fp32 [n, 4] = bf16(<t_a, i_b>) for (a,b) = 00, 01, 10, 11 (the bf16 torch.matmul);

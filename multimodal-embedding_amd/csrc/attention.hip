@@ -284,8 +284,10 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(AttnArgs a) {
 //     opens tile t (WAR: every wave finished tile t-1 before that barrier;
 //     RAW: each wave retires its own DMA of tile t by a counted vmcnt before it).
 // ---------------------------------------------------------------------------
-template <int HD, int NW, int NSTG>
+template <int HD, int NW, int NSTG, int DIAG = 0>
 __global__ __launch_bounds__(NW * 64) void attn_dma_kernel(AttnArgs a) {
+    // DIAG (dev builds, wrong results; tools/attn_bench.py): 1 no K/V DMA, 2 no exp2,
+    // 3 no PV MFMA, 4 no QK MFMA, 5 no O rescale, 6 no LDS fragment reads
     constexpr int HDP = HD == 64 ? 64 : 96;
     constexpr int NKS = HDP / 32;
     constexpr int NCHL = HD / 8;             // real 16-B planes per K (or V) tile
@@ -334,6 +336,7 @@ __global__ __launch_bounds__(NW * 64) void attn_dma_kernel(AttnArgs a) {
     const int nmine = (NINS - wave + NW - 1) / NW;
     auto issue = [&](int t) {
         char* tb = lds + (t % NSTG) * TILE;
+        if (DIAG == 1) return;
 #pragma unroll
         for (int i = 0; i < MAXI; ++i) {
             const int idx = wave + NW * i;
@@ -394,13 +397,24 @@ __global__ __launch_bounds__(NW * 64) void attn_dma_kernel(AttnArgs a) {
         for (int kt = 0; kt < 4; ++kt) {
             bf16x8 kf[NKS];
 #pragma unroll
-            for (int ks = 0; ks < NKS; ++ks)
-                kf[ks] = *reinterpret_cast<const LDS_AS bf16x8*>((uintptr_t)(tb + koff[ks] + kt * 256));
+            for (int ks = 0; ks < NKS; ++ks) {
+                if (DIAG == 6) {
+                    kf[ks] = qf[0][ks];
+                    asm volatile("" : "+v"(kf[ks]));
+                } else {
+                    kf[ks] = *reinterpret_cast<const LDS_AS bf16x8*>((uintptr_t)(tb + koff[ks] + kt * 256));
+                }
+            }
 #pragma unroll
             for (int u = 0; u < 2; ++u) {
                 f32x4 z = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-                for (int ks = 0; ks < NKS; ++ks) z = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf[ks], qf[u][ks], z, 0, 0, 0);
+                for (int ks = 0; ks < NKS; ++ks) {
+                    if (DIAG == 4)
+                        asm volatile("" : "+v"(z) : "v"(kf[ks]), "v"(qf[u][ks]));
+                    else
+                        z = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf[ks], qf[u][ks], z, 0, 0, 0);
+                }
                 sc[u][kt] = z;
             }
         }
@@ -435,13 +449,16 @@ __global__ __launch_bounds__(NW * 64) void attn_dma_kernel(AttnArgs a) {
             for (int kt = 0; kt < 4; ++kt)
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
-                    const float pv = __builtin_amdgcn_exp2f(sc[u][kt][r] * c - mc);
+                    const float pv = DIAG == 2 ? sc[u][kt][r] * c - mc
+                                               : __builtin_amdgcn_exp2f(sc[u][kt][r] * c - mc);
                     sc[u][kt][r] = pv;
                     psum += pv;
                 }
             lsum[u] = lsum[u] * alpha + psum;
+            if (DIAG != 5) {
 #pragma unroll
-            for (int i = 0; i < NDT; ++i) o[u][i] *= alpha;
+                for (int i = 0; i < NDT; ++i) o[u][i] *= alpha;
+            }
         }
 
 #pragma unroll
@@ -454,14 +471,24 @@ __global__ __launch_bounds__(NW * 64) void attn_dma_kernel(AttnArgs a) {
             const int r1 = 32 * hh + 4 * g + (li >> 2);
 #pragma unroll
             for (int dt = 0; dt < NDT; ++dt) {
-                const unsigned va = tb + voff[dt] + ((r1 ^ vsw[dt]) * 16);
-                const unsigned vb2 = tb + voff[dt] + (((r1 + 16) ^ vsw[dt]) * 16);
-                const s16x4 v0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS_AS s16x4*)(uintptr_t)va);
-                const s16x4 v1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS_AS s16x4*)(uintptr_t)vb2);
-                const bf16x8 vv = __builtin_bit_cast(bf16x8, __builtin_shufflevector(v0, v1, 0, 1, 2, 3, 4, 5, 6, 7));
+                bf16x8 vv;
+                if (DIAG == 6) {
+                    vv = pb[0];
+                    asm volatile("" : "+v"(vv));
+                } else {
+                    const unsigned va = tb + voff[dt] + ((r1 ^ vsw[dt]) * 16);
+                    const unsigned vb2 = tb + voff[dt] + (((r1 + 16) ^ vsw[dt]) * 16);
+                    const s16x4 v0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS_AS s16x4*)(uintptr_t)va);
+                    const s16x4 v1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS_AS s16x4*)(uintptr_t)vb2);
+                    vv = __builtin_bit_cast(bf16x8, __builtin_shufflevector(v0, v1, 0, 1, 2, 3, 4, 5, 6, 7));
+                }
 #pragma unroll
-                for (int u = 0; u < 2; ++u)
-                    o[u][dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vv, pb[u], o[u][dt], 0, 0, 0);
+                for (int u = 0; u < 2; ++u) {
+                    if (DIAG == 3)
+                        asm volatile("" : "+v"(o[u][dt]) : "v"(vv), "v"(pb[u]));
+                    else
+                        o[u][dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vv, pb[u], o[u][dt], 0, 0, 0);
+                }
             }
         }
     }
@@ -556,6 +583,12 @@ void launch_attn(int kind, const AttnArgs& a, int B, int T, int H, hipStream_t s
         hipLaunchKernelGGL((attn_fwd_kernel<HD>), dim3(cdiv(T, 128) * H * B), dim3(256), 0, st, a);
     else if (kind == 1)
         hipLaunchKernelGGL((attn_dma_kernel<HD, 4, 2>), dim3(cdiv(T, 128) * H * B), dim3(256), 0, st, a);
+    else if (kind == 3)
+        hipLaunchKernelGGL((attn_dma_kernel<HD, 2, 2>), dim3(cdiv(T, 64) * H * B), dim3(128), 0, st, a);
+    else if (kind == 4)
+        hipLaunchKernelGGL((attn_dma_kernel<HD, 8, 3>), dim3(cdiv(T, 256) * H * B), dim3(512), 0, st, a);
+    else if (kind == 5)
+        hipLaunchKernelGGL((attn_dma_kernel<HD, 4, 3>), dim3(cdiv(T, 128) * H * B), dim3(256), 0, st, a);
     else
         hipLaunchKernelGGL((attn_dma_kernel<HD, 8, 2>), dim3(cdiv(T, 256) * H * B), dim3(512), 0, st, a);
 }
@@ -597,7 +630,20 @@ extern "C" int mme_attention(const void* qkv, int ld_qkv, void* out, int ld_out,
         }
         return mme_check_launch("mme_attention");
     }
-    if (g_attn_variant >= 9 && g_attn_variant <= 11) kind = g_attn_variant - 9;  // dev: force a kernel
+    if (g_attn_variant >= 9 && g_attn_variant <= 14) kind = g_attn_variant - 9;  // dev: force a kernel
+    if (g_attn_variant >= 21 && g_attn_variant <= 26 && hd == 72) {  // dev: attn_dma_kernel<72,8,2> diagnostics
+        const dim3 grid(cdiv(T, 256) * H * B), blk(512);
+        hipStream_t st = as_stream(stream);
+        switch (g_attn_variant) {
+            case 21: hipLaunchKernelGGL((attn_dma_kernel<72, 8, 2, 1>), grid, blk, 0, st, a); break;
+            case 22: hipLaunchKernelGGL((attn_dma_kernel<72, 8, 2, 2>), grid, blk, 0, st, a); break;
+            case 23: hipLaunchKernelGGL((attn_dma_kernel<72, 8, 2, 3>), grid, blk, 0, st, a); break;
+            case 24: hipLaunchKernelGGL((attn_dma_kernel<72, 8, 2, 4>), grid, blk, 0, st, a); break;
+            case 25: hipLaunchKernelGGL((attn_dma_kernel<72, 8, 2, 5>), grid, blk, 0, st, a); break;
+            default: hipLaunchKernelGGL((attn_dma_kernel<72, 8, 2, 6>), grid, blk, 0, st, a); break;
+        }
+        return mme_check_launch("mme_attention");
+    }
     if (hd == 64)
         launch_attn<64>(kind, a, B, T, H, as_stream(stream));
     else if (hd == 72)

@@ -259,6 +259,57 @@ __global__ __launch_bounds__(256) void winoground_kernel(const bf16* __restrict_
     }
 }
 
+// Bootstrap resampling (main.py:586-624): the score matrices of one resample are
+// index gathers of the full matrices: out[b][i][p] = S[rows[b][i]][g*cols[b][p/g] + p%g]
+// (T2I: g = 1; I2T: g = 5 captions per sampled image, compute_similarity_scores over
+// all_txt[sampled_i2t_cap_indices]; I2T-Sym: the transposed T2I matrix, g = 1).
+// One block per output row; 16-B coalesced stores; the column gather reads S[row]
+// (20 KB / 100 KB rows, L2/MALL-resident across the rows that share it).
+__global__ __launch_bounds__(256) void gather_scores_kernel(const float* __restrict__ S, long ld,
+                                                            const int32_t* __restrict__ rows,
+                                                            const int32_t* __restrict__ cols, int R, int C, int g,
+                                                            float* __restrict__ out) {
+    const long orow = blockIdx.x;  // b*R + i
+    const int b = orow / R;
+    const float* src = S + (long)rows[orow] * ld;
+    const int32_t* cb = cols + (long)b * C;
+    const int W = C * g;
+    float* dst = out + orow * W;
+    for (int p0 = threadIdx.x * 4; p0 < W; p0 += 256 * 4) {
+        float v[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            const int p = p0 + e;
+            v[e] = p < W ? src[(long)g * cb[p / g] + p % g] : 0.f;
+        }
+        if (p0 + 3 < W && (W & 3) == 0) {
+            *reinterpret_cast<float4*>(dst + p0) = make_float4(v[0], v[1], v[2], v[3]);
+        } else {
+            for (int e = 0; e < 4; ++e)
+                if (p0 + e < W) dst[p0 + e] = v[e];
+        }
+    }
+}
+
+// Recall hits per group of R rows (one bootstrap resample per group): row r of group
+// b targets columns [(r % R) * tc, (r % R) * tc + tc); hits[b][j] += row hit within kk[j].
+__global__ void recall_groups_kernel(const int32_t* __restrict__ idx, int rows, int k, int R, int tc,
+                                     const int32_t* __restrict__ kk, int nk, unsigned long long* __restrict__ hits) {
+    const int r = blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= rows) return;
+    const int lo = (r % R) * tc, hi = lo + tc;
+    int first = k;
+    for (int j = 0; j < k; ++j) {
+        const int c = idx[(long)r * k + j];
+        if (c >= lo && c < hi) {
+            first = j;
+            break;
+        }
+    }
+    for (int j = 0; j < nk; ++j)
+        if (first < min(kk[j], k)) atomicAdd(&hits[(long)(r / R) * nk + j], 1ull);
+}
+
 size_t sim_splits(int nq, int nd, int k, int* tiles_per_split) {
     const int nqt = (nq + 127) / 128, ntiles = (nd + 127) / 128;
     // aim for >= 1024 workgroups, >= 4 tiles per split, and a candidate list
@@ -321,6 +372,27 @@ extern "C" int mme_topk_rows(const float* scores, int ld, int rows, int cols, in
     hipLaunchKernelGGL(topk_rows_kernel, dim3(cdiv(rows, 4)), dim3(256), 0, as_stream(stream), scores, ld, rows, cols,
                        k, col_offset, out_idx, out_score);
     return mme_check_launch("mme_topk_rows");
+}
+
+extern "C" int mme_gather_scores(const float* S, long ld, const int32_t* rows, const int32_t* cols, int B, int R,
+                                 int C, int g, float* out, void* stream) {
+    MME_REQUIRE(S && rows && cols && out, "mme_gather_scores: null pointer");
+    MME_REQUIRE(B >= 0 && R >= 0 && C > 0 && g >= 1 && ld > 0, "mme_gather_scores: bad shape");
+    MME_REQUIRE((long)B * R < (1L << 31), "mme_gather_scores: too many output rows");
+    if (B == 0 || R == 0) return MME_OK;
+    hipLaunchKernelGGL(gather_scores_kernel, dim3(B * R), dim3(256), 0, as_stream(stream), S, ld, rows, cols, R, C, g,
+                       out);
+    return mme_check_launch("mme_gather_scores");
+}
+
+extern "C" int mme_recall_hits_groups(const int32_t* topk_idx, int rows, int k, int R, int tgt_count, const int32_t* kk,
+                                      int nk, int64_t* hits, void* stream) {
+    MME_REQUIRE(topk_idx && kk && hits, "mme_recall_hits_groups: null pointer");
+    MME_REQUIRE(rows >= 0 && k >= 1 && R >= 1 && tgt_count >= 1 && nk >= 1, "mme_recall_hits_groups: bad args");
+    if (rows == 0) return MME_OK;
+    hipLaunchKernelGGL(recall_groups_kernel, dim3(cdiv(rows, 256)), dim3(256), 0, as_stream(stream), topk_idx, rows, k,
+                       R, tgt_count, kk, nk, (unsigned long long*)hits);
+    return mme_check_launch("mme_recall_hits_groups");
 }
 
 extern "C" int mme_winoground(const void* text, const void* image, int n, int D, float* scores, int64_t* counts,

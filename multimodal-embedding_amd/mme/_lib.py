@@ -39,6 +39,8 @@ SIGNATURES = {
     "mme_sim_topk_workspace_bytes": (c_size_t, [c_int, c_int, c_int]),
     "mme_sim_topk": (c_int, [_P, c_int, _P, c_int, c_int, c_int, c_int, c_int, c_int, _P, _P, _P, c_size_t, _P]),
     "mme_topk_merge": (c_int, [_P, _P, c_int, c_int, c_int, _P, _P, _P]),
+    "mme_gather_scores": (c_int, [_P, ctypes.c_long, _P, _P, c_int, c_int, c_int, c_int, _P, _P]),
+    "mme_recall_hits_groups": (c_int, [_P, c_int, c_int, c_int, c_int, _P, c_int, _P, _P]),
     "mme_winoground": (c_int, [_P, _P, c_int, c_int, _P, _P, _P]),
     "mme_topk_rows": (c_int, [_P, c_int, c_int, c_int, c_int, c_int, _P, _P, _P]),
     "mme_recall_hits":(c_int, [_P, c_int, c_int, _P, c_int, c_int, _P, c_int, _P, _P]),

@@ -392,6 +392,34 @@ def topk_rows(scores: torch.Tensor, k: int, col_offset: int = 0):
     return idx, sc
 
 
+def gather_scores(S: torch.Tensor, rows: torch.Tensor, cols: torch.Tensor, g: int = 1,
+                  out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """out[b*R + i, p] = S[rows[b, i], g*cols[b, p // g] + p % g]  (fp32 [B*R, C*g])."""
+    _dev(S, rows, cols, out)
+    if S.dtype != torch.float32 or rows.dtype != torch.int32 or cols.dtype != torch.int32:
+        raise ValueError("gather_scores: S fp32, rows / cols int32")
+    B, R = rows.shape
+    C = cols.shape[1]
+    if cols.shape[0] != B:
+        raise ValueError("gather_scores: rows / cols batch mismatch")
+    if out is None:
+        out = torch.empty(B * R, C * g, dtype=torch.float32, device=S.device)
+    call("mme_gather_scores", S.data_ptr(), _rowmajor(S, "S"), rows.contiguous().data_ptr(),
+         cols.contiguous().data_ptr(), B, R, C, g, out.data_ptr(), _stream())
+    return out
+
+
+def recall_hits_groups(topk_idx: torch.Tensor, R: int, tgt_count: int, ks: Sequence[int]) -> torch.Tensor:
+    """int64 [rows // R, len(ks)]: per group of R rows, rows whose first ks[j] indices hold a target."""
+    _dev(topk_idx)
+    rows, k = topk_idx.shape
+    kk = torch.tensor(list(ks), dtype=torch.int32, device=topk_idx.device)
+    hits = torch.zeros(rows // R, len(ks), dtype=torch.int64, device=topk_idx.device)
+    call("mme_recall_hits_groups", topk_idx.contiguous().data_ptr(), rows, k, R, tgt_count, kk.data_ptr(), len(ks),
+         hits.data_ptr(), _stream())
+    return hits
+
+
 def winoground(text: torch.Tensor, image: torch.Tensor):
     """(scores fp32 [n, 4] = bf16 <t_a, i_b> for ab = 00,01,10,11, counts int64 [3] text/image/group)."""
     _dev(text, image)

@@ -454,6 +454,32 @@ def make_winoground():
     print("winoground.npz:", {k: v.tolist() for k, v in out.items() if k.endswith("metrics")})
 
 
+# ------------------------------------------------------------------ bootstrap
+def make_bootstrap(main):
+    """The reference's own resampled scoring + compute_metrics_detailed (main.py:586-634) on planted
+    embeddings, with seeded sample indices (the reference's np.random.choice is unseeded, §0.5)."""
+    n, caps, D, iters = 120, 5, 64, 25
+    img, all_txt = planted(n, caps, D, noise=1.2, seed=4)
+    t2i = all_txt[::caps].contiguous()
+    rng = np.random.default_rng(11)
+    samples = rng.integers(0, n, (iters, n)).astype(np.int32)
+    main.DEVICE = "cpu"
+    m_info = {"type": "dense"}
+    vals = []
+    for smp in samples:
+        si, st = img[smp], t2i[smp]
+        capidx = [c for i in smp for c in range(caps * int(i), caps * int(i) + caps)]
+        s_t2i = main.compute_similarity_scores(si, st, m_info, None)
+        s_i2t = main.compute_similarity_scores(all_txt[capidx], si, m_info, None)  # v28 orientation (no .t())
+        m = main.compute_metrics_detailed(s_t2i, s_i2t, s_t2i.t(), list(range(n)),
+                                          {i: list(range(caps * i, caps * i + caps)) for i in range(n)},
+                                          {i: i for i in range(n)}, [""] * n)
+        vals.append([m[f"{p}_R@{k}"] for p in ("T2I", "I2T", "I2T_Sym") for k in (1, 5, 10)])
+    np.savez_compressed(os.path.join(HERE, "bootstrap.npz"), img=bf16_bits(img), all_txt=bf16_bits(all_txt),
+                        samples=samples, metrics=np.array(vals, np.float64))
+    print("bootstrap.npz:", np.array(vals).mean(0).round(2))
+
+
 if __name__ == "__main__":
     torch.manual_seed(0)
     main = import_reference()
@@ -461,7 +487,7 @@ if __name__ == "__main__":
     steps = {"preprocess": make_preprocess, "l2norm": lambda: make_l2norm(main),
              "retrieval": lambda: make_retrieval(main), "maxsim": lambda: make_maxsim(main),
              "encoders": lambda: make_encoders(main), "colpali": lambda: make_colpali(main),
-             "winoground": make_winoground}
+             "winoground": make_winoground, "bootstrap": lambda: make_bootstrap(main)}
     for name, fn in steps.items():
         if not only or name in only:
             fn()

@@ -1,0 +1,79 @@
+"""Bootstrap resampling vs the reference's own resampled scoring +
+compute_metrics_detailed (tests/golden/bootstrap.npz, seeded sample indices).
+
+CPU: the oracle (full matrices + index gathers, position order among ties) gives the
+reference's per-iteration metrics on every row whose result the scores determine:
+|oracle - reference| <= the rows where a duplicated image's tie group straddles the
+k-th place (torch.topk's order among equal values is implementation defined).
+GPU: the device path (mme_gather_scores + mme_topk_rows + mme_recall_hits_groups)
+equals the oracle bit-exactly on the same score matrices."""
+import numpy as np
+import pytest
+import torch
+
+from helpers import bits_to_f32
+
+
+def _tables(g):
+    img = bits_to_f32(g["img"])
+    allt = bits_to_f32(g["all_txt"])
+    return img, allt[::5].copy(), allt
+
+
+def test_oracle_vs_reference_bootstrap(golden):
+    from oracle import bootstrap as ob
+    g = golden("bootstrap")
+    img, t2i, allt = _tables(g)
+    n = img.shape[0]
+    s_t2i = (torch.from_numpy(t2i) @ torch.from_numpy(img).T).numpy()
+    s_i2t = (torch.from_numpy(img) @ torch.from_numpy(allt).T).numpy()
+    exact = 0
+    for smp, ref in zip(g["samples"], g["metrics"]):
+        hits, amb = ob.resample_hits(s_t2i, s_i2t, smp)
+        got = 100.0 * hits / n
+        assert np.all(np.abs(got - ref) <= 100.0 * amb / n + 1e-9), (got, ref, amb)
+        exact += int(np.sum(got == ref))
+    # a duplicated top-1 image is tied with its copy in ~40 % of rows, so which copy
+    # torch.topk returns decides R@1 there; most metric values still agree exactly
+    assert exact > 0.5 * g["metrics"].size
+
+
+@pytest.mark.gpu
+def test_device_bootstrap_equals_oracle(cuda, golden):
+    from mme import bootstrap as mb
+    from oracle import bootstrap as ob
+    g = golden("bootstrap")
+    img, t2i, allt = (torch.from_numpy(x).to("cuda", torch.bfloat16) for x in _tables(g))
+    s_t2i, s_i2t = mb.full_scores(img, t2i, allt)
+    samples = torch.from_numpy(g["samples"]).cuda()
+    hits = mb.bootstrap_hits(s_t2i, s_i2t, samples, batch=7).cpu().numpy()
+    a, b = s_t2i.cpu().numpy(), s_i2t.cpu().numpy()
+    for it, smp in enumerate(g["samples"]):
+        ref, _ = ob.resample_hits(a, b, smp)
+        assert np.array_equal(hits[it], ref), it
+    n = img.shape[0]
+    row = mb.bootstrap_row(torch.from_numpy(hits), n)
+    assert list(row)[:4] == ["T2I_R@1_mean", "T2I_R@1_lower", "T2I_R@1_upper", "T2I_R@1_std"]
+    assert row["T2I_R@1_lower"] <= row["T2I_R@1_mean"] <= row["T2I_R@1_upper"]
+    # metrics vs the reference's per-iteration values within the tie-ambiguous rows
+    assert np.abs(row["T2I_R@1_mean"] - g["metrics"][:, 0].mean()) <= 2.0
+
+
+@pytest.mark.gpu
+def test_device_bootstrap_large(cuda):
+    """n = 5 000, 40 resamples: the device path runs at the headline size (hits vs oracle on 2)."""
+    from mme import bootstrap as mb
+    from oracle import bootstrap as ob
+    gen = torch.Generator(device="cuda").manual_seed(0)
+    n, D = 5000, 256
+    base = torch.randn(n, D, device="cuda", generator=gen)
+    nrm = lambda x: (x / x.norm(dim=-1, keepdim=True)).to(torch.bfloat16)
+    img = nrm(base + 1.5 * torch.randn(n, D, device="cuda", generator=gen))
+    allt = nrm(base.repeat_interleave(5, 0) + 1.5 * torch.randn(5 * n, D, device="cuda", generator=gen))
+    s_t2i, s_i2t = mb.full_scores(img, allt[::5].contiguous(), allt)
+    samples = mb.sample_indices(n, 40, seed=1)
+    hits = mb.bootstrap_hits(s_t2i, s_i2t, samples).cpu().numpy()
+    a, b = s_t2i.cpu().numpy(), s_i2t.cpu().numpy()
+    for it in (0, 39):
+        ref, _ = ob.resample_hits(a, b, samples[it].cpu().numpy())
+        assert np.array_equal(hits[it], ref), it

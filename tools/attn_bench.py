@@ -25,7 +25,7 @@ CASES = [  # name, B, T, H, hd, causal
     ("clip_text_causal", 1024, 77, 16, 64, True),
 ]
 for (name, B, T, H, hd, causal), v in [(c, v) for c in CASES for v in VARIANTS]:
-    if 1 <= v <= 4 and hd != 72:
+    if (1 <= v <= 4 or 21 <= v <= 26) and (hd != 72 or (v >= 21 and T < 256)):
         continue
     torch.manual_seed(0)
     qkv = torch.randn(B * T, 3 * H * hd, device="cuda").to(torch.bfloat16)
@@ -38,11 +38,15 @@ for (name, B, T, H, hd, causal), v in [(c, v) for c in CASES for v in VARIANTS]:
     err = (out.float() - ref).abs().max().item()
     s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     it = 5
-    s.record()
-    for _ in range(it):
+    for _ in range(3):  # warm the clocks / caches for this variant
         ops.attention(qkv, B, T, H, hd, causal=causal, out=out)
-    e.record()
-    torch.cuda.synchronize()
-    ms = s.elapsed_time(e) / it
+    ms = 1e30
+    for rep in range(3):  # best of 3 timed groups
+        s.record()
+        for _ in range(it):
+            ops.attention(qkv, B, T, H, hd, causal=causal, out=out)
+        e.record()
+        torch.cuda.synchronize()
+        ms = min(ms, s.elapsed_time(e) / it)
     fl = 4.0 * B * H * T * T * hd * (0.5 if causal else 1.0)
     print(f"{name:18s} v{v} B={B} T={T} H={H} hd={hd}: {ms:7.3f} ms {fl / ms / 1e9:7.1f} TFLOP/s  maxdiff vs v0 {err:.3g}", flush=True)
