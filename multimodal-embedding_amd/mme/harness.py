@@ -39,8 +39,13 @@ def encode_job(model, images_u8: torch.Tensor, caption_ids: torch.Tensor, captio
 
 
 def run_benchmark(model, images_u8: torch.Tensor, caption_ids: torch.Tensor, caption_lens=None,
-                  caps_per_image: int = 5, warmup: bool = True, **kw) -> Dict[str, object]:
-    """One timed encode + retrieval job; returns the reference's result row."""
+                  caps_per_image: int = 5, warmup: bool = True, n_iterations: int = 0, seed: int = 0,
+                  **kw) -> Dict[str, object]:
+    """One timed encode + retrieval job; returns the reference's result row.
+
+    n_iterations > 0: the metrics are the bootstrap of run_bootstrap_benchmark
+    (main.py:563-651: resamples with replacement, mean / 95 % CI / std per metric) on
+    the device (mme.bootstrap); 0: the identity sample (mean = lower = upper, std 0)."""
     name = model.spec.name
     if warmup:  # v28: warmup outside the timed region
         encode_job(model, images_u8[:2], caption_ids[: 2 * caps_per_image], None if caption_lens is None else
@@ -50,14 +55,20 @@ def run_benchmark(model, images_u8: torch.Tensor, caption_ids: torch.Tensor, cap
     img, t2i, all_txt = encode_job(model, images_u8, caption_ids, caption_lens, caps_per_image, **kw)
     torch.cuda.synchronize()
     t_enc = time.time() - t0
-    metrics = compute_metrics(img, t2i, all_txt, caps_per_image)
-    torch.cuda.synchronize()
-    t_total = time.time() - t0
     n = images_u8.shape[0]
     row: Dict[str, object] = {"Model": name}
-    for k in METRIC_KEYS:
-        v = metrics[k]
-        row[f"{k}_mean"], row[f"{k}_lower"], row[f"{k}_upper"], row[f"{k}_std"] = v, v, v, 0.0
+    if n_iterations > 0:
+        from . import bootstrap as mb
+        s_t2i, s_i2t = mb.full_scores(img, t2i, all_txt)
+        hits = mb.bootstrap_hits(s_t2i, s_i2t, mb.sample_indices(n, n_iterations, seed, img.device), caps_per_image)
+        row.update(mb.bootstrap_row(hits, n, seed=seed))
+    else:
+        metrics = compute_metrics(img, t2i, all_txt, caps_per_image)
+        for k in METRIC_KEYS:
+            v = metrics[k]
+            row[f"{k}_mean"], row[f"{k}_lower"], row[f"{k}_upper"], row[f"{k}_std"] = v, v, v, 0.0
+    torch.cuda.synchronize()
+    t_total = time.time() - t0
     row["Time"] = t_total
     row["QPS"] = n / t_total
     row["Encoding_Time"] = t_enc

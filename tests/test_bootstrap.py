@@ -77,3 +77,23 @@ def test_device_bootstrap_large(cuda):
     for it in (0, 39):
         ref, _ = ob.resample_hits(a, b, samples[it].cpu().numpy())
         assert np.array_equal(hits[it], ref), it
+
+
+@pytest.mark.gpu
+def test_harness_bootstrap_row(cuda, tmp_path):
+    """run_benchmark(n_iterations>0) -> the reference's CSV row with bootstrap mean / CI / std."""
+    from mme import get_spec
+    from mme.harness import METRIC_KEYS, run_benchmark, write_csv
+    from mme.models import SiglipModel
+    from weights_gen import torch_state_dict
+    spec = get_spec("tiny-siglip")
+    model = SiglipModel.from_spec(spec, device="cuda", state_dict=torch_state_dict(spec, 0, torch.bfloat16))
+    rng = np.random.default_rng(0)
+    imgs = torch.from_numpy(rng.integers(0, 256, (12, 64, 64, 3), dtype=np.uint8)).cuda()
+    ids = torch.from_numpy(np.concatenate([rng.integers(2, 1000, (60, 15)), np.ones((60, 1), np.int64)], 1)).cuda()
+    row = run_benchmark(model, imgs, ids, n_iterations=20)
+    cols = [f"{k}_{s}" for k in METRIC_KEYS for s in ("mean", "lower", "upper", "std")]
+    assert list(row)[1:1 + len(cols)] == cols
+    assert all(row[f"{k}_lower"] <= row[f"{k}_mean"] + 1e-9 <= row[f"{k}_upper"] + 2e-9 for k in METRIC_KEYS)
+    write_csv([row], str(tmp_path / "r.csv"))
+    assert (tmp_path / "r.csv").read_text().splitlines()[0].startswith(",Model,T2I_R@1_mean")
