@@ -53,6 +53,9 @@ def parse():
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline sample duration")
     p.add_argument("--no-kernel-timer", action="store_true")
+    p.add_argument("--host-inputs", action="store_true",
+                   help="also time one job whose u8 images start in host memory (streamed H2D, SURVEY 8f-2); "
+                        "reported as host_inputs_img_s, never as value")
     p.add_argument("--bootstrap", type=int, default=0,
                    help="also time N bootstrap resamples of the recall on the device (main.py:586-634; untimed "
                         "by the headline metric, reported separately)")
@@ -383,6 +386,16 @@ def main():
         "roofline": roofline,
         "cpu_baseline": None,
     }
+    if args.host_inputs:
+        host_imgs = my_imgs.cpu().pin_memory()
+        barrier()
+        th = time.perf_counter()
+        img = model.encode_images(host_imgs, batch=args.img_batch)
+        t2i = model.encode_texts(my_t2i, exec_batch=args.txt_batch)
+        allc = model.encode_texts(my_caps, exec_batch=args.txt_batch)
+        sharded_recall(img, t2i, allc, rank, world, n, caps)
+        barrier()
+        out["host_inputs_img_s"] = round(n / (time.perf_counter() - th), 2)
     if world == 1 and args.bootstrap > 0:
         from mme import bootstrap as mb
         torch.cuda.synchronize()

@@ -250,11 +250,14 @@ class DualEncoder:
     @torch.no_grad()
     def encode_images(self, images_u8: torch.Tensor, batch: int = 256, out: Optional[torch.Tensor] = None
                       ) -> torch.Tensor:
-        """u8 [n,H,W,3] device images -> L2-normalised bf16 embeddings [n, D].
+        """u8 [n,H,W,3] images -> L2-normalised bf16 embeddings [n, D].
 
         Fuses the processor (PIL-exact bicubic + normalise) into an im2col
         kernel feeding the patch GEMM. Batch size does not change results
-        (images never interact)."""
+        (images never interact). Images in host memory (the
+        reference's loader hands over host buffers) are streamed: batch i+1 is
+        copied host -> HBM on a side stream (pinned staging, two device buffers)
+        while batch i is encoded, so the PCIe transfer hides under the encoder."""
         from .processor import image_geometry
         v, ip = self.spec.vision, self.spec.image_proc
         n, H, W, _ = images_u8.shape
@@ -262,11 +265,37 @@ class DualEncoder:
         if out is None:
             out = torch.empty(n, self.spec.proj_dim, dtype=BF16, device=self.device)
         batch = balanced(n, batch)
+        stream_in = not images_u8.is_cuda
+        if stream_in:
+            src = images_u8 if images_u8.is_pinned() else images_u8.pin_memory()
+            copy_stream = torch.cuda.Stream(device=self.device)
+            bufs = [torch.empty((batch, H, W, 3), dtype=torch.uint8, device=self.device) for _ in range(2)]
+            done = [torch.cuda.Event(), torch.cuda.Event()]   # copy into buffer j finished
+            free = [torch.cuda.Event(), torch.cuda.Event()]   # compute stopped reading buffer j
+
+            def prefetch(i, j):
+                b = min(batch, n - i)
+                with torch.cuda.stream(copy_stream):
+                    copy_stream.wait_event(free[j])
+                    bufs[j][:b].copy_(src[i:i + b], non_blocking=True)
+                    done[j].record(copy_stream)
+            for j in range(2):
+                free[j].record()
+            prefetch(0, 0)
         for i in range(0, n, batch):
-            chunk = images_u8[i:i + batch]
+            if stream_in:
+                j = (i // batch) & 1
+                if i + batch < n:
+                    prefetch(i + batch, j ^ 1)
+                torch.cuda.current_stream().wait_event(done[j])
+                chunk = bufs[j][:min(batch, n - i)]
+            else:
+                chunk = images_u8[i:i + batch]
             b = chunk.shape[0]
             patches = ops.preprocess_u8(chunk, resize=(rh, rw), crop=(top, left), size=ip.size, mean=ip.mean,
                                         std=ip.std, patch=v.patch, kpad=v.kpad)
+            if stream_in:
+                free[j].record()  # the preprocess kernel (the buffer's only reader) is enqueued
             feats = self.vision.forward_patches(patches, b)
             ops.l2norm(feats, out=out[i:i + b])
         return out

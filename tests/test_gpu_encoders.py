@@ -86,3 +86,15 @@ def test_full_size_towers_vs_oracle(cuda, name, n_img, n_cap):
     oi, ot = oracle_enc.encode_data(spec, sd_cpu, list(imgs), ids.tolist(), bs=n_img, out_dtype=torch.float32)
     assert row_cos(gi, oi).min() >= COS_MIN
     assert row_cos(gt, ot).min() >= COS_MIN
+
+
+def test_encode_images_from_host_memory(cuda, golden):
+    """host-resident u8 images streamed H2D (double-buffered side-stream copies)
+    give the same embeddings as device-resident ones."""
+    spec = get_spec("tiny-siglip")
+    model = _model(spec)
+    rng = np.random.default_rng(3)
+    imgs = torch.from_numpy(rng.integers(0, 256, (11, 80, 96, 3), dtype=np.uint8))
+    dev = model.encode_images(imgs.cuda(), batch=4).cpu()
+    host = model.encode_images(imgs, batch=4).cpu()
+    assert torch.equal(dev, host)
