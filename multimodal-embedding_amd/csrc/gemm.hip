@@ -35,6 +35,7 @@ struct GemmArgs {
     int lda, ldb, ldc, ldr;
     int M, N, K;
     int res_period, act, out_f32;
+    int stagger;  // dev: s_sleep(127) units per phase step for the first wave of blocks (0 = off)
 };
 
 template <class C, int GROUP_M>
@@ -131,9 +132,14 @@ struct PCfg {
 // Shared epilogue of the pipelined kernels: bias + activation in registers,
 // bf16 tile staged in LDS (row pitch BN*2+16 B), 16-B stores with the
 // residual / position-table add fused. Starts with a barrier (LDS reuse).
-template <class C, int ACT>
+template <class C, int ACT, int EDIAG = 0>
 __device__ __forceinline__ void gemm_epilogue_lds(const GemmArgs& p, char* lds, f32x4 (&acc)[C::FM][C::FN], int m0,
                                                   int n0, int wm, int wn, int g, int li, int tid) {
+    // EDIAG (dev builds, wrong results): 1 = no global stores, 2 = no epilogue at all
+    if (EDIAG == 2) {
+        if (tid == 0 && m0 < 0) reinterpret_cast<float*>(p.C)[0] = acc[0][0][0];
+        return;
+    }
     // GeGLU (MME_ACT_GEGLU_TANH): B rows are [gate 4k..4k+3, up 4k..4k+3] per group of 8,
     // so each 16-B chunk of the bf16 tile holds 4 gate and 4 up outputs of the same
     // features -> out[:, gc/2 + e] = bf16( bf16(gelu_tanh(bf16 gate)) * bf16 up )
@@ -183,19 +189,26 @@ __device__ __forceinline__ void gemm_epilogue_lds(const GemmArgs& p, char* lds, 
         const int gr = m0 + row, gc = n0 + cc * 8;
         if (gr >= p.M || gc >= p.N) continue;
         u16x8 v = *reinterpret_cast<const u16x8*>(lds + row * C::OUT_LD + cc * 16);
+        // non-temporal stores: the tile is not re-read by this kernel and its consumer
+        // streams it from HBM anyway (outputs >> MALL); +1-2 % over plain stores
         if (GLU) {
-            bf16x4 o;
+            u16x4 o;
 #pragma unroll
             for (int e = 0; e < 4; ++e)
-                o[e] = f2bf(bf2f(f2bf(apply_act(bits2f(v[e]), MME_ACT_GELU_TANH))) * bits2f(v[4 + e]));
-            *reinterpret_cast<bf16x4*>(Cout + (size_t)gr * p.ldc + gc / 2) = o;
+                o[e] = __builtin_bit_cast(unsigned short,
+                                          f2bf(bf2f(f2bf(apply_act(bits2f(v[e]), MME_ACT_GELU_TANH))) * bits2f(v[4 + e])));
+            __builtin_nontemporal_store(o, reinterpret_cast<u16x4*>(Cout + (size_t)gr * p.ldc + gc / 2));
         } else if (p.res) {
-            bf16x8 o;
+            u16x8 o;
 #pragma unroll
-            for (int e = 0; e < 8; ++e) o[e] = f2bf(bits2f(v[e]) + bits2f(rv[q][e]));
-            *reinterpret_cast<bf16x8*>(Cout + (size_t)gr * p.ldc + gc) = o;
-        } else {
+            for (int e = 0; e < 8; ++e) o[e] = __builtin_bit_cast(unsigned short, f2bf(bits2f(v[e]) + bits2f(rv[q][e])));
+            __builtin_nontemporal_store(o, reinterpret_cast<u16x8*>(Cout + (size_t)gr * p.ldc + gc));
+        } else if (EDIAG == 1) {
+            asm volatile("" ::"v"(v));
+        } else if (EDIAG == 3) {  // dev: plain (temporal) stores, for A/B against the NT default
             *reinterpret_cast<u16x8*>(Cout + (size_t)gr * p.ldc + gc) = v;
+        } else {
+            __builtin_nontemporal_store(v, reinterpret_cast<u16x8*>(Cout + (size_t)gr * p.ldc + gc));
         }
     }
 }
@@ -542,6 +555,10 @@ __global__ __launch_bounds__(C::NT, 2) void gemm_pipe6_kernel(GemmArgs p) {
     int bm, bn;
     tile_coords<GROUP_M>(tile, nbm, nbn, bm, bn);
     const int m0 = bm * C::BM, n0 = bn * C::BN;
+    if (p.stagger && blockIdx.x < 256) {  // dev: de-phase the first wave of blocks
+        const int ph = (blockIdx.x >> 3) & 3;
+        for (int i = 0; i < ph * p.stagger; ++i) __builtin_amdgcn_s_sleep(127);
+    }
 
     const bf16* src[C::PPW];
     int dst[C::PPW];
@@ -632,7 +649,7 @@ __global__ __launch_bounds__(C::NT, 2) void gemm_pipe6_kernel(GemmArgs p) {
     }
     if (STAG && wm == 0) __builtin_amdgcn_s_barrier();
 
-    gemm_epilogue_lds<C, ACT>(p, lds, acc, m0, n0, wm, wn, g, li, tid);
+    gemm_epilogue_lds<C, ACT, (DIAG >= 6 ? DIAG - 5 : 0)>(p, lds, acc, m0, n0, wm, wn, g, li, tid);
 }
 
 template <class C, int GROUP_M, int STAG, int DIAG = 0>
@@ -696,8 +713,12 @@ extern "C" int mme_gemm(const void* A, int lda, const void* B, int ldb, void* Cp
     MME_REQUIRE(!residual || ldr >= N, "mme_gemm: ldr < N");
     MME_REQUIRE(res_period >= 0, "mme_gemm: res_period < 0");
     GemmArgs a{(const bf16*)A, (const bf16*)B, Cp, (const bf16*)bias, (const bf16*)residual,
-               lda, ldb, ldc, ldr, M, N, K, res_period, act, out_f32};
+               lda, ldb, ldc, ldr, M, N, K, res_period, act, out_f32, 0};
     hipStream_t s = as_stream(stream);
+    if (g_variant >= 40 && g_variant <= 43) {  // dev: pipe6 with the first block wave de-phased by
+        a.stagger = (g_variant - 39) * (K / 32) / 12;  // (variant-39)/4 of a tile per phase step
+        return launch_pipe6<Pipe256, 4, 1>(a, s);
+    }
     if (glu) {  // gated epilogue: the pipelined kernel only (its LDS-staged 16-B tile rows pair gate/up)
         MME_REQUIRE(N % 8 == 0 && ldc % 4 == 0 && !out_f32 && !residual && ((uintptr_t)Cp & 7) == 0,
                     "mme_gemm: GeGLU needs N %% 8 == 0, ldc %% 4 == 0, 8-B aligned bf16 C, no residual");
@@ -727,6 +748,9 @@ extern "C" int mme_gemm(const void* A, int lda, const void* B, int ldb, void* Cp
         case 35: return launch_pipe6<Pipe256, 4, 1, 3>(a, s);  // diagnostic: no ds_read
         case 36: return launch_pipe6<Pipe256, 4, 1, 4>(a, s);  // diagnostic: DMA + barriers only
         case 37: return launch_pipe6<Pipe256, 4, 1, 5>(a, s);  // diagnostic: DMA of one L2-resident tile
+        case 38: return launch_pipe6<Pipe256, 4, 1, 6>(a, s);  // diagnostic: epilogue without global stores
+        case 39: return launch_pipe6<Pipe256, 4, 1, 7>(a, s);  // diagnostic: no epilogue
+        case 44: return launch_pipe6<Pipe256, 4, 1, 8>(a, s);  // dev: plain (temporal) output stores
         default: break;
     }
     // production dispatch: the pipelined 256x256 kernel whenever its 16-byte
