@@ -611,6 +611,7 @@ __global__ __launch_bounds__(C::NT, 2) void gemm_pipe6_kernel(GemmArgs p) {
         // ---- memory phase
         const unsigned so = (t % C::NSTAGE) * C::STAGE;
         const unsigned bb = b_lane + so, aa = a_lane + so;
+        if (DIAG == 10 && t + PF < nk) issue(t + PF);  // dev: DMA issued ahead of the fragment reads
         if (DIAG != 3 && DIAG != 4 && DIAG != 5) {
         ds_read16<0>(b[0], bb);
         ds_read16<1024>(b[1], bb);
@@ -626,7 +627,7 @@ __global__ __launch_bounds__(C::NT, 2) void gemm_pipe6_kernel(GemmArgs p) {
         ds_read16<7168>(a[7], aa);
         }
         if (t + PF < nk) {
-            issue(t + PF);
+            if (DIAG != 10) issue(t + PF);
             wait_rem(PF - 1);  // own stage t+1 landed; t+2 .. t+PF in flight
         } else {
             wait_rem(max(0, nk - 2 - t));
@@ -649,7 +650,7 @@ __global__ __launch_bounds__(C::NT, 2) void gemm_pipe6_kernel(GemmArgs p) {
     }
     if (STAG && wm == 0) __builtin_amdgcn_s_barrier();
 
-    gemm_epilogue_lds<C, ACT, (DIAG >= 6 ? DIAG - 5 : 0)>(p, lds, acc, m0, n0, wm, wn, g, li, tid);
+    gemm_epilogue_lds<C, ACT, (DIAG >= 6 && DIAG <= 8 ? DIAG - 5 : 0)>(p, lds, acc, m0, n0, wm, wn, g, li, tid);
 }
 
 template <class C, int GROUP_M, int STAG, int DIAG = 0>
@@ -676,7 +677,194 @@ int launch_pipe6(const GemmArgs& a, hipStream_t s) {
     return mme_check_launch("mme_gemm");
 }
 
+// ---------------------------------------------------------------------------
+// pipe7: one wave per SIMD. 256 x 256 tile, 4 waves (2 x 2), each wave a
+// 128 x 128 sub-tile = 8 x 8 accumulators (256 fp32 registers per lane, in the
+// AGPR half of the unified file), 32-deep stages in a 4-deep LDS-DMA ring.
+// Against pipe6's 128 x 64 wave tiles this reads 1/3 fewer LDS bytes per MFMA
+// (16 ds_read_b128 per 64 MFMAs instead of 12 per 32) at the price of no
+// second wave to hide a stall behind, so the single wave software-pipelines
+// itself: fragments of stage t+1 are read into the other register set while
+// stage t's 64 MFMAs run, the DMA pieces of stage t+3 are spread over the
+// first half of the MFMAs. Per stage, per wave:
+//   groups 0-3 (8 MFMAs each): counted lgkmcnt for this group's A fragment,
+//               then PPW/4 DMA pieces of stage t+3 after the group;
+//   mid:        vmcnt for own stage t+1 (two younger stages may stay in
+//               flight), raw s_barrier -> every wave's stage t+1 has landed;
+//   groups 4-7: 4 ds_read_b128 of stage t+1 before each group.
+// WAR: stage t+3 reuses the buffer of stage t-1, read in the second half of
+// iteration t-2 and retired (lgkmcnt) before iteration t-1's first MFMAs,
+// i.e. before every wave's mid barrier of t-1, which the issuing wave passed.
+// Measured (tools/gemm_bench.py variants 50-53, SigLIP shapes): correct but
+// SLOWER than pipe6 -- fc1 900 vs 1160 TF/s, fc2 975 vs 1150. Without the DMA
+// (v52) the same loop reaches 1325 / 1547 TF/s and without the epilogue (v53)
+// 1197 / 1054: with no second wave on the SIMD, every LDS-DMA issue and the
+// whole VALU-heavy epilogue stall the MFMA pipe, which pipe6's ping-pong hides.
+// Kept as the measured alternative (variant 50), not dispatched.
+// ---------------------------------------------------------------------------
+template <class C, int GROUP_M, int ACT, int DIAG = 0>
+__global__ __launch_bounds__(C::NT, 1) void gemm_pipe7_kernel(GemmArgs p) {
+    __shared__ __attribute__((aligned(16))) char lds[C::LDS];
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wm = wave / C::WN, wn = wave % C::WN;
+    const int g = lane >> 4, li = lane & 15;
+    static_assert(C::FN == 8 && C::FM == 8 && C::NW == 4 && C::NSTAGE == 4 && C::PPW == 8, "pipe7 geometry");
+
+    const int nbm = (p.M + C::BM - 1) / C::BM;
+    const int nbn = (p.N + C::BN - 1) / C::BN;
+    const int tile = xcd_remap(blockIdx.x, gridDim.x);
+    int bm, bn;
+    tile_coords<GROUP_M>(tile, nbm, nbn, bm, bn);
+    const int m0 = bm * C::BM, n0 = bn * C::BN;
+
+    const bf16* src[C::PPW];
+    int dst[C::PPW];
+#pragma unroll
+    for (int q = 0; q < C::PPW; ++q) {
+        const int piece = wave * C::PPW + q;
+        const bool isA = piece < C::A_PIECES;
+        const int prow = (isA ? piece : piece - C::A_PIECES) * 16 + (lane >> 2);
+        const int logical = pswz(prow, lane & 3);
+        if (isA)
+            src[q] = p.A + (size_t)min(m0 + prow, p.M - 1) * p.lda + logical * 8;
+        else
+            src[q] = p.B + (size_t)min(n0 + prow, p.N - 1) * p.ldb + logical * 8;
+        dst[q] = piece * 1024;
+    }
+    const int nk = p.K / C::BKS;
+    auto issue2 = [&](int st, int h) {  // pieces 2h, 2h+1 of stage st
+        if (DIAG == 1) return;
+        char* base = lds + (st % C::NSTAGE) * C::STAGE;
+        const int k0 = st * C::BKS;
+        glds16(src[2 * h] + k0, base + dst[2 * h]);
+        glds16(src[2 * h + 1] + k0, base + dst[2 * h + 1]);
+    };
+    const unsigned lds0 = (unsigned)(uintptr_t)(LDS_AS char*)lds;
+    const unsigned b_lane = lds0 + C::A_ST + (wn * C::TN + li) * 64 + (pswz(li, g) << 4);
+    const unsigned a_lane = lds0 + (wm * C::TM + li) * 64 + (pswz(li, g) << 4);
+
+    f32x4 acc[8][8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    bf16x8 xa[8], xb[8], ya[8], yb[8];
+    // fragment reads of stage st, batch r (0..3): b0-3, b4-7, a0-3, a4-7
+    auto rd = [&](bf16x8(&fa)[8], bf16x8(&fb)[8], int st, int r) {
+        const unsigned so = (st % C::NSTAGE) * C::STAGE;
+        const unsigned bb = b_lane + so, aa = a_lane + so;
+        if (r == 0) {
+            ds_read16<0>(fb[0], bb); ds_read16<1024>(fb[1], bb); ds_read16<2048>(fb[2], bb); ds_read16<3072>(fb[3], bb);
+        } else if (r == 1) {
+            ds_read16<4096>(fb[4], bb); ds_read16<5120>(fb[5], bb); ds_read16<6144>(fb[6], bb); ds_read16<7168>(fb[7], bb);
+        } else if (r == 2) {
+            ds_read16<0>(fa[0], aa); ds_read16<1024>(fa[1], aa); ds_read16<2048>(fa[2], aa); ds_read16<3072>(fa[3], aa);
+        } else {
+            ds_read16<4096>(fa[4], aa); ds_read16<5120>(fa[5], aa); ds_read16<6144>(fa[6], aa); ds_read16<7168>(fa[7], aa);
+        }
+    };
+    // MFMAs as inline asm with the accumulator pinned to AGPRs ("+a"): left to itself
+    // hipcc splits the 256 accumulators over VGPRs and AGPRs and shuttles them
+    // (v_accvgpr_write/read around every MFMA). Hazards: an accumulator is rewritten
+    // 64 MFMAs later at the earliest, fragment registers are overwritten a stage
+    // after their last read; the epilogue's reads are padded below.
+    auto mgroup = [&](bf16x8(&fa)[8], bf16x8(&fb)[8], int i) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+            asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(acc[i][j]) : "v"(fb[j]), "v"(fa[i]));
+    };
+    // one stage: MFMAs on (ca, cb) = stage t, reads of stage t+1 into (na, nb)
+    auto step = [&](int t, bf16x8(&ca)[8], bf16x8(&cb)[8], bf16x8(&na)[8], bf16x8(&nb)[8]) {
+        const bool more = t + 3 < nk;
+        lgkm_wait<7>();
+        mgroup(ca, cb, 0);
+        if (more) issue2(t + 3, 0);
+        lgkm_wait<6>();
+        mgroup(ca, cb, 1);
+        if (more) issue2(t + 3, 1);
+        lgkm_wait<5>();
+        mgroup(ca, cb, 2);
+        if (more) issue2(t + 3, 2);
+        lgkm_wait<4>();
+        mgroup(ca, cb, 3);
+        if (more) issue2(t + 3, 3);
+        lgkm_wait<0>();
+        // own stage t+1 landed; t+2 and t+3 (when issued) may stay in flight. Past the
+        // last stage the reads below fetch a stale buffer into the unused register set.
+        if (t + 3 < nk) vm_wait<2 * C::PPW>();
+        else if (t + 2 < nk) vm_wait<C::PPW>();
+        else vm_wait<0>();
+        __builtin_amdgcn_s_barrier();
+        rd(na, nb, t + 1, 0);
+        mgroup(ca, cb, 4);
+        rd(na, nb, t + 1, 1);
+        mgroup(ca, cb, 5);
+        rd(na, nb, t + 1, 2);
+        mgroup(ca, cb, 6);
+        rd(na, nb, t + 1, 3);
+        mgroup(ca, cb, 7);
+    };
+
+    for (int st = 0; st < 3 && st < nk; ++st) {
+        issue2(st, 0); issue2(st, 1); issue2(st, 2); issue2(st, 3);
+    }
+    if (nk >= 3) vm_wait<2 * C::PPW>();
+    else if (nk == 2) vm_wait<C::PPW>();
+    else vm_wait<0>();
+    __builtin_amdgcn_s_barrier();
+    rd(xa, xb, 0, 0); rd(xa, xb, 0, 1); rd(xa, xb, 0, 2); rd(xa, xb, 0, 3);
+    for (int t = 0; t < nk; t += 2) {  // nk is even (K % 64 == 0)
+        step(t, xa, xb, ya, yb);
+        step(t + 1, ya, yb, xa, xb);
+    }
+    // XDL write -> VALU read of the last accumulators: pad, then tie every accumulator
+    // to an asm after the pad so the epilogue's v_accvgpr_reads cannot move above it
+    asm volatile("s_nop 7\n s_nop 7\n s_nop 7\n s_nop 7" ::: "memory");
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) asm volatile("" : "+a"(acc[i][j]));
+    vm_wait<0>();  // the tail's stale-stage DMA must land before the epilogue reuses the LDS
+    if (DIAG == 2) {  // diagnostic: no epilogue (one reduced value per lane keeps the MFMAs live)
+        float sum = 0.f;
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+#pragma unroll
+            for (int j = 0; j < 8; ++j) sum += acc[i][j][0] + acc[i][j][1] + acc[i][j][2] + acc[i][j][3];
+        if (sum == 12345.f) reinterpret_cast<float*>(p.C)[tid] = sum;
+        return;
+    }
+    gemm_epilogue_lds<C, ACT>(p, lds, acc, m0, n0, wm, wn, g, li, tid);
+}
+
+template <class C, int GROUP_M, int DIAG = 0>
+int launch_pipe7(const GemmArgs& a, hipStream_t s) {
+    const int nbm = (a.M + C::BM - 1) / C::BM, nbn = (a.N + C::BN - 1) / C::BN;
+    const dim3 grid(nbm * nbn), block(C::NT);
+    switch (a.act) {
+        case MME_ACT_GELU_TANH:
+            hipLaunchKernelGGL((gemm_pipe7_kernel<C, GROUP_M, MME_ACT_GELU_TANH, DIAG>), grid, block, 0, s, a);
+            break;
+        case MME_ACT_QUICK_GELU:
+            hipLaunchKernelGGL((gemm_pipe7_kernel<C, GROUP_M, MME_ACT_QUICK_GELU, DIAG>), grid, block, 0, s, a);
+            break;
+        case MME_ACT_GELU_ERF:
+            hipLaunchKernelGGL((gemm_pipe7_kernel<C, GROUP_M, MME_ACT_GELU_ERF, DIAG>), grid, block, 0, s, a);
+            break;
+        case MME_ACT_GEGLU_TANH:
+            hipLaunchKernelGGL((gemm_pipe7_kernel<C, GROUP_M, MME_ACT_GEGLU_TANH, DIAG>), grid, block, 0, s, a);
+            break;
+        default:
+            hipLaunchKernelGGL((gemm_pipe7_kernel<C, GROUP_M, MME_ACT_NONE, DIAG>), grid, block, 0, s, a);
+            break;
+    }
+    return mme_check_launch("mme_gemm");
+}
+
 using Pipe256 = PCfg<256, 256, 2, 4>;
+using Pipe256w = PCfg<256, 256, 2, 2>;  // pipe7: 4 waves of 128 x 128
 using Pipe256q = QCfg<256, 256, 2, 4>;
 
 template <class C, int GROUP_M>
@@ -751,6 +939,12 @@ extern "C" int mme_gemm(const void* A, int lda, const void* B, int ldb, void* Cp
         case 38: return launch_pipe6<Pipe256, 4, 1, 6>(a, s);  // diagnostic: epilogue without global stores
         case 39: return launch_pipe6<Pipe256, 4, 1, 7>(a, s);  // diagnostic: no epilogue
         case 44: return launch_pipe6<Pipe256, 4, 1, 8>(a, s);  // dev: plain (temporal) output stores
+        case 45: return launch_pipe6<Pipe256, 4, 1, 10>(a, s);  // dev: DMA before the fragment reads
+        case 46: return launch_pipe6<PCfg<256, 256, 2, 4, 3>, 4, 1>(a, s);  // dev: 3-deep ring (2 stages ahead)
+        case 50: return launch_pipe7<Pipe256w, 4>(a, s);
+        case 51: return launch_pipe7<Pipe256w, 8>(a, s);
+        case 52: return launch_pipe7<Pipe256w, 4, 1>(a, s);  // diagnostic: no DMA
+        case 53: return launch_pipe7<Pipe256w, 4, 2>(a, s);  // diagnostic: no epilogue
         default: break;
     }
     // production dispatch: the pipelined 256x256 kernel whenever its 16-byte

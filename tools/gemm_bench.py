@@ -16,7 +16,7 @@ sys.path.insert(0, os.path.join(ROOT, "multimodal-embedding_amd"))
 import torch  # noqa: E402
 from mme import _lib, ops  # noqa: E402
 
-DIAG_VARIANTS = {22, 23, 26, 27, 33, 34, 35, 36, 37, 38, 39}  # diagnostic builds with deliberately wrong results
+DIAG_VARIANTS = {22, 23, 26, 27, 33, 34, 35, 36, 37, 38, 39, 52, 53}  # diagnostic builds with deliberately wrong results
 SHAPES = {  # name: (N, K)  with M = rows (SigLIP vision: 256 images x 729 tokens)
     "qkv": (3456, 1152), "o_proj": (1152, 1152), "fc1": (4352, 1152), "fc2": (1152, 4352),
     # DFN5B-H / ViT-H (d 1280, I 5120): rows 256 x 730
@@ -31,6 +31,7 @@ def main():
     p.add_argument("--variants", default="")
     p.add_argument("--shapes", default="qkv,o_proj,fc1,fc2")
     p.add_argument("--mx", action="store_true", help="also time the mx8 (block-scaled fp8) GEMM")
+    p.add_argument("--torch", action="store_true", help="also time torch F.linear (hipBLASLt) on each shape")
     p.add_argument("--epi", default="none", help="epilogue: none | bias | res (residual in place) | gelu (bias+gelu_tanh)")
     a = p.parse_args()
     lib = _lib.load()
@@ -76,6 +77,26 @@ def main():
             tf = 2.0 * M * N * K / ms / 1e9
             res[f"{name}/v{v}"] = {"ms": round(ms, 4), "tflops": round(tf, 1)}
             print(f"{name:7s} v{v:<2d} M={M} N={N} K={K} epi={a.epi}: {ms:8.3f} ms  {tf:7.1f} TFLOP/s", flush=True)
+        if a.torch:  # vendor library baseline on the same operands (bias-free X @ W^T)
+            Ct = torch.nn.functional.linear(A, W)
+            err = (Ct.float() - ref.float()).abs().max().item() if (ref is not None and a.epi == "none") else 0.0
+            for _ in range(3):
+                torch.matmul(A, W.t(), out=Ct)
+            torch.cuda.synchronize()
+            s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            ms = 1e30
+            for rep in range(3):
+                s.record()
+                for _ in range(a.iters):
+                    torch.matmul(A, W.t(), out=Ct)
+                e.record()
+                torch.cuda.synchronize()
+                ms = min(ms, s.elapsed_time(e) / a.iters)
+            tf = 2.0 * M * N * K / ms / 1e9
+            res[f"{name}/torch"] = {"ms": round(ms, 4), "tflops": round(tf, 1)}
+            print(f"{name:7s} torch M={M} N={N} K={K}: {ms:8.3f} ms  {tf:7.1f} TFLOP/s  (max |torch - mme| {err:.3g})",
+                  flush=True)
+            del Ct
         if a.mx:
             from mme import mx
             Aq, Wq = mx.quantize(A), mx.quantize(W)
