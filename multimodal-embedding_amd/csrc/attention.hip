@@ -284,8 +284,8 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(AttnArgs a) {
 //     opens tile t (WAR: every wave finished tile t-1 before that barrier;
 //     RAW: each wave retires its own DMA of tile t by a counted vmcnt before it).
 // ---------------------------------------------------------------------------
-template <int HD, int NW, int NSTG, int DIAG = 0>
-__global__ __launch_bounds__(NW * 64) void attn_dma_kernel(AttnArgs a) {
+template <int HD, int NW, int NSTG, int DIAG = 0, int MINW = 1>
+__global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(MINW))) void attn_dma_kernel(AttnArgs a) {
     // DIAG (dev builds, wrong results; tools/attn_bench.py): 1 no K/V DMA, 2 no exp2,
     // 3 no PV MFMA, 4 no QK MFMA, 5 no O rescale, 6 no LDS fragment reads
     constexpr int HDP = HD == 64 ? 64 : 96;
@@ -515,6 +515,287 @@ __global__ __launch_bounds__(NW * 64) void attn_dma_kernel(AttnArgs a) {
     }
 }
 
+// ---------------------------------------------------------------------------
+// attn_pipe_kernel: attn_dma_kernel's per-wave math, software-pipelined across
+// key tiles. attn_dma_kernel runs QK^T(t) -> softmax(t) -> PV(t) as one dependent
+// chain per tile, so with two waves per SIMD the MFMA pipe idles whenever both
+// sit in their softmax (tools/attn_bench.py ablations: latency-bound, no single
+// part > 14 %). Here iteration t computes S(t+1) = K(t+1).Q^T right after the
+// barrier and only then the softmax and PV of tile t, so tile t's VALU work has
+// independent MFMAs beside it. Needs K(t+1) resident one iteration earlier ->
+// 3-deep tile ring (tile t+2 in flight). Also:
+//   * row max / row sum cross-lane steps with v_permlane16/32_swap (VALU) instead
+//     of ds_bpermute round trips through the LDS;
+//   * per-lane fragment addresses computed once; per tile only the ring slot
+//     offset is added (the swizzled V row r ^ 8 commutes with +16 / +32 rows).
+// Ordering: tile t+2 overwrites the slot of tile t-1, whose last reads (PV(t-1))
+// every wave finished before the barrier of iteration t; K(t+1) is read after
+// that barrier, which follows every wave's own vmcnt wait for tile t+1.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ float xmax16(float v) {  // max over lanes l, l^16
+    const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+    return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+}
+__device__ __forceinline__ float xmax32(float v) {  // max over lanes l, l^32
+    const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+    return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+}
+__device__ __forceinline__ float xsum16(float v) {
+    const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+    return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+__device__ __forceinline__ float xsum32(float v) {
+    const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+    return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+
+template <int HD, int NW, int NSTG, bool PIPE, bool ONES, bool LAZY>
+__global__ __launch_bounds__(NW * 64) void attn_pipe_kernel(AttnArgs a) {
+    static_assert(!PIPE || NSTG == 3, "the pipelined loop keeps tile t+1 resident while t+2 lands");
+    static_assert(!ONES || HD == 72, "the ones column lives in the padding of the 80-wide V^T tiles");
+    constexpr int HDP = HD == 64 ? 64 : 96;
+    constexpr int NKS = HDP / 32;
+    constexpr int NCHL = HD / 8;
+    constexpr int NDT = (HD + 15) / 16;
+    constexpr int QW = 32, QB = NW * QW;
+    constexpr int TILE = (2 * NCHL + (ONES ? 1 : 0)) * 1024;  // K planes, V planes (+ a plane of ones)
+    constexpr int NINS = 2 * NCHL;
+    constexpr int MAXI = (NINS + NW - 1) / NW;
+    __shared__ __attribute__((aligned(16))) char lds[NSTG * TILE];
+
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int g = lane >> 4, li = lane & 15;
+    const int nqb = (a.T + QB - 1) / QB;
+    int id;
+    {
+        const int bid = blockIdx.x, nwg = gridDim.x;
+        const int xcd = bid & 7, loc = bid >> 3, q8 = nwg >> 3, r8 = nwg & 7;
+        id = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + loc;
+    }
+    const int qb = id % nqb, h = (id / nqb) % a.H, b = id / (nqb * a.H);
+    const int T = a.T, D = a.H * HD;
+    const bf16* base = a.qkv + (long)b * T * a.ld;
+    const int qw0 = qb * QB + wave * QW;
+    const int Tk = a.seq_lens ? a.seq_lens[b] : T;
+    const float c = a.scale_log2;
+
+    if (ONES) {  // V^T column HD (inside the 80-wide padding) = 1: the PV MFMAs then also sum the weights
+        for (int i = tid; i < NSTG * 64; i += NW * 64)
+            *reinterpret_cast<u16x8*>(lds + (i >> 6) * TILE + 2 * NCHL * 1024 + (i & 63) * 16) =
+                u16x8{0x3F80, 0x3F80, 0x3F80, 0x3F80, 0x3F80, 0x3F80, 0x3F80, 0x3F80};
+    }
+
+    bf16x8 qf[2][NKS];
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+        const bf16* qrow = base + (long)min(qw0 + u * 16 + li, T - 1) * a.ld + h * HD;
+#pragma unroll
+        for (int ks = 0; ks < NKS; ++ks) {
+            const int col = ks * 32 + 8 * g;
+            if (col < HD)
+                qf[u][ks] = *reinterpret_cast<const bf16x8*>(qrow + col);
+            else
+                qf[u][ks] = bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
+        }
+    }
+
+    int nkt = (Tk + 63) / 64;
+    if (a.causal) nkt = min(nkt, (min(T, qb * QB + QB) + 63) / 64);
+
+    const int nmine = (NINS - wave + NW - 1) / NW;
+    auto issue = [&](int t) {
+        char* tb = lds + (t % NSTG) * TILE;
+#pragma unroll
+        for (int i = 0; i < MAXI; ++i) {
+            const int idx = wave + NW * i;
+            if (i < MAXI - 1 || idx < NINS) {
+                const bool isV = idx >= NCHL;
+                const int plane = isV ? idx - NCHL : idx;
+                const int key = isV && (plane & 1) ? lane ^ 8 : lane;
+                const bf16* src = base + (long)min(t * 64 + key, T - 1) * a.ld + (isV ? 2 : 1) * D + h * HD + plane * 8;
+                glds16(src, tb + idx * 1024);
+            }
+        }
+    };
+    auto wait_own = [&](int later) {  // retire own DMA except `later` (0/1) tiles after it
+        if (later == 0) {
+            vm_wait<0>();
+        } else if (nmine == MAXI) {
+            vm_wait<MAXI>();
+        } else {
+            vm_wait<MAXI - 1>();
+        }
+    };
+
+    const unsigned lds0 = (unsigned)(uintptr_t)(LDS_AS char*)lds;
+    unsigned kb[NKS];
+#pragma unroll
+    for (int ks = 0; ks < NKS; ++ks) {
+        const int cch = ks * 4 + g;
+        kb[ks] = lds0 + (cch < NCHL ? cch : 0) * 1024 + li * 16;
+    }
+    unsigned vb[NDT];
+#pragma unroll
+    for (int dt = 0; dt < NDT; ++dt) {
+        int plane = 2 * dt + ((li >> 1) & 1);
+        if (plane >= NCHL) plane = ONES ? NCHL : 0;  // ONES: plane 2*NCHL of the tile (all ones)
+        const int vsw = (plane & 1) ? 8 : 0;
+        vb[dt] = lds0 + (NCHL + plane) * 1024 + (li & 1) * 8 + (((4 * g + (li >> 2)) ^ vsw) * 16);
+    }
+
+    f32x4 o[2][NDT];
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+#pragma unroll
+        for (int i = 0; i < NDT; ++i) o[u][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+    float m[2] = {-1e30f, -1e30f}, lsum[2] = {0.f, 0.f};
+
+    auto qk = [&](int t, f32x4(&sc)[2][4]) {
+        const unsigned so = (t % NSTG) * TILE;
+#pragma unroll
+        for (int kt = 0; kt < 4; ++kt) {
+            bf16x8 kf[NKS];
+#pragma unroll
+            for (int ks = 0; ks < NKS; ++ks)
+                kf[ks] = *reinterpret_cast<const LDS_AS bf16x8*>((uintptr_t)(kb[ks] + so + kt * 256));
+#pragma unroll
+            for (int u = 0; u < 2; ++u) {
+                f32x4 z = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+                for (int ks = 0; ks < NKS; ++ks) z = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf[ks], qf[u][ks], z, 0, 0, 0);
+                sc[u][kt] = z;
+            }
+        }
+        if ((t * 64 + 64 > Tk) || (a.causal && t * 64 + 63 > qw0)) {
+#pragma unroll
+            for (int u = 0; u < 2; ++u) {
+                const int q = qw0 + u * 16 + li;
+                const int lim = a.causal ? min(Tk, q + 1) : Tk;
+#pragma unroll
+                for (int kt = 0; kt < 4; ++kt)
+#pragma unroll
+                    for (int r = 0; r < 4; ++r)
+                        if (t * 64 + kt * 16 + 4 * g + r >= lim) sc[u][kt][r] = -INFINITY;
+            }
+        }
+    };
+    auto softmax_pv = [&](int t, f32x4(&sc)[2][4]) {
+        const unsigned so = (t % NSTG) * TILE;
+        float mnew[2];
+        bool grew = false;
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+            float mloc = fmaxf(fmaxf(sc[u][0][0], sc[u][0][1]), fmaxf(sc[u][0][2], sc[u][0][3]));
+#pragma unroll
+            for (int kt = 1; kt < 4; ++kt)
+                mloc = fmaxf(mloc, fmaxf(fmaxf(sc[u][kt][0], sc[u][kt][1]), fmaxf(sc[u][kt][2], sc[u][kt][3])));
+            mloc = xmax32(xmax16(mloc));
+            mnew[u] = fmaxf(m[u], mloc);
+            grew |= mnew[u] != m[u];
+        }
+        // LAZY: alpha == 1 exactly when no row max of the wave grew -> skip the rescale
+        if (!LAZY || __builtin_amdgcn_ballot_w64(grew)) {
+#pragma unroll
+            for (int u = 0; u < 2; ++u) {
+                const float alpha = __builtin_amdgcn_exp2f((m[u] - mnew[u]) * c);
+                if (!ONES) lsum[u] *= alpha;
+#pragma unroll
+                for (int i = 0; i < NDT; ++i) o[u][i] *= alpha;
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+            m[u] = mnew[u];
+            const float mc = mnew[u] * c;
+            float psum = 0.f;
+#pragma unroll
+            for (int kt = 0; kt < 4; ++kt)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const float pv = __builtin_amdgcn_exp2f(sc[u][kt][r] * c - mc);
+                    sc[u][kt][r] = pv;
+                    if (!ONES) psum += pv;
+                }
+            if (!ONES) lsum[u] += psum;
+        }
+#pragma unroll
+        for (int hh = 0; hh < 2; ++hh) {
+            bf16x8 pb[2];
+#pragma unroll
+            for (int u = 0; u < 2; ++u)
+                pb[u] = __builtin_convertvector(__builtin_shufflevector(sc[u][2 * hh], sc[u][2 * hh + 1], 0, 1, 2, 3,
+                                                                        4, 5, 6, 7), bf16x8);
+#pragma unroll
+            for (int dt = 0; dt < NDT; ++dt) {
+                const unsigned va = vb[dt] + so + hh * 512;
+                const s16x4 v0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS_AS s16x4*)(uintptr_t)va);
+                const s16x4 v1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS_AS s16x4*)(uintptr_t)(va + 256));
+                const bf16x8 vv = __builtin_bit_cast(bf16x8, __builtin_shufflevector(v0, v1, 0, 1, 2, 3, 4, 5, 6, 7));
+#pragma unroll
+                for (int u = 0; u < 2; ++u)
+                    o[u][dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vv, pb[u], o[u][dt], 0, 0, 0);
+            }
+        }
+    };
+
+    f32x4 sA[2][4], sB[2][4];
+    if (PIPE) {
+        // iteration t: [tile t+1 landed, barrier, issue t+2, S(t+1)] then softmax + PV of tile t
+        auto iter = [&](int t, f32x4(&cur)[2][4], f32x4(&nxt)[2][4]) {
+            if (t + 1 < nkt) {
+                wait_own(0);
+                __builtin_amdgcn_s_barrier();
+                if (t + 2 < nkt) issue(t + 2);
+                qk(t + 1, nxt);
+            }
+            softmax_pv(t, cur);
+        };
+        issue(0);
+        if (nkt > 1) issue(1);
+        wait_own(nkt > 1 ? 1 : 0);
+        __builtin_amdgcn_s_barrier();
+        qk(0, sA);
+        for (int t = 0; t < nkt; t += 2) {
+            iter(t, sA, sB);
+            if (t + 1 < nkt) iter(t + 1, sB, sA);
+        }
+    } else {
+        for (int t = 0; t < NSTG - 1 && t < nkt; ++t) issue(t);
+        for (int t = 0; t < nkt; ++t) {
+            wait_own(NSTG == 3 && t + 1 < nkt ? 1 : 0);
+            __builtin_amdgcn_s_barrier();
+            if (t + NSTG - 1 < nkt) issue(t + NSTG - 1);
+            qk(t, sA);
+            softmax_pv(t, sA);
+        }
+    }
+
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+        float ltot;
+        if (ONES)  // the weight sums sit in O^T row HD = 64 + 4*2 + 0: lanes 32..47, element 0
+            ltot = __shfl(o[u][NDT - 1][0], 32 + li, 64);
+        else
+            ltot = xsum32(xsum16(lsum[u]));
+        const float inv = 1.0f / ltot;
+        const int q = qw0 + u * 16 + li;
+        if (q < T) {
+            bf16* orow = a.out + ((long)b * T + q) * a.ldo + h * HD;
+#pragma unroll
+            for (int dt = 0; dt < NDT; ++dt) {
+                const int d0 = dt * 16 + 4 * g;
+                if (d0 < HD) {
+                    bf16x4 v;
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) v[r] = f2bf(o[u][dt][r] * inv);
+                    *reinterpret_cast<bf16x4*>(orow + d0) = v;
+                }
+            }
+        }
+    }
+}
+
 // SigLIP MAP head: one probe query per head, keys = the T tokens of image b.
 constexpr int PROBE_MAXT = 1024;
 __global__ __launch_bounds__(256) void probe_attn_kernel(const bf16* __restrict__ qv, const bf16* __restrict__ kv,
@@ -589,6 +870,24 @@ void launch_attn(int kind, const AttnArgs& a, int B, int T, int H, hipStream_t s
         hipLaunchKernelGGL((attn_dma_kernel<HD, 8, 3>), dim3(cdiv(T, 256) * H * B), dim3(512), 0, st, a);
     else if (kind == 5)
         hipLaunchKernelGGL((attn_dma_kernel<HD, 4, 3>), dim3(cdiv(T, 128) * H * B), dim3(256), 0, st, a);
+    else if (kind == 6)  // dev: 8 waves, register budget for 4 waves / SIMD (2 blocks per CU)
+        hipLaunchKernelGGL((attn_dma_kernel<HD, 8, 2, 0, 4>), dim3(cdiv(T, 256) * H * B), dim3(512), 0, st, a);
+    else if (kind == 7)  // dev: 4 waves, 4 waves / SIMD
+        hipLaunchKernelGGL((attn_dma_kernel<HD, 4, 2, 0, 4>), dim3(cdiv(T, 128) * H * B), dim3(256), 0, st, a);
+    else if (kind == 8)  // dev: pipelined QK(t+1) under softmax(t)
+        hipLaunchKernelGGL((attn_pipe_kernel<HD, 8, 3, true, false, false>), dim3(cdiv(T, 256) * H * B), dim3(512), 0, st, a);
+    else if (kind == 9)  // dev: lean per-tile VALU (lane-base addresses, permlane reductions)
+        hipLaunchKernelGGL((attn_pipe_kernel<HD, 8, 2, false, false, false>), dim3(cdiv(T, 256) * H * B), dim3(512), 0, st, a);
+    else if (kind == 10)  // dev: + lazy rescale
+        hipLaunchKernelGGL((attn_pipe_kernel<HD, 8, 2, false, false, true>), dim3(cdiv(T, 256) * H * B), dim3(512), 0, st, a);
+    else if (kind == 11)  // dev: + ones column (HD 72 only)
+        hipLaunchKernelGGL((attn_pipe_kernel<HD, 8, 2, false, HD == 72, true>), dim3(cdiv(T, 256) * H * B), dim3(512), 0, st, a);
+    else if (kind == 13)  // dev: lean + lazy (+ ones), 2 waves = 64 queries per block (text towers)
+        hipLaunchKernelGGL((attn_pipe_kernel<HD, 2, 2, false, HD == 72, true>), dim3(cdiv(T, 64) * H * B), dim3(128), 0, st, a);
+    else if (kind == 14)  // dev: lean + lazy (+ ones), 4 waves = 128 queries per block
+        hipLaunchKernelGGL((attn_pipe_kernel<HD, 4, 2, false, HD == 72, true>), dim3(cdiv(T, 128) * H * B), dim3(256), 0, st, a);
+    else if (kind == 12)  // dev: pipelined + lazy + ones
+        hipLaunchKernelGGL((attn_pipe_kernel<HD, 8, 3, true, HD == 72, true>), dim3(cdiv(T, 256) * H * B), dim3(512), 0, st, a);
     else
         hipLaunchKernelGGL((attn_dma_kernel<HD, 8, 2>), dim3(cdiv(T, 256) * H * B), dim3(512), 0, st, a);
 }
@@ -618,8 +917,11 @@ extern "C" int mme_attention(const void* qkv, int ld_qkv, void* out, int ld_out,
     // LDS-DMA staging, 8 waves (256 queries) per block unless that pads the query range by
     // > 10 % more than 128-query blocks (T = 257), then 4 waves. SigLIP-400M vision
     // (T 729, hd 72): 1.80 -> 1.27 ms per 256-image layer; ViT-H (T 257, hd 80): 0.40 -> 0.355.
+    // The LDS-DMA kernels run as attn_pipe_kernel's lean non-pipelined form (kinds 11 / 14:
+    // lane-base fragment addresses, permlane reductions, lazy rescale, and for hd 72 the
+    // weight sums from a ones column of V^T): SigLIP vision 1.27-1.33 -> 1.16-1.17 ms.
     int kind = (T <= 128 || hd == 64) ? 0
-               : ((long)cdiv(T, 256) * 256 * 10 <= (long)cdiv(T, 128) * 128 * 11 ? 2 : 1);
+               : ((long)cdiv(T, 256) * 256 * 10 <= (long)cdiv(T, 128) * 128 * 11 ? 11 : 14);
     if (g_attn_variant >= 1 && g_attn_variant <= 4 && hd == 72) {  // dev-only diagnostic builds
         const dim3 grid(cdiv(T, 128) * H * B);
         switch (g_attn_variant) {
@@ -630,7 +932,8 @@ extern "C" int mme_attention(const void* qkv, int ld_qkv, void* out, int ld_out,
         }
         return mme_check_launch("mme_attention");
     }
-    if (g_attn_variant >= 9 && g_attn_variant <= 14) kind = g_attn_variant - 9;  // dev: force a kernel
+    if (g_attn_variant >= 9 && g_attn_variant <= 16) kind = g_attn_variant - 9;  // dev: force a kernel
+    if (g_attn_variant >= 30 && g_attn_variant <= 45) kind = g_attn_variant - 30;  // dev: force a kernel
     if (g_attn_variant >= 21 && g_attn_variant <= 26 && hd == 72) {  // dev: attn_dma_kernel<72,8,2> diagnostics
         const dim3 grid(cdiv(T, 256) * H * B), blk(512);
         hipStream_t st = as_stream(stream);
