@@ -136,8 +136,13 @@ template <class C, int ACT, int EDIAG = 0>
 __device__ __forceinline__ void gemm_epilogue_lds(const GemmArgs& p, char* lds, f32x4 (&acc)[C::FM][C::FN], int m0,
                                                   int n0, int wm, int wn, int g, int li, int tid) {
     // EDIAG (dev builds, wrong results): 1 = no global stores, 2 = no epilogue at all
-    if (EDIAG == 2) {
-        if (tid == 0 && m0 < 0) reinterpret_cast<float*>(p.C)[0] = acc[0][0][0];
+    if (EDIAG == 2) {  // one reduced value per lane keeps every MFMA live
+        float sum = 0.f;
+#pragma unroll
+        for (int i = 0; i < C::FM; ++i)
+#pragma unroll
+            for (int j = 0; j < C::FN; ++j) sum += acc[i][j][0] + acc[i][j][1] + acc[i][j][2] + acc[i][j][3];
+        if (sum == 12345.f) reinterpret_cast<float*>(p.C)[tid] = sum;
         return;
     }
     // GeGLU (MME_ACT_GEGLU_TANH): B rows are [gate 4k..4k+3, up 4k..4k+3] per group of 8,
@@ -545,7 +550,7 @@ __device__ __forceinline__ void pipe6_tile(const GemmArgs& p, char* lds, const i
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int wm = wave / C::WN, wn = wave % C::WN;
     const int g = lane >> 4, li = lane & 15;
-    static_assert(C::FN == 4 && C::FM == 8 && C::NW == 8, "pipe6 geometry: 8 waves of 128 x 64");
+    static_assert((C::FN == 4 || C::FN == 6) && C::FM == 8 && C::NW == 8, "pipe6 geometry: 8 waves of 128 x 64|96");
     constexpr int PF = C::NSTAGE - 1;  // stages issued ahead of the one being read
     static_assert(PF >= 2 && PF <= 4, "pipe6 is written for 3- to 5-deep rings");
     // ping-pong partners: waves w and w + 4 share a SIMD; the upper half runs one barrier behind
@@ -583,7 +588,7 @@ __device__ __forceinline__ void pipe6_tile(const GemmArgs& p, char* lds, const i
 #pragma unroll
         for (int j = 0; j < C::FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-    bf16x8 b[4], a[8];
+    bf16x8 b[C::FN], a[8];
     const int nk = p.K / C::BKS;
 
     // own DMA of stage s retired while `rem` later stages may stay in flight
@@ -608,6 +613,10 @@ __device__ __forceinline__ void pipe6_tile(const GemmArgs& p, char* lds, const i
         ds_read16<1024>(b[1], bb);
         ds_read16<2048>(b[2], bb);
         ds_read16<3072>(b[3], bb);
+        if constexpr (C::FN == 6) {
+            ds_read16<4096>(b[4], bb);
+            ds_read16<5120>(b[5], bb);
+        }
         ds_read16<0>(a[0], aa);
         ds_read16<1024>(a[1], aa);
         ds_read16<2048>(a[2], aa);
@@ -630,7 +639,7 @@ __device__ __forceinline__ void pipe6_tile(const GemmArgs& p, char* lds, const i
 #pragma unroll
         for (int i = 0; i < 8; ++i)
 #pragma unroll
-            for (int j = 0; j < 4; ++j)
+            for (int j = 0; j < C::FN; ++j)
                 if (DIAG == 2 || DIAG == 4 || DIAG == 5)
                     asm volatile("" ::"v"(b[j]), "v"(a[i]));
                 else
