@@ -544,6 +544,80 @@ int launch_pipe4(const GemmArgs& a, hipStream_t s) {
 // (lgkmcnt(0)) before that phase's closing barrier -> WAR safe.
 // ---------------------------------------------------------------------------
 // One 256 x 256 (or, for the split grid below, 512 x 128) output tile of pipe6.
+// Epilogue without LDS staging. Per 16 x 16 accumulator a lane owns 4 consecutive
+// columns of one row; lane groups g and g^1 (lanes l, l^16) trade halves with
+// v_permlane16_swap so every lane then holds 8 consecutive columns (even g: tile j0,
+// odd g: tile j0 + 1), and one wave instruction stores 16 rows x 64 contiguous bytes
+// as 16-B non-temporal stores -- the same instruction count as the LDS-staged path,
+// without its LDS round trip and barriers. Residual rows are loaded in the same
+// layout first (the fragment registers are free by then). GeGLU: the 8 columns are
+// [gate x4, up x4] of one interleave group -> 4 outputs, an 8-byte store.
+template <class C, int ACT>
+__device__ __forceinline__ void gemm_epilogue_direct(const GemmArgs& p, f32x4 (&acc)[C::FM][C::FN], int m0, int n0,
+                                                     int wm, int wn, int g, int li) {
+    static_assert(C::FN % 2 == 0, "tiles pair up across lane groups");
+    constexpr bool GLU = ACT == MME_ACT_GEGLU_TANH;
+    constexpr int RACT = GLU ? MME_ACT_NONE : ACT;
+    bf16* Cout = reinterpret_cast<bf16*>(p.C);
+    const bool odd = g & 1;
+    const int rbase = m0 + wm * C::TM + li;
+    auto col8 = [&](int jp) { return n0 + wn * C::TN + (jp + (odd ? 1 : 0)) * 16 + 4 * (g & 2); };
+    u16x8 rv[C::FM][C::FN / 2];
+    if (!GLU && p.res) {
+#pragma unroll
+        for (int i = 0; i < C::FM; ++i) {
+            const int gr = min(rbase + i * 16, p.M - 1);
+            const int rr = p.res_period ? gr % p.res_period : gr;
+#pragma unroll
+            for (int jp = 0; jp < C::FN; jp += 2)
+                rv[i][jp / 2] = *reinterpret_cast<const u16x8*>(p.res + (size_t)rr * p.ldr + min(col8(jp), p.N - 8));
+        }
+    }
+#pragma unroll
+    for (int jp = 0; jp < C::FN; jp += 2) {
+        float bv[2][4];
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const int c4 = n0 + wn * C::TN + (jp + h) * 16 + 4 * g;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) bv[h][r] = p.bias ? bf2f(p.bias[min(c4 + r, p.N - 1)]) : 0.f;
+        }
+        const int gc = col8(jp);
+#pragma unroll
+        for (int i = 0; i < C::FM; ++i) {
+            const int gr = rbase + i * 16;
+            bf16x4 o0, o1;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                o0[r] = f2bf(apply_act(acc[i][jp][r] + bv[0][r], RACT));
+                o1[r] = f2bf(apply_act(acc[i][jp + 1][r] + bv[1][r], RACT));
+            }
+            const auto x = __builtin_bit_cast(uint2, o0), y = __builtin_bit_cast(uint2, o1);
+            const auto s0 = __builtin_amdgcn_permlane16_swap(x.x, y.x, false, false);
+            const auto s1 = __builtin_amdgcn_permlane16_swap(x.y, y.y, false, false);
+            // even g: (own tile jp, partner tile jp); odd g: (partner tile jp+1, own tile jp+1)
+            const u16x8 v = __builtin_bit_cast(u16x8, uint4{s0[0], s1[0], s0[1], s1[1]});
+            if (gr >= p.M || gc >= p.N) continue;
+            if (GLU) {
+                u16x4 o;
+#pragma unroll
+                for (int e = 0; e < 4; ++e)
+                    o[e] = __builtin_bit_cast(unsigned short,
+                                              f2bf(bf2f(f2bf(apply_act(bits2f(v[e]), MME_ACT_GELU_TANH))) * bits2f(v[4 + e])));
+                __builtin_nontemporal_store(o, reinterpret_cast<u16x4*>(Cout + (size_t)gr * p.ldc + gc / 2));
+            } else if (p.res) {
+                u16x8 o;
+#pragma unroll
+                for (int e = 0; e < 8; ++e)
+                    o[e] = __builtin_bit_cast(unsigned short, f2bf(bits2f(v[e]) + bits2f(rv[i][jp / 2][e])));
+                __builtin_nontemporal_store(o, reinterpret_cast<u16x8*>(Cout + (size_t)gr * p.ldc + gc));
+            } else {
+                __builtin_nontemporal_store(v, reinterpret_cast<u16x8*>(Cout + (size_t)gr * p.ldc + gc));
+            }
+        }
+    }
+}
+
 template <class C, int ACT, int STAG, int DIAG>
 __device__ __forceinline__ void pipe6_tile(const GemmArgs& p, char* lds, const int m0, const int n0) {
     const int tid = threadIdx.x, lane = tid & 63;
@@ -650,7 +724,10 @@ __device__ __forceinline__ void pipe6_tile(const GemmArgs& p, char* lds, const i
     }
     if (STAG && !late) __builtin_amdgcn_s_barrier();
 
-    gemm_epilogue_lds<C, ACT, (DIAG >= 6 && DIAG <= 8 ? DIAG - 5 : 0)>(p, lds, acc, m0, n0, wm, wn, g, li, tid);
+    if constexpr (DIAG == 11)
+        gemm_epilogue_direct<C, ACT>(p, acc, m0, n0, wm, wn, g, li);
+    else
+        gemm_epilogue_lds<C, ACT, (DIAG >= 6 && DIAG <= 8 ? DIAG - 5 : 0)>(p, lds, acc, m0, n0, wm, wn, g, li, tid);
 }
 
 // Split grid for N = 256 k + 128 (SigLIP: o_proj / fc2 N = 1152, QKV N = 3456): the
@@ -991,6 +1068,9 @@ extern "C" int mme_gemm(const void* A, int lda, const void* B, int ldb, void* Cp
         case 39: return launch_pipe6<Pipe256, 4, 1, 7>(a, s);  // diagnostic: no epilogue
         case 44: return launch_pipe6<Pipe256, 4, 1, 8>(a, s);  // dev: plain (temporal) output stores
         case 45: return launch_pipe6<Pipe256, 4, 1, 10>(a, s);  // dev: DMA before the fragment reads
+        case 49:  // dev: epilogue stored straight from the accumulators (no LDS staging)
+            if (a.N % 256 == 128) return launch_pipe6<Pipe256, 4, 1, 11, true>(a, s);
+            return launch_pipe6<Pipe256, 4, 1, 11>(a, s);
         case 47:  // split grid (512 x 128 tiles for the last 128 columns) where N = 256 k + 128
             if (a.N % 256 == 128) return launch_pipe6<Pipe256, 4, 1, 0, true>(a, s);
             return launch_pipe6<Pipe256, 4, 1>(a, s);
