@@ -35,7 +35,7 @@ extern "C" {
 #define MME_ERR_HIP 2         /* HIP runtime error at launch               */
 #define MME_ERR_UNSUPPORTED 3 /* valid request this build does not handle  */
 
-#define MME_ABI_VERSION 3
+#define MME_ABI_VERSION 4
 
 /* activation codes for mme_gemm (HF config.hidden_act) */
 #define MME_ACT_NONE 0
@@ -90,6 +90,23 @@ int mme_im2col(const void* pixels, int in_is_f32, int n, int S, int patch, int k
 int mme_gemm(const void* A, int lda, const void* B, int ldb, void* C, int ldc, int M, int N, int K,
              const void* bias, const void* residual, int ldr, int res_period, int act, int out_f32,
              void* stream);
+
+/* GEMM with the preceding LayerNorm folded into the weights: for
+ * LN(x) = (x - mean) * rstd * gamma + beta feeding nn.Linear(W, b),
+ *   C[r, n] = act( rstd_r * (A[r,:] . B[n,:] - mean_r * col_sum[n]) + bias_f32[n] )
+ * with A = x (the un-normalised residual stream), B = bf16(W * gamma) (per input
+ * column), col_sum[n] = sum_k B[n, k] (fp32) and bias_f32 = b + W . beta (fp32);
+ * row_stats = [M][2] (mean, rstd) from mme_rowstats. Replaces the
+ * LayerNorm -> Linear pairs of SiglipEncoderLayer / CLIPEncoderLayer
+ * (TF:models/siglip/modeling_siglip.py:341-357, layer_norm1 -> q/k/v_proj and
+ * layer_norm2 -> mlp.fc1) without writing the normalised rows. act: NONE .. GELU_ERF;
+ * bf16 out; same shape rules as mme_gemm. */
+int mme_gemm_lnfold(const void* A, int lda, const void* B, int ldb, void* C, int ldc, int M, int N, int K,
+                    const float* row_stats, const float* col_sum, const float* bias_f32, int act, void* stream);
+
+/* LayerNorm statistics per row: stats[2r] = mean, stats[2r+1] = rsqrt(var + eps)
+ * (fp32, biased variance; the arithmetic of mme_layernorm) for mme_gemm_lnfold. */
+int mme_rowstats(const void* x, int ldx, int rows, int d, float eps, float* stats, void* stream);
 
 /* LayerNorm over the last dim (fp32 statistics), bf16 in/out.
  * y[r] = (x[r]-mean)*rsqrt(var+eps)*gamma + beta. Replaces nn.LayerNorm

@@ -36,6 +36,10 @@ struct GemmArgs {
     int M, N, K;
     int res_period, act, out_f32;
     int stagger;  // dev: s_sleep(127) units per phase step for the first wave of blocks (0 = off)
+    // LayerNorm folded into the weights (mme_gemm_lnfold): out = act(rstd_r * (acc - mean_r * cs_n) + b_n)
+    const float* ln_stats;  // [M][2] (mean, rstd) of the A rows, or null
+    const float* ln_cs;     // [N] column sums of the folded weight
+    const float* ln_b;      // [N] folded bias (fp32)
 };
 
 template <class C, int GROUP_M>
@@ -61,14 +65,17 @@ __global__ __launch_bounds__(C::NT) void gemm_tn_kernel(GemmArgs p) {
     for (int j = 0; j < C::FN; ++j) {
         const int col = n0 + wn * C::TN + j * 16 + (lane & 15);
         if (col >= p.N) continue;
-        const float bv = p.bias ? bf2f(p.bias[col]) : 0.f;
+        const float bv = p.ln_stats ? p.ln_b[col] : p.bias ? bf2f(p.bias[col]) : 0.f;
+        const float cs = p.ln_stats ? p.ln_cs[col] : 0.f;
 #pragma unroll
         for (int i = 0; i < C::FM; ++i) {
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
                 const int row = m0 + wm * C::TM + i * 16 + 4 * (lane >> 4) + r;
                 if (row >= p.M) continue;
-                float v = apply_act(acc[i][j][r] + bv, p.act);
+                float a = acc[i][j][r];
+                if (p.ln_stats) a = p.ln_stats[2 * row + 1] * (a - p.ln_stats[2 * row] * cs);
+                float v = apply_act(a + bv, p.act);
                 if (p.res) {
                     const int rr = p.res_period ? row % p.res_period : row;
                     v += bf2f(p.res[(size_t)rr * p.ldr + col]);
@@ -168,11 +175,28 @@ __device__ __forceinline__ void gemm_epilogue_lds(const GemmArgs& p, char* lds, 
         }
     }
     __syncthreads();
+    // folded LayerNorm: per row (scale, shift) = (rstd, -rstd * mean), per column (cs, b)
+    float lr[C::FM], lm[C::FM];
+    if (p.ln_stats) {
+#pragma unroll
+        for (int i = 0; i < C::FM; ++i) {
+            const int gr = min(m0 + wm * C::TM + i * 16 + li, p.M - 1);
+            const float2 st = *reinterpret_cast<const float2*>(p.ln_stats + 2 * gr);
+            lr[i] = st.y;
+            lm[i] = -st.y * st.x;
+        }
+    }
 #pragma unroll
     for (int j = 0; j < C::FN; ++j) {
         const int nl = wn * C::TN + j * 16 + 4 * g;
-        float bv[4] = {0.f, 0.f, 0.f, 0.f};
-        if (p.bias) {
+        float bv[4] = {0.f, 0.f, 0.f, 0.f}, cs[4] = {0.f, 0.f, 0.f, 0.f};
+        if (p.ln_stats) {  // 4 consecutive columns: one 16-B load each (N % 8 == 0 on this path)
+            const int c4 = min(n0 + nl, p.N - 4);
+            const float4 b4 = *reinterpret_cast<const float4*>(p.ln_b + c4);
+            const float4 s4 = *reinterpret_cast<const float4*>(p.ln_cs + c4);
+            bv[0] = b4.x, bv[1] = b4.y, bv[2] = b4.z, bv[3] = b4.w;
+            cs[0] = s4.x, cs[1] = s4.y, cs[2] = s4.z, cs[3] = s4.w;
+        } else if (p.bias) {
 #pragma unroll
             for (int r = 0; r < 4; ++r) bv[r] = bf2f(p.bias[min(n0 + nl + r, p.N - 1)]);
         }
@@ -180,8 +204,14 @@ __device__ __forceinline__ void gemm_epilogue_lds(const GemmArgs& p, char* lds, 
         for (int i = 0; i < C::FM; ++i) {
             const int ml = wm * C::TM + i * 16 + li;
             bf16x4 o;
+            if (p.ln_stats) {
 #pragma unroll
-            for (int r = 0; r < 4; ++r) o[r] = f2bf(apply_act(acc[i][j][r] + bv[r], RACT));
+                for (int r = 0; r < 4; ++r)
+                    o[r] = f2bf(apply_act(fmaf(lr[i], acc[i][j][r], fmaf(lm[i], cs[r], bv[r])), RACT));
+            } else {
+#pragma unroll
+                for (int r = 0; r < 4; ++r) o[r] = f2bf(apply_act(acc[i][j][r] + bv[r], RACT));
+            }
             *reinterpret_cast<bf16x4*>(lds + ml * C::OUT_LD + nl * 2) = o;
         }
     }
@@ -1007,6 +1037,7 @@ using SqCfg = Cfg<256, 256, 2, 4>;
 using SmallCfg = Cfg<128, 128, 2, 2>;
 
 int g_variant = -1;  // dev-only override (tools/gemm_bench.py)
+int gemm_dispatch(GemmArgs a, hipStream_t s);
 
 }  // namespace
 
@@ -1029,8 +1060,33 @@ extern "C" int mme_gemm(const void* A, int lda, const void* B, int ldb, void* Cp
     MME_REQUIRE(!residual || ldr >= N, "mme_gemm: ldr < N");
     MME_REQUIRE(res_period >= 0, "mme_gemm: res_period < 0");
     GemmArgs a{(const bf16*)A, (const bf16*)B, Cp, (const bf16*)bias, (const bf16*)residual,
-               lda, ldb, ldc, ldr, M, N, K, res_period, act, out_f32, 0};
-    hipStream_t s = as_stream(stream);
+               lda, ldb, ldc, ldr, M, N, K, res_period, act, out_f32, 0, nullptr, nullptr, nullptr};
+    return gemm_dispatch(a, as_stream(stream));
+}
+
+extern "C" int mme_gemm_lnfold(const void* A, int lda, const void* B, int ldb, void* Cp, int ldc, int M, int N,
+                               int K, const float* row_stats, const float* col_sum, const float* bias_f32, int act,
+                               void* stream) {
+    MME_REQUIRE(A && B && Cp && row_stats && col_sum && bias_f32, "mme_gemm_lnfold: null operand");
+    MME_REQUIRE(M > 0 && N > 0 && K > 0, "mme_gemm_lnfold: empty shape M=%d N=%d K=%d", M, N, K);
+    MME_REQUIRE(K % BK == 0, "mme_gemm_lnfold: K=%d must be a multiple of %d", K, BK);
+    MME_REQUIRE(lda % 8 == 0 && ldb % 8 == 0 && lda >= K && ldb >= K && ldc >= N, "mme_gemm_lnfold: bad leading dims");
+    MME_REQUIRE(act >= MME_ACT_NONE && act <= MME_ACT_GELU_ERF, "mme_gemm_lnfold: bad act %d", act);
+    MME_REQUIRE(((uintptr_t)A & 15) == 0 && ((uintptr_t)B & 15) == 0, "mme_gemm_lnfold: A/B must be 16-byte aligned");
+    MME_REQUIRE(((uintptr_t)col_sum & 15) == 0 && ((uintptr_t)bias_f32 & 15) == 0 && ((uintptr_t)row_stats & 7) == 0,
+                "mme_gemm_lnfold: col_sum / bias_f32 must be 16-byte and row_stats 8-byte aligned");
+    GemmArgs a{(const bf16*)A, (const bf16*)B, Cp, nullptr, nullptr, lda, ldb, ldc, 0, M, N, K, 0, act, 0, 0,
+               row_stats, col_sum, bias_f32};
+    return gemm_dispatch(a, as_stream(stream));
+}
+
+namespace {
+int gemm_dispatch(GemmArgs a, hipStream_t s) {
+    const int M = a.M, N = a.N, K = a.K, ldc = a.ldc, ldr = a.ldr, act = a.act, out_f32 = a.out_f32;
+    const void* Cp = a.C;
+    const void* residual = a.res;
+    (void)K;
+    const bool glu = act == MME_ACT_GEGLU_TANH;
     if (g_variant >= 40 && g_variant <= 43) {  // dev: pipe6 with the first block wave de-phased by
         a.stagger = (g_variant - 39) * (K / 32) / 12;  // (variant-39)/4 of a tile per phase step
         return launch_pipe6<Pipe256, 4, 1>(a, s);
@@ -1093,3 +1149,4 @@ extern "C" int mme_gemm(const void* A, int lda, const void* B, int ldb, void* Cp
     if ((long)M * N >= 2048L * 1024) return launch<BigCfg, 1>(a, s);
     return launch<SmallCfg, 8>(a, s);
 }
+}  // namespace

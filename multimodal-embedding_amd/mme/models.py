@@ -14,6 +14,7 @@ TF:models/clip/modeling_clip.py:494-656.
 """
 from __future__ import annotations
 
+import os
 from typing import List, Optional, Sequence, Tuple
 
 import torch
@@ -23,6 +24,9 @@ from .config import ACTS, ModelSpec, TowerConfig, get_spec
 from .weights import LayerW, ModelW, TextW, VisionW, from_hf_state_dict, random_state_dict
 
 BF16 = torch.bfloat16
+# LayerNorm -> Linear pairs run as mme_rowstats + mme_gemm_lnfold (the normalised rows are
+# never written); MME_LN_FOLD=0 restores mme_layernorm + mme_gemm
+LN_FOLD = os.environ.get("MME_LN_FOLD", "1") != "0"
 
 
 class _Bufs:
@@ -37,6 +41,7 @@ class _Bufs:
         # fp8 mode: mx8 LayerNorm output and mx8 MLP hidden (fc1 -> fc2 operand)
         self.hq = mx.MXTensor.empty(rows, d, device) if fp8 else None
         self.midq = mx.MXTensor.empty(rows, cfg.inter_pad, device) if fp8 else None
+        self.stats = torch.empty(rows, 2, dtype=torch.float32, device=device)
 
 
 def encoder_layer(x: torch.Tensor, L: LayerW, cfg: TowerConfig, B: int, T: int, bufs: _Bufs, *,
@@ -54,12 +59,23 @@ def encoder_layer(x: torch.Tensor, L: LayerW, cfg: TowerConfig, B: int, T: int, 
         midq = mx.gemm(hq, L.mx.fc1, L.fc1_b, act=act, out_mx=bufs.midq, algo_flops=mlp_flops)
         mx.gemm(midq, L.mx.fc2, L.fc2_b, residual=x, out=x, algo_flops=mlp_flops)
         return
+    mlp_flops = 2.0 * x.shape[0] * d * cfg.intermediate  # unpadded intermediate width
+    if LN_FOLD:  # layer_norm1 -> qkv and layer_norm2 -> fc1 folded (mme.h mme_gemm_lnfold)
+        if L.fold is None:
+            L.fold = (ops.LNFolded(L.qkv_w, L.qkv_b, L.ln1_g, L.ln1_b), ops.LNFolded(L.fc1_w, L.fc1_b, L.ln2_g, L.ln2_b))
+        st = ops.rowstats(x, cfg.eps, d=d, out=bufs.stats)
+        qkv = ops.gemm_lnfold(x, L.fold[0], st, out=bufs.wide[:, : 3 * d])
+        a = ops.attention(qkv, B, T, H, hd, seq_lens=seq_lens, causal=causal, out=bufs.h)
+        ops.gemm(a, L.o_w, L.o_b, residual=x, out=x)
+        st = ops.rowstats(x, cfg.eps, d=d, out=bufs.stats)
+        mid = ops.gemm_lnfold(x, L.fold[1], st, act=act, out=bufs.wide[:, : cfg.inter_pad], algo_flops=mlp_flops)
+        ops.gemm(mid, L.fc2_w, L.fc2_b, residual=x, out=x, algo_flops=mlp_flops)
+        return
     h = ops.layernorm(x, L.ln1_g, L.ln1_b, cfg.eps, out=bufs.h)
     qkv = ops.gemm(h, L.qkv_w, L.qkv_b, out=bufs.wide[:, : 3 * d])
     a = ops.attention(qkv, B, T, H, hd, seq_lens=seq_lens, causal=causal, out=bufs.h)
     ops.gemm(a, L.o_w, L.o_b, residual=x, out=x)
     h = ops.layernorm(x, L.ln2_g, L.ln2_b, cfg.eps, out=bufs.h)
-    mlp_flops = 2.0 * x.shape[0] * d * cfg.intermediate  # unpadded intermediate width
     mid = ops.gemm(h, L.fc1_w, L.fc1_b, act=act, out=bufs.wide[:, : cfg.inter_pad], algo_flops=mlp_flops)
     ops.gemm(mid, L.fc2_w, L.fc2_b, residual=x, out=x, algo_flops=mlp_flops)
 

@@ -137,6 +137,59 @@ def gemm(a: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None, 
     return out
 
 
+def rowstats(x: torch.Tensor, eps: float, *, d: Optional[int] = None,
+             out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """LayerNorm statistics [rows, 2] fp32 = (mean, rsqrt(var + eps)) over the first d columns."""
+    _dev(x, out)
+    rows = x.shape[0]
+    d = d or x.shape[1]
+    if out is None:
+        out = torch.empty(rows, 2, dtype=torch.float32, device=x.device)
+    if out.dtype != torch.float32 or not out.is_contiguous() or out.numel() < 2 * rows:
+        raise ValueError("rowstats: out must be contiguous fp32 [rows, 2]")
+    call("mme_rowstats", x.data_ptr(), _rowmajor(x, "x"), rows, d, float(eps), out.data_ptr(), _stream())
+    return out
+
+
+def gemm_lnfold(x: torch.Tensor, folded: "LNFolded", stats: torch.Tensor, *, act: int = _lib.ACT_NONE,
+                out: Optional[torch.Tensor] = None, algo_flops: Optional[float] = None) -> torch.Tensor:
+    """act(LayerNorm(x) @ W.T + b) with the LayerNorm folded into the weights (mme_gemm_lnfold):
+    x is the raw residual stream, stats its rowstats()."""
+    _dev(x, folded.w, stats, out)
+    M, K = x.shape
+    N = folded.w.shape[0]
+    if folded.w.shape[1] != K or stats.shape[0] < M:
+        raise ValueError(f"gemm_lnfold: x {tuple(x.shape)} vs w {tuple(folded.w.shape)} / stats {tuple(stats.shape)}")
+    if out is None:
+        out = torch.empty(M, N, dtype=BF16, device=x.device)
+    ev = KernelTimer.begin()
+    call("mme_gemm_lnfold", x.data_ptr(), _rowmajor(x, "x"), folded.w.data_ptr(), _rowmajor(folded.w, "w"),
+         out.data_ptr(), _rowmajor(out, "out"), M, N, K, stats.data_ptr(), folded.cs.data_ptr(),
+         folded.b.data_ptr(), act, _stream())
+    KernelTimer.end(ev, "gemm", algo_flops if algo_flops is not None else 2.0 * M * N * K,
+                    2.0 * (M * K + N * K + M * N))
+    return out
+
+
+class LNFolded:
+    """nn.LayerNorm(gamma, beta) followed by nn.Linear(w, bias), folded for mme_gemm_lnfold:
+    w' = bf16(w * gamma) (per input column), cs = sum_k w'[n, k] (fp32), b' = bias + w . beta (fp32)."""
+
+    def __init__(self, w: torch.Tensor, bias: Optional[torch.Tensor], gamma: torch.Tensor, beta: torch.Tensor):
+        K = w.shape[1]
+        g = torch.zeros(K, dtype=torch.float32, device=w.device)
+        bt = torch.zeros(K, dtype=torch.float32, device=w.device)
+        g[: gamma.numel()] = gamma.float()  # K may be zero-padded past the LayerNorm width
+        bt[: beta.numel()] = beta.float()
+        wf = w.float()
+        self.w = (wf * g).to(BF16).contiguous()
+        self.cs = self.w.float().sum(dim=1).contiguous()
+        b = wf @ bt
+        if bias is not None:
+            b[: bias.numel()] += bias.float()[: b.numel()]
+        self.b = b.contiguous()
+
+
 def layernorm(x: torch.Tensor, gamma: torch.Tensor, beta: torch.Tensor, eps: float, *,
               rows_idx: Optional[torch.Tensor] = None, out: Optional[torch.Tensor] = None,
               d: Optional[int] = None) -> torch.Tensor:

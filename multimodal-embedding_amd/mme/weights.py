@@ -41,6 +41,7 @@ class LayerW:
     fc2_w: torch.Tensor   # [d, Ipad]
     fc2_b: torch.Tensor
     mx: Optional[object] = None  # mme.mx.LayerMX: fp8 copies of qkv/fc1/fc2 (opt-in precision mode)
+    fold: Optional[tuple] = None  # (ops.LNFolded qkv, ops.LNFolded fc1): LayerNorms folded into the weights
 
 
 @dataclass

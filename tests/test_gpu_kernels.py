@@ -162,6 +162,43 @@ def test_layernorm(cuda, rows, d):
     torch.testing.assert_close(out2.float(), ref[idx.long()], atol=3e-2, rtol=1e-2)
 
 
+@pytest.mark.parametrize("rows,d", [(1, 64), (1000, 1152), (37, 1280), (5, 768)])
+def test_rowstats(cuda, rows, d):
+    g = torch.Generator(device="cuda").manual_seed(rows * 3 + d)
+    x = rnd(rows, d, scale=3.0, gen=g) + 0.5
+    st = ops.rowstats(x, 1e-6)
+    xf = x.float()
+    mean = xf.mean(dim=1)
+    rstd = torch.rsqrt(xf.var(dim=1, unbiased=False) + 1e-6)
+    torch.testing.assert_close(st[:, 0], mean, atol=1e-5, rtol=1e-5)
+    torch.testing.assert_close(st[:, 1], rstd, atol=1e-5, rtol=1e-4)
+
+
+# LayerNorm -> Linear with the LayerNorm folded into the weights (mme_gemm_lnfold) against
+# the unfused fp32 chain; the residual-stream rows carry an offset (mean) and a scale so
+# the mean-subtraction term matters. Shapes cover the generic (small) and pipelined
+# (incl. split-grid N = 1152 / 3456) kernels.
+@pytest.mark.parametrize("M,N,K", [(100, 200, 128), (2048, 3456, 1152), (1500, 4352, 1152), (4096, 1152, 1152)])
+@pytest.mark.parametrize("act", [0, 1])
+def test_gemm_lnfold(cuda, M, N, K, act):
+    g = torch.Generator(device="cuda").manual_seed(M + N + act)
+    x = rnd(M, K, scale=4.0, gen=g) + 2.0
+    gm = (1.0 + 0.2 * torch.randn(K, generator=g, device="cuda")).to(torch.bfloat16)
+    bt = rnd(K, scale=0.1, gen=g)
+    w = rnd(N, K, scale=1 / math.sqrt(K), gen=g)
+    b = rnd(N, scale=0.1, gen=g)
+    fold = ops.LNFolded(w, b, gm, bt)
+    out = ops.gemm_lnfold(x, fold, ops.rowstats(x, 1e-6), act=act)
+    h = torch.nn.functional.layer_norm(x.float(), (K,), gm.float(), bt.float(), 1e-6)
+    ref = act_ref(h @ w.float().T + b.float(), act)
+    torch.testing.assert_close(out.float(), ref, atol=3e-2, rtol=2e-2)
+    # and within the same error budget as the unfolded bf16 chain (LayerNorm rounded to bf16)
+    unf = ops.gemm(ops.layernorm(x, gm, bt, 1e-6), w, b, act=act).float()
+    e_fold = (out.float() - ref).abs().mean().item()
+    e_unf = (unf - ref).abs().mean().item()
+    assert e_fold <= 1.5 * e_unf + 1e-4, (e_fold, e_unf)
+
+
 def test_l2norm_bit_exact(cuda, golden):
     g = golden("l2norm")
     x = bits_to_bf16(g["x"]).cuda()

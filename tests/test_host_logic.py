@@ -118,3 +118,24 @@ def test_random_init_matches_hf_shapes(name):
     sd = random_state_dict(spec, seed=0, device="cpu")
     assert {k: tuple(v.shape) for k, v in sd.items()} == shapes
     assert {k: v.shape for k, v in np_state_dict(spec).items()} == shapes
+
+
+def test_layernorm_fold_algebra():
+    """ops.LNFolded (mme_gemm_lnfold's weights): rstd * (x . w'^T - mean * cs) + b' equals
+    LayerNorm(x) . w^T + b up to the bf16 rounding of w' = w * gamma (host-side check of the
+    identity the GPU epilogue evaluates; the kernel itself is tested in test_gpu_kernels)."""
+    from mme import ops
+    g = torch.Generator().manual_seed(0)
+    M, K, N = 64, 256, 96
+    x = (torch.randn(M, K, generator=g) * 3 + 1.5).bfloat16().float()
+    gamma = (1 + 0.2 * torch.randn(K, generator=g)).bfloat16()
+    beta = (0.1 * torch.randn(K, generator=g)).bfloat16()
+    w = (torch.randn(N, K, generator=g) / K ** 0.5).bfloat16()
+    b = (0.1 * torch.randn(N, generator=g)).bfloat16()
+    fold = ops.LNFolded(w, b, gamma, beta)
+    mean = x.mean(dim=1, keepdim=True)
+    rstd = torch.rsqrt(x.var(dim=1, unbiased=False, keepdim=True) + 1e-6)
+    out = rstd * (x @ fold.w.float().T - mean * fold.cs) + fold.b
+    ref = torch.nn.functional.layer_norm(x, (K,), gamma.float(), beta.float(), 1e-6) @ w.float().T + b.float()
+    torch.testing.assert_close(out, ref, atol=2e-2, rtol=2e-2)
+    assert fold.w.dtype == torch.bfloat16 and fold.cs.dtype == torch.float32 and fold.b.dtype == torch.float32
