@@ -549,9 +549,10 @@ __device__ __forceinline__ float xsum32(float v) {
     return __uint_as_float(r[0]) + __uint_as_float(r[1]);
 }
 
-template <int HD, int NW, int NSTG, bool PIPE, bool ONES, bool LAZY>
+template <int HD, int NW, int NSTG, bool PIPE, bool ONES, bool LAZY, bool PING = false>
 __global__ __launch_bounds__(NW * 64) void attn_pipe_kernel(AttnArgs a) {
     static_assert(!PIPE || NSTG == 3, "the pipelined loop keeps tile t+1 resident while t+2 lands");
+    static_assert(!PING || (!PIPE && NSTG == 4), "ping-pong: two tiles resident beside the one landing");
     static_assert(!ONES || HD == 72, "the ones column lives in the padding of the 80-wide V^T tiles");
     constexpr int HDP = HD == 64 ? 64 : 96;
     constexpr int NKS = HDP / 32;
@@ -680,7 +681,7 @@ __global__ __launch_bounds__(NW * 64) void attn_pipe_kernel(AttnArgs a) {
             }
         }
     };
-    auto softmax_pv = [&](int t, f32x4(&sc)[2][4]) {
+    auto softmax_pv = [&](int t, f32x4(&sc)[2][4], auto&& before_pv) {
         const unsigned so = (t % NSTG) * TILE;
         float mnew[2];
         bool grew = false;
@@ -719,6 +720,7 @@ __global__ __launch_bounds__(NW * 64) void attn_pipe_kernel(AttnArgs a) {
                 }
             if (!ONES) lsum[u] += psum;
         }
+        before_pv();
 #pragma unroll
         for (int hh = 0; hh < 2; ++hh) {
             bf16x8 pb[2];
@@ -749,7 +751,7 @@ __global__ __launch_bounds__(NW * 64) void attn_pipe_kernel(AttnArgs a) {
                 if (t + 2 < nkt) issue(t + 2);
                 qk(t + 1, nxt);
             }
-            softmax_pv(t, cur);
+            softmax_pv(t, cur, [] {});
         };
         issue(0);
         if (nkt > 1) issue(1);
@@ -760,6 +762,31 @@ __global__ __launch_bounds__(NW * 64) void attn_pipe_kernel(AttnArgs a) {
             iter(t, sA, sB);
             if (t + 1 < nkt) iter(t + 1, sB, sA);
         }
+    } else if (PING) {
+        // Ping-pong (two barriers per tile: S(t) before QK, H(t) before PV): waves NW/2.. run
+        // one barrier behind, so on every SIMD one wave's exp / max VALU meets the other's PV
+        // or QK MFMAs instead of both waves hitting the softmax together. Tile t+2 goes into
+        // the slot of tile t-2, whose last reads (the late half's PV(t-2)) end two barriers
+        // earlier. Every wave's own pieces of tile t+1 land before the barrier after which the
+        // early half reads it: early waves wait at S(t+1), late waves before their H(t).
+        const bool late = wave >= NW / 2;
+        issue(0);
+        if (nkt > 1) issue(1);
+        if (late) {
+            wait_own(nkt > 1 ? 1 : 0);
+            __builtin_amdgcn_s_barrier();
+        }
+        for (int t = 0; t < nkt; ++t) {
+            if (!late) wait_own(t + 1 < nkt ? 1 : 0);
+            __builtin_amdgcn_s_barrier();
+            if (t + 2 < nkt) issue(t + 2);
+            qk(t, sA);
+            softmax_pv(t, sA, [&] {
+                if (late) wait_own(t + 2 < nkt ? 1 : 0);
+                __builtin_amdgcn_s_barrier();
+            });
+        }
+        if (!late) __builtin_amdgcn_s_barrier();
     } else {
         for (int t = 0; t < NSTG - 1 && t < nkt; ++t) issue(t);
         for (int t = 0; t < nkt; ++t) {
@@ -767,7 +794,7 @@ __global__ __launch_bounds__(NW * 64) void attn_pipe_kernel(AttnArgs a) {
             __builtin_amdgcn_s_barrier();
             if (t + NSTG - 1 < nkt) issue(t + NSTG - 1);
             qk(t, sA);
-            softmax_pv(t, sA);
+            softmax_pv(t, sA, [] {});
         }
     }
 
@@ -886,6 +913,8 @@ void launch_attn(int kind, const AttnArgs& a, int B, int T, int H, hipStream_t s
         hipLaunchKernelGGL((attn_pipe_kernel<HD, 2, 2, false, HD == 72, true>), dim3(cdiv(T, 64) * H * B), dim3(128), 0, st, a);
     else if (kind == 14)  // dev: lean + lazy (+ ones), 4 waves = 128 queries per block
         hipLaunchKernelGGL((attn_pipe_kernel<HD, 4, 2, false, HD == 72, true>), dim3(cdiv(T, 128) * H * B), dim3(256), 0, st, a);
+    else if (kind == 15)  // dev: ping-pong halves (8 waves), lean + lazy (+ ones)
+        hipLaunchKernelGGL((attn_pipe_kernel<HD, 8, 4, false, HD == 72, true, true>), dim3(cdiv(T, 256) * H * B), dim3(512), 0, st, a);
     else if (kind == 12)  // dev: pipelined + lazy + ones
         hipLaunchKernelGGL((attn_pipe_kernel<HD, 8, 3, true, HD == 72, true>), dim3(cdiv(T, 256) * H * B), dim3(512), 0, st, a);
     else
