@@ -49,7 +49,8 @@ def parse():
     p.add_argument("--n-images", type=int, default=5000)
     p.add_argument("--caps", type=int, default=5)
     p.add_argument("--img-batch", type=int, default=256)
-    p.add_argument("--txt-batch", type=int, default=1024)
+    p.add_argument("--txt-batch", type=int, default=2048,
+                   help="captions per text-tower launch (2048 x 64 tokens tiles the N = 1152 / 3456 GEMMs exactly)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline sample duration")
     p.add_argument("--no-kernel-timer", action="store_true")

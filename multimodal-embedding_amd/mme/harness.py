@@ -26,7 +26,7 @@ METRIC_KEYS = [f"{p}_R@{k}" for p in ("T2I", "I2T", "I2T_Sym") for k in KS]
 
 
 def encode_job(model, images_u8: torch.Tensor, caption_ids: torch.Tensor, caption_lens: Optional[torch.Tensor] = None,
-               caps_per_image: int = 5, img_batch: int = 256, txt_batch: int = 1024):
+               caps_per_image: int = 5, img_batch: int = 256, txt_batch: int = 2048):
     """Encode n images, their caption-0 T2I queries and all 5n captions (main.py:551-557)."""
     n = images_u8.shape[0]
     img = model.encode_images(images_u8, batch=img_batch)

@@ -318,7 +318,7 @@ class DualEncoder:
 
     @torch.no_grad()
     def encode_texts(self, ids: torch.Tensor, lens: Optional[torch.Tensor] = None, ref_batch: Optional[int] = None,
-                     exec_batch: int = 1024, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+                     exec_batch: int = 2048, out: Optional[torch.Tensor] = None) -> torch.Tensor:
         """Token ids -> L2-normalised bf16 embeddings, reproducing the reference's
         batch-padding semantics exactly: each reference batch of `ref_batch`
         captions (main.py:420) is padded to its own longest caption (processor
