@@ -72,33 +72,41 @@ __global__ __launch_bounds__(256) void layernorm_kernel(const bf16* __restrict__
 // LayerNorm statistics only (mean, rstd) per row, for a GEMM with the LayerNorm folded
 // into its weights (mme_gemm_lnfold): same fp32 two-pass arithmetic as layernorm_kernel,
 // 8 bytes written per row instead of the normalised row.
+// Rows per wave (loads of all its rows issued before any reduction). Measured on 430 MB of
+// SigLIP rows (tools/rowstats_bench.py): 1 row 4.7 TB/s, 2 rows 3.8, 4 rows 2.7 -- the
+// pass wants waves, not bytes per wave.
+constexpr int RS_ROWS = 1;
 __global__ __launch_bounds__(256) void rowstats_kernel(const bf16* __restrict__ x, int ldx, float* __restrict__ st,
                                                        int rows, int d, float eps) {
-    const int row = blockIdx.x * ROWS_PER_BLOCK + (threadIdx.x >> 6);
+    const int row0 = (blockIdx.x * ROWS_PER_BLOCK + (threadIdx.x >> 6)) * RS_ROWS;
     const int lane = threadIdx.x & 63;
-    if (row >= rows) return;
+    if (row0 >= rows) return;
     const int nch = d >> 3;
-    float v[MAXC][8];
-    load_row(x + (long)row * ldx, nch, lane, v);
-    float s = 0.f;
+    float v[RS_ROWS][MAXC][8];
 #pragma unroll
-    for (int c = 0; c < MAXC; ++c)
+    for (int k = 0; k < RS_ROWS; ++k) load_row(x + (long)min(row0 + k, rows - 1) * ldx, nch, lane, v[k]);
 #pragma unroll
-        for (int e = 0; e < 8; ++e) s += v[c][e];
-    const float mean = wave_sum(s) / d;
-    float s2 = 0.f;
+    for (int k = 0; k < RS_ROWS; ++k) {
+        float s = 0.f;
 #pragma unroll
-    for (int c = 0; c < MAXC; ++c) {
-        if (lane + c * 64 < nch) {
+        for (int c = 0; c < MAXC; ++c)
 #pragma unroll
-            for (int e = 0; e < 8; ++e) {
-                const float t = v[c][e] - mean;
-                s2 += t * t;
+            for (int e = 0; e < 8; ++e) s += v[k][c][e];
+        const float mean = wave_sum(s) / d;
+        float s2 = 0.f;
+#pragma unroll
+        for (int c = 0; c < MAXC; ++c) {
+            if (lane + c * 64 < nch) {
+#pragma unroll
+                for (int e = 0; e < 8; ++e) {
+                    const float t = v[k][c][e] - mean;
+                    s2 += t * t;
+                }
             }
         }
+        const float rstd = rsqrtf(wave_sum(s2) / d + eps);
+        if (lane == 0 && row0 + k < rows) *reinterpret_cast<float2*>(st + 2 * (long)(row0 + k)) = make_float2(mean, rstd);
     }
-    const float rstd = rsqrtf(wave_sum(s2) / d + eps);
-    if (lane == 0) *reinterpret_cast<float2*>(st + 2 * (long)row) = make_float2(mean, rstd);
 }
 
 // out / out.norm(dim=-1, keepdim=True) on a bf16 tensor (main.py:414,434):
@@ -160,7 +168,7 @@ extern "C" int mme_rowstats(const void* x, int ldx, int rows, int d, float eps, 
     MME_REQUIRE(rows >= 0 && d > 0 && d % 8 == 0 && d <= 8 * 64 * MAXC, "mme_rowstats: d=%d unsupported", d);
     MME_REQUIRE(ldx % 8 == 0 && ldx >= d && ((uintptr_t)stats & 7) == 0, "mme_rowstats: bad leading dim / alignment");
     if (rows == 0) return MME_OK;
-    hipLaunchKernelGGL(rowstats_kernel, dim3(cdiv(rows, ROWS_PER_BLOCK)), dim3(256), 0, as_stream(stream),
+    hipLaunchKernelGGL(rowstats_kernel, dim3(cdiv(rows, ROWS_PER_BLOCK * RS_ROWS)), dim3(256), 0, as_stream(stream),
                        (const bf16*)x, ldx, stats, rows, d, eps);
     return mme_check_launch("mme_rowstats");
 }
