@@ -823,6 +823,176 @@ __global__ __launch_bounds__(NW * 64) void attn_pipe_kernel(AttnArgs a) {
     }
 }
 
+// attn_short_kernel: sequences of at most 64 tokens (SigLIP text, L = 64) — the
+// whole key range is ONE 64-key tile, so there is no online softmax and no tile
+// ring. attn_fwd_kernel's 128-query blocks computed 64 clamped duplicate query
+// rows there (half its MFMA / exp work wasted: ~125 TF/s on the text towers).
+// Here a workgroup = 4 waves = TWO (batch, head) units: waves 2s, 2s+1 take the
+// 32-query halves of unit s, whose K and V tiles sit in LDS slot s (the two
+// buffers attn_fwd_kernel rings through). Same per-wave math (S^T = K.Q^T, P in
+// registers as the B operand of O^T = V^T.P^T, V^T by ds_read_b64_tr_b16).
+template <int HD>
+__global__ __launch_bounds__(256, 3) void attn_short_kernel(AttnArgs a, int units) {
+    constexpr int HDP = HD == 64 ? 64 : 96;
+    constexpr int NKS = HDP / 32;
+    constexpr int KS = HDP + 8;  // K LDS row stride (elements)
+    constexpr int VS = 80;       // V LDS row stride: conflict-free tr reads
+    constexpr int NCHL = HD / 8;
+    constexpr int NDT = (HD + 15) / 16;
+    constexpr int NCH = 64 * NCHL;  // 16-B chunks per K (or V) tile
+    static_assert((4 * NCH) % 256 == 0, "K + V tiles of both slots split evenly over 256 threads");
+    __shared__ __attribute__((aligned(16))) bf16 Ks[2][64 * KS];
+    __shared__ __attribute__((aligned(16))) bf16 Vs[2][64 * VS];
+
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int g = lane >> 4, li = lane & 15;
+    const int T = a.T, D = a.H * HD;
+
+    // stage K and V of both units (rows past T clamped: finite, masked below)
+#pragma unroll
+    for (int i = 0; i < 4 * NCH / 256; ++i) {
+        const int c = tid + i * 256;
+        const int s = c / (2 * NCH), r = c % (2 * NCH);
+        const bool isV = r >= NCH;
+        const int row = (r % NCH) / NCHL, ch = (r % NCH) % NCHL;
+        const int un = min(blockIdx.x * 2 + s, units - 1);
+        const int ub = un / a.H, uh = un % a.H;
+        const bf16* src = a.qkv + ((long)ub * T + min(row, T - 1)) * a.ld + (isV ? 2 : 1) * D + uh * HD + ch * 8;
+        const u16x8 v = *reinterpret_cast<const u16x8*>(src);
+        if (isV)
+            *reinterpret_cast<u16x8*>(&Vs[s][row * VS + ch * 8]) = v;
+        else
+            *reinterpret_cast<u16x8*>(&Ks[s][row * KS + ch * 8]) = v;
+    }
+    if (HDP > HD || VS > HD) {  // zero the padding columns (disjoint from the tile bytes)
+        for (int i = tid; i < 2 * 64; i += 256) {
+            bf16* kr = &Ks[i >> 6][(i & 63) * KS];
+            for (int col = HD; col < HDP; col += 8) *reinterpret_cast<u16x8*>(kr + col) = u16x8{0, 0, 0, 0, 0, 0, 0, 0};
+            bf16* vr = &Vs[i >> 6][(i & 63) * VS];
+            for (int col = HD; col < VS; col += 8) *reinterpret_cast<u16x8*>(vr + col) = u16x8{0, 0, 0, 0, 0, 0, 0, 0};
+        }
+    }
+
+    const int slot = wave >> 1;
+    const int unit = blockIdx.x * 2 + slot;
+    const int uc = min(unit, units - 1);
+    const int b = uc / a.H, h = uc % a.H;
+    const bf16* base = a.qkv + (long)b * T * a.ld;
+    const int qw0 = (wave & 1) * 32;
+    const int Tk = a.seq_lens ? a.seq_lens[b] : T;
+    const float c = a.scale_log2;
+
+    bf16x8 qf[2][NKS];
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+        const bf16* qrow = base + (long)min(qw0 + u * 16 + li, T - 1) * a.ld + h * HD;
+#pragma unroll
+        for (int ks = 0; ks < NKS; ++ks) {
+            const int col = ks * 32 + 8 * g;
+            if (col < HD)
+                qf[u][ks] = *reinterpret_cast<const bf16x8*>(qrow + col);
+            else
+                qf[u][ks] = bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
+        }
+    }
+    __syncthreads();
+
+    const bf16* Kb = Ks[slot];
+    const bf16* Vb = Vs[slot];
+    f32x4 sc[2][4];
+#pragma unroll
+    for (int kt = 0; kt < 4; ++kt) {
+        const bf16* krow = Kb + (kt * 16 + li) * KS;
+        bf16x8 kf[NKS];
+#pragma unroll
+        for (int ks = 0; ks < NKS; ++ks) kf[ks] = *reinterpret_cast<const bf16x8*>(krow + ks * 32 + 8 * g);
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+            f32x4 z = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int ks = 0; ks < NKS; ++ks) z = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf[ks], qf[u][ks], z, 0, 0, 0);
+            sc[u][kt] = z;
+        }
+    }
+    if (Tk < 64 || a.causal) {
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+            const int q = qw0 + u * 16 + li;
+            const int lim = a.causal ? min(Tk, q + 1) : Tk;
+#pragma unroll
+            for (int kt = 0; kt < 4; ++kt)
+#pragma unroll
+                for (int r = 0; r < 4; ++r)
+                    if (kt * 16 + 4 * g + r >= lim) sc[u][kt][r] = -INFINITY;
+        }
+    }
+
+    float lsum[2];
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+        float mloc = -1e30f;
+#pragma unroll
+        for (int kt = 0; kt < 4; ++kt)
+            mloc = fmaxf(mloc, fmaxf(fmaxf(sc[u][kt][0], sc[u][kt][1]), fmaxf(sc[u][kt][2], sc[u][kt][3])));
+        mloc = xmax32(xmax16(mloc));
+        const float mc = mloc * c;
+        float psum = 0.f;
+#pragma unroll
+        for (int kt = 0; kt < 4; ++kt)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const float pv = __builtin_amdgcn_exp2f(sc[u][kt][r] * c - mc);
+                sc[u][kt][r] = pv;
+                psum += pv;
+            }
+        lsum[u] = xsum32(xsum16(psum));
+    }
+
+    f32x4 o[2][NDT];
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+#pragma unroll
+        for (int i = 0; i < NDT; ++i) o[u][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int hh = 0; hh < 2; ++hh) {
+        bf16x8 pb[2];
+#pragma unroll
+        for (int u = 0; u < 2; ++u)
+            pb[u] = __builtin_convertvector(__builtin_shufflevector(sc[u][2 * hh], sc[u][2 * hh + 1], 0, 1, 2, 3, 4, 5,
+                                                                    6, 7), bf16x8);
+        const int r1 = 32 * hh + 4 * g + (li >> 2);
+#pragma unroll
+        for (int dt = 0; dt < NDT; ++dt) {
+            const int col = dt * 16 + 4 * (li & 3);
+            const s16x4 v0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS_AS s16x4*)(Vb + r1 * VS + col));
+            const s16x4 v1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS_AS s16x4*)(Vb + (r1 + 16) * VS + col));
+            const bf16x8 vv = __builtin_bit_cast(bf16x8, __builtin_shufflevector(v0, v1, 0, 1, 2, 3, 4, 5, 6, 7));
+#pragma unroll
+            for (int u = 0; u < 2; ++u) o[u][dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vv, pb[u], o[u][dt], 0, 0, 0);
+        }
+    }
+
+    if (unit >= units) return;
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+        const float inv = 1.0f / lsum[u];
+        const int q = qw0 + u * 16 + li;
+        if (q < T) {
+            bf16* orow = a.out + ((long)b * T + q) * a.ldo + h * HD;
+#pragma unroll
+            for (int dt = 0; dt < NDT; ++dt) {
+                const int d0 = dt * 16 + 4 * g;
+                if (d0 < HD) {
+                    bf16x4 v;
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) v[r] = f2bf(o[u][dt][r] * inv);
+                    *reinterpret_cast<bf16x4*>(orow + d0) = v;
+                }
+            }
+        }
+    }
+}
+
 // SigLIP MAP head: one probe query per head, keys = the T tokens of image b.
 constexpr int PROBE_MAXT = 1024;
 __global__ __launch_bounds__(256) void probe_attn_kernel(const bf16* __restrict__ qv, const bf16* __restrict__ kv,
@@ -889,6 +1059,8 @@ template <int HD>
 void launch_attn(int kind, const AttnArgs& a, int B, int T, int H, hipStream_t st) {
     if (kind == 0)
         hipLaunchKernelGGL((attn_fwd_kernel<HD>), dim3(cdiv(T, 128) * H * B), dim3(256), 0, st, a);
+    else if (kind == 16)  // T <= 64: one key tile, two (batch, head) units per block
+        hipLaunchKernelGGL((attn_short_kernel<HD>), dim3(cdiv(B * H, 2)), dim3(256), 0, st, a, B * H);
     else if (kind == 1)
         hipLaunchKernelGGL((attn_dma_kernel<HD, 4, 2>), dim3(cdiv(T, 128) * H * B), dim3(256), 0, st, a);
     else if (kind == 3)
@@ -949,7 +1121,9 @@ extern "C" int mme_attention(const void* qkv, int ld_qkv, void* out, int ld_out,
     // The LDS-DMA kernels run as attn_pipe_kernel's lean non-pipelined form (kinds 11 / 14:
     // lane-base fragment addresses, permlane reductions, lazy rescale, and for hd 72 the
     // weight sums from a ones column of V^T): SigLIP vision 1.27-1.33 -> 1.16-1.17 ms.
-    int kind = (T <= 128 || hd == 64) ? 0
+    // T <= 64 (SigLIP text): attn_short_kernel, two (batch, head) units of one key tile per block.
+    int kind = T <= 64 ? 16
+               : (T <= 128 || hd == 64) ? 0
                : ((long)cdiv(T, 256) * 256 * 10 <= (long)cdiv(T, 128) * 128 * 11 ? 11 : 14);
     if (g_attn_variant >= 1 && g_attn_variant <= 4 && hd == 72) {  // dev-only diagnostic builds
         const dim3 grid(cdiv(T, 128) * H * B);
@@ -962,7 +1136,7 @@ extern "C" int mme_attention(const void* qkv, int ld_qkv, void* out, int ld_out,
         return mme_check_launch("mme_attention");
     }
     if (g_attn_variant >= 9 && g_attn_variant <= 16) kind = g_attn_variant - 9;  // dev: force a kernel
-    if (g_attn_variant >= 30 && g_attn_variant <= 45) kind = g_attn_variant - 30;  // dev: force a kernel
+    if (g_attn_variant >= 30 && g_attn_variant <= 46) kind = g_attn_variant - 30;  // dev: force a kernel
     if (g_attn_variant >= 21 && g_attn_variant <= 26 && hd == 72) {  // dev: attn_dma_kernel<72,8,2> diagnostics
         const dim3 grid(cdiv(T, 256) * H * B), blk(512);
         hipStream_t st = as_stream(stream);

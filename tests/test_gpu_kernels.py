@@ -101,6 +101,9 @@ def attn_ref(qkv, B, T, H, hd, lens, causal, scale):
 @pytest.mark.parametrize("B,T,H,hd,causal,lens", [
     (2, 729, 16, 72, False, None),     # SigLIP-400M vision
     (2, 64, 16, 72, False, [64, 23]),  # SigLIP text with padding mask
+    (3, 64, 3, 72, False, [64, 1, 30]),  # short kernel: odd unit count (9), last block half empty
+    (5, 40, 1, 80, True, [40, 7, 40, 1, 33]),  # short kernel: causal + padding, T < 64
+    (3, 64, 5, 64, True, None),
     (3, 77, 12, 64, True, None),       # CLIP-L text
     (3, 77, 16, 64, True, [77, 9, 40]),
     (2, 257, 16, 80, False, None),     # ViT-H/14-224
