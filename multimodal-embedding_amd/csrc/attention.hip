@@ -549,8 +549,8 @@ __device__ __forceinline__ float xsum32(float v) {
     return __uint_as_float(r[0]) + __uint_as_float(r[1]);
 }
 
-template <int HD, int NW, int NSTG, bool PIPE, bool ONES, bool LAZY, bool PING = false>
-__global__ __launch_bounds__(NW * 64) void attn_pipe_kernel(AttnArgs a) {
+template <int HD, int NW, int NSTG, bool PIPE, bool ONES, bool LAZY, bool PING = false, int MINW = 1>
+__global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(MINW))) void attn_pipe_kernel(AttnArgs a) {
     static_assert(!PIPE || NSTG == 3, "the pipelined loop keeps tile t+1 resident while t+2 lands");
     static_assert(!PING || (!PIPE && NSTG == 4), "ping-pong: two tiles resident beside the one landing");
     static_assert(!ONES || HD == 72, "the ones column lives in the padding of the 80-wide V^T tiles");
@@ -630,12 +630,13 @@ __global__ __launch_bounds__(NW * 64) void attn_pipe_kernel(AttnArgs a) {
     };
 
     const unsigned lds0 = (unsigned)(uintptr_t)(LDS_AS char*)lds;
-    unsigned kb[NKS];
-#pragma unroll
-    for (int ks = 0; ks < NKS; ++ks) {
-        const int cch = ks * 4 + g;
-        kb[ks] = lds0 + (cch < NCHL ? cch : 0) * 1024 + li * 16;
-    }
+    // K fragment of step ks = plane 4 ks + g; lanes past HD read planes beyond the K planes
+    // (V planes of the same tile: finite, landed with it) against zero Q columns, so every
+    // step is the lane base + an immediate (no per-step address registers).
+    const unsigned kb0 = lds0 + g * 1024 + li * 16;
+    // V^T fragment of d-tile dt = plane 2 dt + ((li >> 1) & 1): the lane base + dt * 2 KiB,
+    // except at head dim 72 without the ones plane, where plane 9 does not exist (clamped)
+    constexpr bool VLIN = !(HD == 72 && !ONES);
     unsigned vb[NDT];
 #pragma unroll
     for (int dt = 0; dt < NDT; ++dt) {
@@ -659,7 +660,7 @@ __global__ __launch_bounds__(NW * 64) void attn_pipe_kernel(AttnArgs a) {
             bf16x8 kf[NKS];
 #pragma unroll
             for (int ks = 0; ks < NKS; ++ks)
-                kf[ks] = *reinterpret_cast<const LDS_AS bf16x8*>((uintptr_t)(kb[ks] + so + kt * 256));
+                kf[ks] = *reinterpret_cast<const LDS_AS bf16x8*>((uintptr_t)(kb0 + so + kt * 256 + ks * 4096));
 #pragma unroll
             for (int u = 0; u < 2; ++u) {
                 f32x4 z = {0.f, 0.f, 0.f, 0.f};
@@ -730,7 +731,7 @@ __global__ __launch_bounds__(NW * 64) void attn_pipe_kernel(AttnArgs a) {
                                                                         4, 5, 6, 7), bf16x8);
 #pragma unroll
             for (int dt = 0; dt < NDT; ++dt) {
-                const unsigned va = vb[dt] + so + hh * 512;
+                const unsigned va = (VLIN ? vb[0] + dt * 2048 : vb[dt]) + so + hh * 512;
                 const s16x4 v0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS_AS s16x4*)(uintptr_t)va);
                 const s16x4 v1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS_AS s16x4*)(uintptr_t)(va + 256));
                 const bf16x8 vv = __builtin_bit_cast(bf16x8, __builtin_shufflevector(v0, v1, 0, 1, 2, 3, 4, 5, 6, 7));
@@ -1087,6 +1088,10 @@ void launch_attn(int kind, const AttnArgs& a, int B, int T, int H, hipStream_t s
         hipLaunchKernelGGL((attn_pipe_kernel<HD, 4, 2, false, HD == 72, true>), dim3(cdiv(T, 128) * H * B), dim3(256), 0, st, a);
     else if (kind == 15)  // dev: ping-pong halves (8 waves), lean + lazy (+ ones)
         hipLaunchKernelGGL((attn_pipe_kernel<HD, 8, 4, false, HD == 72, true, true>), dim3(cdiv(T, 256) * H * B), dim3(512), 0, st, a);
+    else if (kind == 17)  // dev: kind 11 held to 128 VGPRs -> two 8-wave blocks per CU (4 waves / SIMD)
+        hipLaunchKernelGGL((attn_pipe_kernel<HD, 8, 2, false, HD == 72, true, false, 4>), dim3(cdiv(T, 256) * H * B), dim3(512), 0, st, a);
+    else if (kind == 18)  // dev: kind 14 held to 128 VGPRs (4-wave blocks, 4 per CU)
+        hipLaunchKernelGGL((attn_pipe_kernel<HD, 4, 2, false, HD == 72, true, false, 4>), dim3(cdiv(T, 128) * H * B), dim3(256), 0, st, a);
     else if (kind == 12)  // dev: pipelined + lazy + ones
         hipLaunchKernelGGL((attn_pipe_kernel<HD, 8, 3, true, HD == 72, true>), dim3(cdiv(T, 256) * H * B), dim3(512), 0, st, a);
     else
@@ -1122,9 +1127,13 @@ extern "C" int mme_attention(const void* qkv, int ld_qkv, void* out, int ld_out,
     // lane-base fragment addresses, permlane reductions, lazy rescale, and for hd 72 the
     // weight sums from a ones column of V^T): SigLIP vision 1.27-1.33 -> 1.16-1.17 ms.
     // T <= 64 (SigLIP text): attn_short_kernel, two (batch, head) units of one key tile per block.
+    // Head dim 72 (SigLIP vision): kind 17 = kind 11 held to 128 VGPRs (amdgpu_waves_per_eu(4);
+    // its 3 spilled registers live outside the tile loop), so two 8-wave blocks share a CU and
+    // each SIMD interleaves 4 waves: 1.18 -> 0.98 ms per 256-image layer (532 -> 638 TF/s).
+    // At head dim 80 the same cap spills inside the loop and gains nothing (DFN5B 0.628 / 0.622 ms).
     int kind = T <= 64 ? 16
                : (T <= 128 || hd == 64) ? 0
-               : ((long)cdiv(T, 256) * 256 * 10 <= (long)cdiv(T, 128) * 128 * 11 ? 11 : 14);
+               : ((long)cdiv(T, 256) * 256 * 10 <= (long)cdiv(T, 128) * 128 * 11 ? (hd == 72 ? 17 : 11) : 14);
     if (g_attn_variant >= 1 && g_attn_variant <= 4 && hd == 72) {  // dev-only diagnostic builds
         const dim3 grid(cdiv(T, 128) * H * B);
         switch (g_attn_variant) {
@@ -1136,7 +1145,7 @@ extern "C" int mme_attention(const void* qkv, int ld_qkv, void* out, int ld_out,
         return mme_check_launch("mme_attention");
     }
     if (g_attn_variant >= 9 && g_attn_variant <= 16) kind = g_attn_variant - 9;  // dev: force a kernel
-    if (g_attn_variant >= 30 && g_attn_variant <= 46) kind = g_attn_variant - 30;  // dev: force a kernel
+    if (g_attn_variant >= 30 && g_attn_variant <= 48) kind = g_attn_variant - 30;  // dev: force a kernel
     if (g_attn_variant >= 21 && g_attn_variant <= 26 && hd == 72) {  // dev: attn_dma_kernel<72,8,2> diagnostics
         const dim3 grid(cdiv(T, 256) * H * B), blk(512);
         hipStream_t st = as_stream(stream);

@@ -22,6 +22,7 @@ CASES = [  # name, B, T, H, hd, causal
     ("siglip_text", 1024, 64, 16, 72, False),
     ("clipL_vision", 256, 577, 16, 64, False),
     ("vitH_vision", 256, 257, 16, 80, False),
+    ("dfn5b_vision", 128, 730, 16, 80, False),
     ("clip_text_causal", 1024, 77, 16, 64, True),
 ]
 for (name, B, T, H, hd, causal), v in [(c, v) for c in CASES for v in VARIANTS]:
