@@ -89,3 +89,31 @@ __device__ __forceinline__ float apply_act(float x, int act) {
             return x;
     }
 }
+
+// The same activations on a pair of values with packed f32 math (v_pk_mul_f32 /
+// v_pk_fma_f32 / v_pk_add_f32: two lanes' worth per 4-cycle issue); only the
+// transcendentals stay per element. gelu_tanh argument as x * (c2 + c2 k1 x^2)
+// (one multiply fewer than the scalar form; fp32 rounding differs by ~1 ulp,
+// far below the bf16 output). Used by the GEMM epilogue, where these VALU
+// cycles are pure overhead on the MFMA pipe (fc1: ~25 % of its epilogue time).
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ f32x2 pk_fma(f32x2 a, f32x2 b, f32x2 c) { return __builtin_elementwise_fma(a, b, c); }
+__device__ __forceinline__ f32x2 apply_act2(f32x2 x, int act) {
+    switch (act) {
+        case MME_ACT_GELU_TANH: {
+            const float c2 = -2.0f * 0.7978845608028654f * 1.4426950408889634f;
+            const f32x2 u = pk_fma(x * x, f32x2{c2 * 0.044715f, c2 * 0.044715f}, f32x2{c2, c2}) * x;
+            const f32x2 d = f32x2{__builtin_amdgcn_exp2f(u.x), __builtin_amdgcn_exp2f(u.y)} + 1.0f;
+            return x * f32x2{__builtin_amdgcn_rcpf(d.x), __builtin_amdgcn_rcpf(d.y)};
+        }
+        case MME_ACT_QUICK_GELU: {
+            const f32x2 u = x * (-1.702f * 1.4426950408889634f);
+            const f32x2 d = f32x2{__builtin_amdgcn_exp2f(u.x), __builtin_amdgcn_exp2f(u.y)} + 1.0f;
+            return x * f32x2{__builtin_amdgcn_rcpf(d.x), __builtin_amdgcn_rcpf(d.y)};
+        }
+        case MME_ACT_GELU_ERF:
+            return f32x2{apply_act(x.x, act), apply_act(x.y, act)};
+        default:
+            return x;
+    }
+}

@@ -206,11 +206,22 @@ __device__ __forceinline__ void gemm_epilogue_lds(const GemmArgs& p, char* lds, 
             bf16x4 o;
             if (p.ln_stats) {
 #pragma unroll
-                for (int r = 0; r < 4; ++r)
-                    o[r] = f2bf(apply_act(fmaf(lr[i], acc[i][j][r], fmaf(lm[i], cs[r], bv[r])), RACT));
+                for (int r = 0; r < 4; r += 2) {
+                    const f32x2 y = apply_act2(
+                        pk_fma(f32x2{lr[i], lr[i]}, f32x2{acc[i][j][r], acc[i][j][r + 1]},
+                               pk_fma(f32x2{lm[i], lm[i]}, f32x2{cs[r], cs[r + 1]}, f32x2{bv[r], bv[r + 1]})),
+                        RACT);
+                    o[r] = f2bf(y.x);
+                    o[r + 1] = f2bf(y.y);
+                }
             } else {
 #pragma unroll
-                for (int r = 0; r < 4; ++r) o[r] = f2bf(apply_act(acc[i][j][r] + bv[r], RACT));
+                for (int r = 0; r < 4; r += 2) {
+                    const f32x2 y =
+                        apply_act2(f32x2{acc[i][j][r], acc[i][j][r + 1]} + f32x2{bv[r], bv[r + 1]}, RACT);
+                    o[r] = f2bf(y.x);
+                    o[r + 1] = f2bf(y.y);
+                }
             }
             *reinterpret_cast<bf16x4*>(lds + ml * C::OUT_LD + nl * 2) = o;
         }
