@@ -832,18 +832,25 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(MINW)))
 // 32-query halves of unit s, whose K and V tiles sit in LDS slot s (the two
 // buffers attn_fwd_kernel rings through). Same per-wave math (S^T = K.Q^T, P in
 // registers as the B operand of O^T = V^T.P^T, V^T by ds_read_b64_tr_b16).
-template <int HD>
+// COMPACT (head dims 72/80): K rows at the V pitch of 80 elements, so one block holds
+// 40 KiB of LDS and four blocks share a CU (three at the padded 104-element K pitch).
+// The zero-padded 96-deep QK^T reduction then reads past a K row's 80 elements into
+// the next row (or, for the last row, into the V tile behind it): finite values
+// against zero Q columns; only the K padding columns HD..80 are zeroed.
+template <int HD, bool COMPACT = false>
 __global__ __launch_bounds__(256, 3) void attn_short_kernel(AttnArgs a, int units) {
     constexpr int HDP = HD == 64 ? 64 : 96;
     constexpr int NKS = HDP / 32;
-    constexpr int KS = HDP + 8;  // K LDS row stride (elements)
+    constexpr int KS = COMPACT && HD != 64 ? 80 : HDP + 8;  // K LDS row stride (elements)
+    constexpr int KZ = COMPACT && HD != 64 ? KS : HDP;      // K columns HD..KZ zeroed
     constexpr int VS = 80;       // V LDS row stride: conflict-free tr reads
     constexpr int NCHL = HD / 8;
     constexpr int NDT = (HD + 15) / 16;
     constexpr int NCH = 64 * NCHL;  // 16-B chunks per K (or V) tile
     static_assert((4 * NCH) % 256 == 0, "K + V tiles of both slots split evenly over 256 threads");
-    __shared__ __attribute__((aligned(16))) bf16 Ks[2][64 * KS];
-    __shared__ __attribute__((aligned(16))) bf16 Vs[2][64 * VS];
+    __shared__ __attribute__((aligned(16))) bf16 sm[2 * 64 * KS + 2 * 64 * VS];  // K slots, then V slots
+    bf16 (*Ks)[64 * KS] = reinterpret_cast<bf16 (*)[64 * KS]>(sm);
+    bf16 (*Vs)[64 * VS] = reinterpret_cast<bf16 (*)[64 * VS]>(sm + 2 * 64 * KS);
 
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int g = lane >> 4, li = lane & 15;
@@ -865,10 +872,10 @@ __global__ __launch_bounds__(256, 3) void attn_short_kernel(AttnArgs a, int unit
         else
             *reinterpret_cast<u16x8*>(&Ks[s][row * KS + ch * 8]) = v;
     }
-    if (HDP > HD || VS > HD) {  // zero the padding columns (disjoint from the tile bytes)
+    if (KZ > HD || VS > HD) {  // zero the padding columns (disjoint from the tile bytes)
         for (int i = tid; i < 2 * 64; i += 256) {
             bf16* kr = &Ks[i >> 6][(i & 63) * KS];
-            for (int col = HD; col < HDP; col += 8) *reinterpret_cast<u16x8*>(kr + col) = u16x8{0, 0, 0, 0, 0, 0, 0, 0};
+            for (int col = HD; col < KZ; col += 8) *reinterpret_cast<u16x8*>(kr + col) = u16x8{0, 0, 0, 0, 0, 0, 0, 0};
             bf16* vr = &Vs[i >> 6][(i & 63) * VS];
             for (int col = HD; col < VS; col += 8) *reinterpret_cast<u16x8*>(vr + col) = u16x8{0, 0, 0, 0, 0, 0, 0, 0};
         }
@@ -1062,6 +1069,8 @@ void launch_attn(int kind, const AttnArgs& a, int B, int T, int H, hipStream_t s
         hipLaunchKernelGGL((attn_fwd_kernel<HD>), dim3(cdiv(T, 128) * H * B), dim3(256), 0, st, a);
     else if (kind == 16)  // T <= 64: one key tile, two (batch, head) units per block
         hipLaunchKernelGGL((attn_short_kernel<HD>), dim3(cdiv(B * H, 2)), dim3(256), 0, st, a, B * H);
+    else if (kind == 19)  // dev: short kernel, compact K pitch (4 blocks per CU): no gain, HBM-bound (0.138 / 0.136 ms)
+        hipLaunchKernelGGL((attn_short_kernel<HD, true>), dim3(cdiv(B * H, 2)), dim3(256), 0, st, a, B * H);
     else if (kind == 1)
         hipLaunchKernelGGL((attn_dma_kernel<HD, 4, 2>), dim3(cdiv(T, 128) * H * B), dim3(256), 0, st, a);
     else if (kind == 3)
@@ -1145,7 +1154,8 @@ extern "C" int mme_attention(const void* qkv, int ld_qkv, void* out, int ld_out,
         return mme_check_launch("mme_attention");
     }
     if (g_attn_variant >= 9 && g_attn_variant <= 16) kind = g_attn_variant - 9;  // dev: force a kernel
-    if (g_attn_variant >= 30 && g_attn_variant <= 48) kind = g_attn_variant - 30;  // dev: force a kernel
+    if (g_attn_variant >= 30 && g_attn_variant <= 49) kind = g_attn_variant - 30;  // dev: force a kernel
+    if ((kind == 16 || kind == 19) && T > 64) kind = 0;  // the short kernels hold one 64-key tile  // dev: force a kernel
     if (g_attn_variant >= 21 && g_attn_variant <= 26 && hd == 72) {  // dev: attn_dma_kernel<72,8,2> diagnostics
         const dim3 grid(cdiv(T, 256) * H * B), blk(512);
         hipStream_t st = as_stream(stream);
