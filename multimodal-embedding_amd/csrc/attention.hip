@@ -1155,7 +1155,7 @@ extern "C" int mme_attention(const void* qkv, int ld_qkv, void* out, int ld_out,
     }
     if (g_attn_variant >= 9 && g_attn_variant <= 16) kind = g_attn_variant - 9;  // dev: force a kernel
     if (g_attn_variant >= 30 && g_attn_variant <= 49) kind = g_attn_variant - 30;  // dev: force a kernel
-    if ((kind == 16 || kind == 19) && T > 64) kind = 0;  // the short kernels hold one 64-key tile  // dev: force a kernel
+    if ((kind == 16 || kind == 19) && T > 64) kind = 0;  // the short kernels hold one 64-key tile
     if (g_attn_variant >= 21 && g_attn_variant <= 26 && hd == 72) {  // dev: attn_dma_kernel<72,8,2> diagnostics
         const dim3 grid(cdiv(T, 256) * H * B), blk(512);
         hipStream_t st = as_stream(stream);
