@@ -855,34 +855,17 @@ __global__ __launch_bounds__(256, 3) void attn_short_kernel(AttnArgs a, int unit
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int g = lane >> 4, li = lane & 15;
     const int T = a.T, D = a.H * HD;
-
-    // stage K and V of both units (rows past T clamped: finite, masked below)
-#pragma unroll
-    for (int i = 0; i < 4 * NCH / 256; ++i) {
-        const int c = tid + i * 256;
-        const int s = c / (2 * NCH), r = c % (2 * NCH);
-        const bool isV = r >= NCH;
-        const int row = (r % NCH) / NCHL, ch = (r % NCH) % NCHL;
-        const int un = min(blockIdx.x * 2 + s, units - 1);
-        const int ub = un / a.H, uh = un % a.H;
-        const bf16* src = a.qkv + ((long)ub * T + min(row, T - 1)) * a.ld + (isV ? 2 : 1) * D + uh * HD + ch * 8;
-        const u16x8 v = *reinterpret_cast<const u16x8*>(src);
-        if (isV)
-            *reinterpret_cast<u16x8*>(&Vs[s][row * VS + ch * 8]) = v;
-        else
-            *reinterpret_cast<u16x8*>(&Ks[s][row * KS + ch * 8]) = v;
-    }
-    if (KZ > HD || VS > HD) {  // zero the padding columns (disjoint from the tile bytes)
-        for (int i = tid; i < 2 * 64; i += 256) {
-            bf16* kr = &Ks[i >> 6][(i & 63) * KS];
-            for (int col = HD; col < KZ; col += 8) *reinterpret_cast<u16x8*>(kr + col) = u16x8{0, 0, 0, 0, 0, 0, 0, 0};
-            bf16* vr = &Vs[i >> 6][(i & 63) * VS];
-            for (int col = HD; col < VS; col += 8) *reinterpret_cast<u16x8*>(vr + col) = u16x8{0, 0, 0, 0, 0, 0, 0, 0};
-        }
+    // XCD-aware: consecutive unit pairs (neighbouring heads of one sequence, whose
+    // 2*HD-byte row segments share cache lines) run on the same XCD / L2
+    int pair;
+    {
+        const int bid = blockIdx.x, nwg = gridDim.x;
+        const int xcd = bid & 7, loc = bid >> 3, q8 = nwg >> 3, r8 = nwg & 7;
+        pair = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + loc;
     }
 
     const int slot = wave >> 1;
-    const int unit = blockIdx.x * 2 + slot;
+    const int unit = pair * 2 + slot;
     const int uc = min(unit, units - 1);
     const int b = uc / a.H, h = uc % a.H;
     const bf16* base = a.qkv + (long)b * T * a.ld;
@@ -903,6 +886,31 @@ __global__ __launch_bounds__(256, 3) void attn_short_kernel(AttnArgs a, int unit
                 qf[u][ks] = bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
         }
     }
+    // stage K and V of both units (rows past T clamped: finite, masked below)
+#pragma unroll
+    for (int i = 0; i < 4 * NCH / 256; ++i) {
+        const int ci = tid + i * 256;
+        const int s = ci / (2 * NCH), r = ci % (2 * NCH);
+        const bool isV = r >= NCH;
+        const int row = (r % NCH) / NCHL, ch = (r % NCH) % NCHL;
+        const int un = min(pair * 2 + s, units - 1);
+        const int ub = un / a.H, uh = un % a.H;
+        const bf16* src = a.qkv + ((long)ub * T + min(row, T - 1)) * a.ld + (isV ? 2 : 1) * D + uh * HD + ch * 8;
+        const u16x8 v = *reinterpret_cast<const u16x8*>(src);
+        if (isV)
+            *reinterpret_cast<u16x8*>(&Vs[s][row * VS + ch * 8]) = v;
+        else
+            *reinterpret_cast<u16x8*>(&Ks[s][row * KS + ch * 8]) = v;
+    }
+    if (KZ > HD || VS > HD) {  // zero the padding columns (disjoint from the tile bytes)
+        for (int i = tid; i < 2 * 64; i += 256) {
+            bf16* kr = &Ks[i >> 6][(i & 63) * KS];
+            for (int col = HD; col < KZ; col += 8) *reinterpret_cast<u16x8*>(kr + col) = u16x8{0, 0, 0, 0, 0, 0, 0, 0};
+            bf16* vr = &Vs[i >> 6][(i & 63) * VS];
+            for (int col = HD; col < VS; col += 8) *reinterpret_cast<u16x8*>(vr + col) = u16x8{0, 0, 0, 0, 0, 0, 0, 0};
+        }
+    }
+
     __syncthreads();
 
     const bf16* Kb = Ks[slot];
