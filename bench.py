@@ -355,7 +355,7 @@ def main():
         # HBM bytes per launch from the rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes (tools/pmc_gemm.sh,
         # gfx950-corrected by tools/pmc_summary.py) of the same launch shapes
         pmc = os.path.join(ROOT, "profiles", "gemm_traffic.json")
-        if os.path.exists(pmc) and not args.fp8:
+        if os.path.exists(pmc) and not args.fp8 and args.model == "SigLIP-400M":  # measured on SigLIP's shapes
             try:
                 roofline["traffic"] = round(json.load(open(pmc))["mme_gemm"]["hbm_bytes_per_launch"])
             except (KeyError, ValueError, TypeError):

@@ -1109,6 +1109,12 @@ void launch_attn(int kind, const AttnArgs& a, int B, int T, int H, hipStream_t s
         hipLaunchKernelGGL((attn_pipe_kernel<HD, 8, 2, false, HD == 72, true, false, 4>), dim3(cdiv(T, 256) * H * B), dim3(512), 0, st, a);
     else if (kind == 18)  // dev: kind 14 held to 128 VGPRs (4-wave blocks, 4 per CU)
         hipLaunchKernelGGL((attn_pipe_kernel<HD, 4, 2, false, HD == 72, true, false, 4>), dim3(cdiv(T, 128) * H * B), dim3(256), 0, st, a);
+    else if (kind == 20)  // dev: 3 waves = 96 queries per block (T = 257: 288 padded rows): 0.337 ms, no gain
+        hipLaunchKernelGGL((attn_pipe_kernel<HD, 3, 2, false, HD == 72, true>), dim3(cdiv(T, 96) * H * B), dim3(192), 0, st, a);
+    else if (kind == 21)  // 9 waves = 288 queries per block (T = 257 in one block per batch-head)
+        hipLaunchKernelGGL((attn_pipe_kernel<HD, 9, 2, false, HD == 72, true>), dim3(cdiv(T, 288) * H * B), dim3(576), 0, st, a);
+    else if (kind == 22)  // dev: 5 waves = 160 queries per block
+        hipLaunchKernelGGL((attn_pipe_kernel<HD, 5, 2, false, HD == 72, true>), dim3(cdiv(T, 160) * H * B), dim3(320), 0, st, a);
     else if (kind == 12)  // dev: pipelined + lazy + ones
         hipLaunchKernelGGL((attn_pipe_kernel<HD, 8, 3, true, HD == 72, true>), dim3(cdiv(T, 256) * H * B), dim3(512), 0, st, a);
     else
@@ -1148,9 +1154,14 @@ extern "C" int mme_attention(const void* qkv, int ld_qkv, void* out, int ld_out,
     // its 3 spilled registers live outside the tile loop), so two 8-wave blocks share a CU and
     // each SIMD interleaves 4 waves: 1.18 -> 0.98 ms per 256-image layer (532 -> 638 TF/s).
     // At head dim 80 the same cap spills inside the loop and gains nothing (DFN5B 0.628 / 0.622 ms).
+    // 9-wave blocks (288 queries, kind 21) when they pad far less than 256 / 128-query blocks: ViT-H
+    // (T 257, hd 80) runs one block per batch-head, K/V staged once instead of three times and 288
+    // padded query rows instead of 384: 0.342 -> 0.277 ms per 256-image layer (253 -> 313 TF/s).
+    const long pad8 = (long)cdiv(T, 256) * 256, pad4 = (long)cdiv(T, 128) * 128, pad9 = (long)cdiv(T, 288) * 288;
     int kind = T <= 64 ? 16
                : (T <= 128 || hd == 64) ? 0
-               : ((long)cdiv(T, 256) * 256 * 10 <= (long)cdiv(T, 128) * 128 * 11 ? (hd == 72 ? 17 : 11) : 14);
+               : pad9 * 10 < min(pad8, pad4) * 9 ? 21
+               : (pad8 * 10 <= pad4 * 11 ? (hd == 72 ? 17 : 11) : 14);
     if (g_attn_variant >= 1 && g_attn_variant <= 4 && hd == 72) {  // dev-only diagnostic builds
         const dim3 grid(cdiv(T, 128) * H * B);
         switch (g_attn_variant) {
@@ -1162,7 +1173,7 @@ extern "C" int mme_attention(const void* qkv, int ld_qkv, void* out, int ld_out,
         return mme_check_launch("mme_attention");
     }
     if (g_attn_variant >= 9 && g_attn_variant <= 16) kind = g_attn_variant - 9;  // dev: force a kernel
-    if (g_attn_variant >= 30 && g_attn_variant <= 49) kind = g_attn_variant - 30;  // dev: force a kernel
+    if (g_attn_variant >= 30 && g_attn_variant <= 59) kind = g_attn_variant - 30;  // dev: force a kernel
     if ((kind == 16 || kind == 19) && T > 64) kind = 0;  // the short kernels hold one 64-key tile
     if (g_attn_variant >= 21 && g_attn_variant <= 26 && hd == 72) {  // dev: attn_dma_kernel<72,8,2> diagnostics
         const dim3 grid(cdiv(T, 256) * H * B), blk(512);

@@ -106,7 +106,9 @@ def attn_ref(qkv, B, T, H, hd, lens, causal, scale):
     (3, 64, 5, 64, True, None),
     (3, 77, 12, 64, True, None),       # CLIP-L text
     (3, 77, 16, 64, True, [77, 9, 40]),
-    (2, 257, 16, 80, False, None),     # ViT-H/14-224
+    (2, 257, 16, 80, False, None),     # ViT-H/14-224 (9-wave blocks, one per batch-head)
+    (2, 270, 3, 80, True, [270, 100]),  # 9-wave blocks: causal + padding
+    (2, 257, 2, 72, False, [257, 200]),  # 9-wave blocks at hd 72 (ones column of V^T)
     (1, 730, 4, 80, False, None),      # DFN5B-H-378
     (2, 577, 4, 64, False, None),      # CLIP-L-336
     (3, 17, 4, 80, False, None),
