@@ -1113,6 +1113,14 @@ void launch_attn(int kind, const AttnArgs& a, int B, int T, int H, hipStream_t s
         hipLaunchKernelGGL((attn_pipe_kernel<HD, 3, 2, false, HD == 72, true>), dim3(cdiv(T, 96) * H * B), dim3(192), 0, st, a);
     else if (kind == 21)  // 9 waves = 288 queries per block (T = 257 in one block per batch-head)
         hipLaunchKernelGGL((attn_pipe_kernel<HD, 9, 2, false, HD == 72, true>), dim3(cdiv(T, 288) * H * B), dim3(576), 0, st, a);
+    else if (kind == 23)  // 12 waves = 384 queries per block (hd 80, T = 730: two blocks per batch-head)
+        hipLaunchKernelGGL((attn_pipe_kernel<HD, 12, 2, false, HD == 72, true>), dim3(cdiv(T, 384) * H * B), dim3(768), 0, st, a);
+    else if (kind == 24)  // dev: 12 waves, 3 waves / SIMD register budget (hd 72 T 729: 1.033 ms vs 1.03-1.07, noise)
+        hipLaunchKernelGGL((attn_pipe_kernel<HD, 12, 2, false, HD == 72, true, false, 3>), dim3(cdiv(T, 384) * H * B), dim3(768), 0, st, a);
+    else if (kind == 25)  // dev: 12 waves, 3-stage ring (slower: LDS occupancy)
+        hipLaunchKernelGGL((attn_pipe_kernel<HD, 12, 3, false, HD == 72, true>), dim3(cdiv(T, 384) * H * B), dim3(768), 0, st, a);
+    else if (kind == 26)  // dev: 9 waves, 3-stage ring
+        hipLaunchKernelGGL((attn_pipe_kernel<HD, 9, 3, false, HD == 72, true>), dim3(cdiv(T, 288) * H * B), dim3(576), 0, st, a);
     else if (kind == 22)  // dev: 5 waves = 160 queries per block
         hipLaunchKernelGGL((attn_pipe_kernel<HD, 5, 2, false, HD == 72, true>), dim3(cdiv(T, 160) * H * B), dim3(320), 0, st, a);
     else if (kind == 12)  // dev: pipelined + lazy + ones
@@ -1157,10 +1165,15 @@ extern "C" int mme_attention(const void* qkv, int ld_qkv, void* out, int ld_out,
     // 9-wave blocks (288 queries, kind 21) when they pad far less than 256 / 128-query blocks: ViT-H
     // (T 257, hd 80) runs one block per batch-head, K/V staged once instead of three times and 288
     // padded query rows instead of 384: 0.342 -> 0.277 ms per 256-image layer (253 -> 313 TF/s).
+    // Head dim 80: 12-wave blocks (384 queries, kind 23) where they pad no more than 256-query
+    // blocks. The 133-VGPR hd-80 build fits 3 waves per SIMD, which 8-wave blocks leave at 2
+    // (one block per CU either way): DFN5B (T 730) 0.640 -> 0.558 ms per 128-image layer.
     const long pad8 = (long)cdiv(T, 256) * 256, pad4 = (long)cdiv(T, 128) * 128, pad9 = (long)cdiv(T, 288) * 288;
+    const long pad12 = (long)cdiv(T, 384) * 384;
     int kind = T <= 64 ? 16
                : (T <= 128 || hd == 64) ? 0
                : pad9 * 10 < min(pad8, pad4) * 9 ? 21
+               : (hd == 80 && pad12 <= pad8 && pad12 * 10 <= pad4 * 11) ? 23
                : (pad8 * 10 <= pad4 * 11 ? (hd == 72 ? 17 : 11) : 14);
     if (g_attn_variant >= 1 && g_attn_variant <= 4 && hd == 72) {  // dev-only diagnostic builds
         const dim3 grid(cdiv(T, 128) * H * B);

@@ -109,7 +109,8 @@ def attn_ref(qkv, B, T, H, hd, lens, causal, scale):
     (2, 257, 16, 80, False, None),     # ViT-H/14-224 (9-wave blocks, one per batch-head)
     (2, 270, 3, 80, True, [270, 100]),  # 9-wave blocks: causal + padding
     (2, 257, 2, 72, False, [257, 200]),  # 9-wave blocks at hd 72 (ones column of V^T)
-    (1, 730, 4, 80, False, None),      # DFN5B-H-378
+    (1, 730, 4, 80, False, None),      # DFN5B-H-378 (12-wave blocks)
+    (2, 700, 2, 80, True, [700, 390]),  # 12-wave blocks: causal + padding
     (2, 577, 4, 64, False, None),      # CLIP-L-336
     (3, 17, 4, 80, False, None),
     (4, 16, 8, 72, False, [16, 5, 9, 13]),
