@@ -35,7 +35,7 @@ extern "C" {
 #define MME_ERR_HIP 2         /* HIP runtime error at launch               */
 #define MME_ERR_UNSUPPORTED 3 /* valid request this build does not handle  */
 
-#define MME_ABI_VERSION 4
+#define MME_ABI_VERSION 5
 
 /* activation codes for mme_gemm (HF config.hidden_act) */
 #define MME_ACT_NONE 0
@@ -103,6 +103,19 @@ int mme_gemm(const void* A, int lda, const void* B, int ldb, void* C, int ldc, i
  * bf16 out; same shape rules as mme_gemm. */
 int mme_gemm_lnfold(const void* A, int lda, const void* B, int ldb, void* C, int ldc, int M, int N, int K,
                     const float* row_stats, const float* col_sum, const float* bias_f32, int act, void* stream);
+
+/* Residual GEMM that also leaves the next LayerNorm's statistics: C = A . B^T + bias +
+ * residual (bf16, as mme_gemm with res_period 0, act NONE) and row_stats = [M][2]
+ * (mean, rsqrt(var + eps)) of the bf16 rows of C, i.e. what mme_rowstats(C) returns
+ * up to fp32 summation order. The pipelined kernel's epilogue reduces each 128-column
+ * slice of every output row two-pass into row_part = [M][N / 128][2] (mean, M2;
+ * caller-provided scratch) and a per-row pass combines the slices (Chan), so the
+ * residual stream is not re-read. Replaces the o_proj / fc2 residual adds followed by
+ * layer_norm2 / the next layer's layer_norm1 (TF:models/siglip/modeling_siglip.py:341-357)
+ * on the LayerNorm-folded path. N % 128 == 0. */
+int mme_gemm_res_stats(const void* A, int lda, const void* B, int ldb, void* C, int ldc, int M, int N, int K,
+                       const void* bias, const void* residual, int ldr, float eps, float* row_part,
+                       float* row_stats, void* stream);
 
 /* LayerNorm statistics per row: stats[2r] = mean, stats[2r+1] = rsqrt(var + eps)
  * (fp32, biased variance; the arithmetic of mme_layernorm) for mme_gemm_lnfold. */

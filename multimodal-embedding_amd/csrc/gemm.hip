@@ -40,6 +40,9 @@ struct GemmArgs {
     const float* ln_stats;  // [M][2] (mean, rstd) of the A rows, or null
     const float* ln_cs;     // [N] column sums of the folded weight
     const float* ln_b;      // [N] folded bias (fp32)
+    // mme_gemm_res_stats: per 128-column slice of every output row, (mean, M2) of the
+    // bf16 outputs -> row_part[M][N / 128][2] (pipelined kernel, residual epilogue only)
+    float* row_part;
 };
 
 template <class C, int GROUP_M>
@@ -135,6 +138,16 @@ struct PCfg {
     static_assert(PPW * NW == PIECES, "stage must split evenly into 1 KiB pieces per wave");
 };
 
+
+// Sum over the 16 lanes of a DPP row (every lane gets the total; fp add commutes, so all
+// lanes of the row hold the same bits): quad_perm [1,0,3,2], [2,3,0,1], row_half_mirror, row_mirror.
+__device__ __forceinline__ float row16_sum(float v) {
+    v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0xB1, 0xF, 0xF, false));
+    v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x4E, 0xF, 0xF, false));
+    v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x141, 0xF, 0xF, false));
+    v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x140, 0xF, 0xF, false));
+    return v;
+}
 
 // Shared epilogue of the pipelined kernels: bias + activation in registers,
 // bf16 tile staged in LDS (row pitch BN*2+16 B), 16-B stores with the
@@ -249,6 +262,22 @@ __device__ __forceinline__ void gemm_epilogue_lds(const GemmArgs& p, char* lds, 
 #pragma unroll
             for (int e = 0; e < 8; ++e) o[e] = __builtin_bit_cast(unsigned short, f2bf(bits2f(v[e]) + bits2f(rv[q][e])));
             __builtin_nontemporal_store(o, reinterpret_cast<u16x8*>(Cout + (size_t)gr * p.ldc + gc));
+            if (p.row_part) {
+                // LayerNorm statistics of the next layer, two-pass per 128-column slice: the 16
+                // lanes of a DPP row hold one slice of one output row (16 B each; slices align
+                // with lane groups because CPR and NT are multiples of 16, and N % 128 == 0)
+                float xf[8], sum = 0.f;
+#pragma unroll
+                for (int e = 0; e < 8; ++e) sum += (xf[e] = bits2f(o[e]));
+                const float mean = row16_sum(sum) * (1.f / 128.f);
+                float m2 = 0.f;
+#pragma unroll
+                for (int e = 0; e < 8; ++e) m2 += (xf[e] - mean) * (xf[e] - mean);
+                m2 = row16_sum(m2);
+                if ((cc & 15) == 0)
+                    *reinterpret_cast<float2*>(p.row_part + 2 * ((size_t)gr * (p.N >> 7) + (gc >> 7))) =
+                        make_float2(mean, m2);
+            }
         } else if (EDIAG == 1) {
             asm volatile("" ::"v"(v));
         } else if (EDIAG == 3) {  // dev: plain (temporal) stores, for A/B against the NT default
@@ -1071,8 +1100,64 @@ extern "C" int mme_gemm(const void* A, int lda, const void* B, int ldb, void* Cp
     MME_REQUIRE(!residual || ldr >= N, "mme_gemm: ldr < N");
     MME_REQUIRE(res_period >= 0, "mme_gemm: res_period < 0");
     GemmArgs a{(const bf16*)A, (const bf16*)B, Cp, (const bf16*)bias, (const bf16*)residual,
-               lda, ldb, ldc, ldr, M, N, K, res_period, act, out_f32, 0, nullptr, nullptr, nullptr};
+               lda, ldb, ldc, ldr, M, N, K, res_period, act, out_f32, 0, nullptr, nullptr, nullptr, nullptr};
     return gemm_dispatch(a, as_stream(stream));
+}
+
+namespace {
+// (mean_i, M2_i) of the N / 128 slices of a row -> (mean, rstd), Chan's pairwise combination
+// for equal slice counts: mean = avg(mean_i), M2 = sum M2_i + 128 * sum (mean_i - mean)^2.
+__global__ __launch_bounds__(256) void row_part_combine_kernel(const float* __restrict__ part, float* __restrict__ st,
+                                                               int rows, int nparts, float eps) {
+    const int r = blockIdx.x * 256 + threadIdx.x;
+    if (r >= rows) return;
+    const float2* pr = reinterpret_cast<const float2*>(part) + (size_t)r * nparts;
+    float s = 0.f;
+    for (int i = 0; i < nparts; ++i) s += pr[i].x;
+    const float mean = s / nparts;
+    float m2 = 0.f, dev = 0.f;
+    for (int i = 0; i < nparts; ++i) {
+        const float2 v = pr[i];
+        m2 += v.y;
+        dev += (v.x - mean) * (v.x - mean);
+    }
+    const float var = (m2 + 128.f * dev) / (128.f * nparts);
+    *reinterpret_cast<float2*>(st + 2 * (size_t)r) = make_float2(mean, rsqrtf(var + eps));
+}
+}  // namespace
+
+extern "C" int mme_gemm_res_stats(const void* A, int lda, const void* B, int ldb, void* Cp, int ldc, int M, int N,
+                                  int K, const void* bias, const void* residual, int ldr, float eps, float* row_part,
+                                  float* row_stats, void* stream) {
+    MME_REQUIRE(A && B && Cp && residual && row_part && row_stats, "mme_gemm_res_stats: null operand");
+    MME_REQUIRE(M > 0 && N > 0 && K > 0, "mme_gemm_res_stats: empty shape M=%d N=%d K=%d", M, N, K);
+    MME_REQUIRE(K % BK == 0, "mme_gemm_res_stats: K=%d must be a multiple of %d", K, BK);
+    MME_REQUIRE(N % 128 == 0, "mme_gemm_res_stats: N=%d must be a multiple of 128", N);
+    MME_REQUIRE(lda % 8 == 0 && ldb % 8 == 0 && lda >= K && ldb >= K && ldc >= N && ldr >= N,
+                "mme_gemm_res_stats: bad leading dims");
+    MME_REQUIRE(((uintptr_t)A & 15) == 0 && ((uintptr_t)B & 15) == 0, "mme_gemm_res_stats: A/B must be 16-byte aligned");
+    MME_REQUIRE(((uintptr_t)row_part & 7) == 0 && ((uintptr_t)row_stats & 7) == 0,
+                "mme_gemm_res_stats: row_part / row_stats must be 8-byte aligned");
+    hipStream_t s = as_stream(stream);
+    GemmArgs a{(const bf16*)A, (const bf16*)B, Cp, (const bf16*)bias, (const bf16*)residual,
+               lda, ldb, ldc, ldr, M, N, K, 0, MME_ACT_NONE, 0, 0, nullptr, nullptr, nullptr, row_part};
+    const bool fused = g_variant < 0 && ldc % 8 == 0 && ((uintptr_t)Cp & 15) == 0 && ldr % 8 == 0 &&
+                       ((uintptr_t)residual & 15) == 0 && (long)M * N >= 1024L * 1024;
+    if (!fused) {  // shapes the pipelined kernel does not take: GEMM, then the row statistics pass
+        a.row_part = nullptr;
+        const int rc = gemm_dispatch(a, s);
+        if (rc != MME_OK) return rc;
+        return mme_rowstats(Cp, ldc, M, N, eps, row_stats, stream);
+    }
+    if (N % 256 == 128)
+        launch_pipe6<Pipe256, 4, 1, 0, true>(a, s);
+    else
+        launch_pipe6<Pipe256, 4, 1>(a, s);
+    const int rc = mme_check_launch("mme_gemm_res_stats");
+    if (rc != MME_OK) return rc;
+    hipLaunchKernelGGL(row_part_combine_kernel, dim3(cdiv(M, 256)), dim3(256), 0, s, row_part, row_stats, M, N / 128,
+                       eps);
+    return mme_check_launch("mme_gemm_res_stats");
 }
 
 extern "C" int mme_gemm_lnfold(const void* A, int lda, const void* B, int ldb, void* Cp, int ldc, int M, int N,
@@ -1087,7 +1172,7 @@ extern "C" int mme_gemm_lnfold(const void* A, int lda, const void* B, int ldb, v
     MME_REQUIRE(((uintptr_t)col_sum & 15) == 0 && ((uintptr_t)bias_f32 & 15) == 0 && ((uintptr_t)row_stats & 7) == 0,
                 "mme_gemm_lnfold: col_sum / bias_f32 must be 16-byte and row_stats 8-byte aligned");
     GemmArgs a{(const bf16*)A, (const bf16*)B, Cp, nullptr, nullptr, lda, ldb, ldc, 0, M, N, K, 0, act, 0, 0,
-               row_stats, col_sum, bias_f32};
+               row_stats, col_sum, bias_f32, nullptr};
     return gemm_dispatch(a, as_stream(stream));
 }
 

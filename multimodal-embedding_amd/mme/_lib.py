@@ -16,7 +16,7 @@ LIB_PATH = os.environ.get("MME_LIB", os.path.join(_HERE, "libmme.so"))
 # MME_ACT_* / MME_PIX_* from include/mme.h
 ACT_NONE, ACT_GELU_TANH, ACT_QUICK_GELU, ACT_GELU_ERF, ACT_GEGLU_TANH = 0, 1, 2, 3, 4
 PIX_F32_NCHW, PIX_PATCHES = 0, 1
-ABI_VERSION = 4
+ABI_VERSION = 5
 
 # name -> (restype, argtypes)
 _P = c_void_p
@@ -31,6 +31,8 @@ SIGNATURES = {
                          _P]),
     "mme_gemm_lnfold": (c_int, [_P, c_int, _P, c_int, _P, c_int, c_int, c_int, c_int, _P, _P, _P, c_int, _P]),
     "mme_rowstats": (c_int, [_P, c_int, c_int, c_int, c_float, _P, _P]),
+    "mme_gemm_res_stats": (c_int, [_P, c_int, _P, c_int, _P, c_int, c_int, c_int, c_int, _P, _P, c_int, c_float, _P,
+                                   _P, _P]),
     "mme_layernorm": (c_int, [_P, c_int, _P, _P, _P, c_int, c_int, c_int, c_float, _P, _P]),
     "mme_attention": (c_int, [_P, c_int, _P, c_int, c_int, c_int, c_int, c_int, _P, c_int, c_float, _P]),
     "mme_probe_attention": (c_int, [_P, _P, c_int, _P, c_int, c_int, c_int, c_int, c_int, c_float, _P]),

@@ -27,6 +27,9 @@ BF16 = torch.bfloat16
 # LayerNorm -> Linear pairs run as mme_rowstats + mme_gemm_lnfold (the normalised rows are
 # never written); MME_LN_FOLD=0 restores mme_layernorm + mme_gemm
 LN_FOLD = os.environ.get("MME_LN_FOLD", "1") != "0"
+# the o_proj / fc2 residual GEMMs leave the next LayerNorm's row statistics
+# (mme_gemm_res_stats) instead of a separate mme_rowstats pass over the residual stream
+FUSED_STATS = os.environ.get("MME_FUSED_STATS", "1") != "0"
 
 
 class _Bufs:
@@ -42,11 +45,19 @@ class _Bufs:
         self.hq = mx.MXTensor.empty(rows, d, device) if fp8 else None
         self.midq = mx.MXTensor.empty(rows, cfg.inter_pad, device) if fp8 else None
         self.stats = torch.empty(rows, 2, dtype=torch.float32, device=device)
+        # per-128-column (mean, M2) slices of the residual GEMMs' output rows (mme_gemm_res_stats)
+        self.part = torch.empty(rows, max(1, d // 128), 2, dtype=torch.float32, device=device) \
+            if FUSED_STATS and d % 128 == 0 else None
 
 
 def encoder_layer(x: torch.Tensor, L: LayerW, cfg: TowerConfig, B: int, T: int, bufs: _Bufs, *,
-                  seq_lens: Optional[torch.Tensor] = None, causal: bool = False) -> None:
-    """Pre-LN transformer block, in place on x (SiglipEncoderLayer.forward, TF:…siglip.py:341-357)."""
+                  seq_lens: Optional[torch.Tensor] = None, causal: bool = False, stats_in: bool = False,
+                  stats_out: bool = False) -> bool:
+    """Pre-LN transformer block, in place on x (SiglipEncoderLayer.forward, TF:…siglip.py:341-357).
+
+    LayerNorm-folded path: stats_in = bufs.stats already holds x's row statistics (left by
+    the previous layer's fc2); stats_out = leave the statistics of the output x there for
+    the next layer. Returns whether it did (mme_gemm_res_stats on the fc2 residual GEMM)."""
     d, H, hd = cfg.hidden, cfg.heads, cfg.head_dim
     act = ACTS[cfg.act]
     if L.mx is not None:  # fp8 mode: QKV / fc1 / fc2 on the block-scaled fp8 MFMA (mme/mx.py)
@@ -58,19 +69,27 @@ def encoder_layer(x: torch.Tensor, L: LayerW, cfg: TowerConfig, B: int, T: int, 
         hq = mx.layernorm(x, L.ln2_g, L.ln2_b, cfg.eps, out=bufs.hq)
         midq = mx.gemm(hq, L.mx.fc1, L.fc1_b, act=act, out_mx=bufs.midq, algo_flops=mlp_flops)
         mx.gemm(midq, L.mx.fc2, L.fc2_b, residual=x, out=x, algo_flops=mlp_flops)
-        return
+        return False
     mlp_flops = 2.0 * x.shape[0] * d * cfg.intermediate  # unpadded intermediate width
     if LN_FOLD:  # layer_norm1 -> qkv and layer_norm2 -> fc1 folded (mme.h mme_gemm_lnfold)
         if L.fold is None:
             L.fold = (ops.LNFolded(L.qkv_w, L.qkv_b, L.ln1_g, L.ln1_b), ops.LNFolded(L.fc1_w, L.fc1_b, L.ln2_g, L.ln2_b))
-        st = ops.rowstats(x, cfg.eps, d=d, out=bufs.stats)
+        fused = bufs.part is not None
+        st = bufs.stats if (stats_in and fused) else ops.rowstats(x, cfg.eps, d=d, out=bufs.stats)
         qkv = ops.gemm_lnfold(x, L.fold[0], st, out=bufs.wide[:, : 3 * d])
         a = ops.attention(qkv, B, T, H, hd, seq_lens=seq_lens, causal=causal, out=bufs.h)
-        ops.gemm(a, L.o_w, L.o_b, residual=x, out=x)
-        st = ops.rowstats(x, cfg.eps, d=d, out=bufs.stats)
+        if fused:  # o_proj + residual, with layer_norm2's statistics from the epilogue
+            ops.gemm_res_stats(a, L.o_w, L.o_b, x, cfg.eps, bufs.stats, bufs.part, out=x)
+            st = bufs.stats
+        else:
+            ops.gemm(a, L.o_w, L.o_b, residual=x, out=x)
+            st = ops.rowstats(x, cfg.eps, d=d, out=bufs.stats)
         mid = ops.gemm_lnfold(x, L.fold[1], st, act=act, out=bufs.wide[:, : cfg.inter_pad], algo_flops=mlp_flops)
+        if fused and stats_out:
+            ops.gemm_res_stats(mid, L.fc2_w, L.fc2_b, x, cfg.eps, bufs.stats, bufs.part, out=x, algo_flops=mlp_flops)
+            return True
         ops.gemm(mid, L.fc2_w, L.fc2_b, residual=x, out=x, algo_flops=mlp_flops)
-        return
+        return False
     h = ops.layernorm(x, L.ln1_g, L.ln1_b, cfg.eps, out=bufs.h)
     qkv = ops.gemm(h, L.qkv_w, L.qkv_b, out=bufs.wide[:, : 3 * d])
     a = ops.attention(qkv, B, T, H, hd, seq_lens=seq_lens, causal=causal, out=bufs.h)
@@ -78,6 +97,7 @@ def encoder_layer(x: torch.Tensor, L: LayerW, cfg: TowerConfig, B: int, T: int, 
     h = ops.layernorm(x, L.ln2_g, L.ln2_b, cfg.eps, out=bufs.h)
     mid = ops.gemm(h, L.fc1_w, L.fc1_b, act=act, out=bufs.wide[:, : cfg.inter_pad], algo_flops=mlp_flops)
     ops.gemm(mid, L.fc2_w, L.fc2_b, residual=x, out=x, algo_flops=mlp_flops)
+    return False
 
 
 class VisionTower:
@@ -99,8 +119,7 @@ class VisionTower:
             x = ops.clip_embed_ln(pe, w.cls, w.pos, w.pre_ln_g, w.pre_ln_b, cfg.eps, B, P)
             del pe
         bufs = _Bufs(B * T, cfg, dev, fp8=w.layers[0].mx is not None)
-        for L in w.layers:
-            encoder_layer(x, L, cfg, B, T, bufs)
+        run_layers(x, w.layers, cfg, B, T, bufs)
         if self.spec.family == "siglip":
             return self._map_head(x, B, T, bufs)
         rows = torch.arange(B, device=dev, dtype=torch.int32) * T  # CLS rows
@@ -115,8 +134,7 @@ class VisionTower:
         x = ops.gemm(patches, w.patch_w, w.patch_b, residual=w.pos, res_period=P,
                      algo_flops=2.0 * B * P * d * 3 * cfg.patch ** 2)
         bufs = _Bufs(B * P, cfg, patches.device)
-        for L in w.layers:
-            encoder_layer(x, L, cfg, B, P, bufs)
+        run_layers(x, w.layers, cfg, B, P, bufs)
         return ops.layernorm(x, w.post_ln_g, w.post_ln_b, cfg.eps, out=bufs.h)
 
     def _map_head(self, x, B, T, bufs) -> torch.Tensor:
@@ -142,8 +160,7 @@ class TextTower:
         B, L = ids.shape
         x = ops.token_embed(ids, w.tok, w.pos)
         bufs = _Bufs(B * L, cfg, ids.device, fp8=self.w.layers[0].mx is not None)
-        for layer in w.layers:
-            encoder_layer(x, layer, cfg, B, L, bufs, seq_lens=seq_lens, causal=cfg.causal)
+        run_layers(x, w.layers, cfg, B, L, bufs, seq_lens=seq_lens, causal=cfg.causal)
         mode = {"eos": 0, "argmax": 1, "last": 2}[cfg.pool]
         rows = ops.text_pool_rows(ids, cfg.eos_id, mode)
         pooled = ops.layernorm(x, w.final_ln_g, w.final_ln_b, cfg.eps, rows_idx=rows)
@@ -250,6 +267,13 @@ def _seq_lens(attention_mask: Optional[torch.Tensor], B: int, L: int, device) ->
     if int(lens.min()) == L:
         return None
     return lens
+
+
+def run_layers(x: torch.Tensor, layers, cfg: TowerConfig, B: int, T: int, bufs: _Bufs, **kw) -> None:
+    """The encoder stack; each layer's fc2 hands the next layer its LayerNorm statistics."""
+    have = False
+    for i, L in enumerate(layers):
+        have = encoder_layer(x, L, cfg, B, T, bufs, stats_in=have, stats_out=i + 1 < len(layers), **kw)
 
 
 class DualEncoder:

@@ -137,6 +137,33 @@ def gemm(a: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None, 
     return out
 
 
+def gemm_res_stats(a: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor], residual: torch.Tensor,
+                   eps: float, stats: torch.Tensor, part: torch.Tensor, *, out: Optional[torch.Tensor] = None,
+                   algo_flops: Optional[float] = None) -> torch.Tensor:
+    """out = a @ w.T + bias + residual (bf16) and stats = rowstats(out, eps), the statistics
+    reduced in the GEMM epilogue (mme_gemm_res_stats). part: fp32 scratch >= [M, N / 128, 2]."""
+    _dev(a, w, bias, residual, stats, part, out)
+    M, K = a.shape
+    N = w.shape[0]
+    if w.shape[1] != K or residual.shape[0] < M or stats.shape[0] < M:
+        raise ValueError(f"gemm_res_stats: a {tuple(a.shape)} vs w {tuple(w.shape)} / residual / stats")
+    if N % 128 or part.dtype != torch.float32 or not part.is_contiguous() or part.numel() < M * (N // 128) * 2:
+        raise ValueError("gemm_res_stats: N % 128 != 0 or part is not contiguous fp32 >= [M, N / 128, 2]")
+    if stats.dtype != torch.float32 or not stats.is_contiguous():
+        raise ValueError("gemm_res_stats: stats must be contiguous fp32 [M, 2]")
+    if bias is not None and bias.numel() < N:
+        raise ValueError("gemm_res_stats: bias shorter than N")
+    if out is None:
+        out = torch.empty(M, N, dtype=BF16, device=a.device)
+    ev = KernelTimer.begin()
+    call("mme_gemm_res_stats", a.data_ptr(), _rowmajor(a, "a"), w.data_ptr(), _rowmajor(w, "w"), out.data_ptr(),
+         _rowmajor(out, "out"), M, N, K, _ptr(bias), residual.data_ptr(), _rowmajor(residual, "residual"),
+         float(eps), part.data_ptr(), stats.data_ptr(), _stream())
+    KernelTimer.end(ev, "gemm", algo_flops if algo_flops is not None else 2.0 * M * N * K,
+                    2.0 * (M * K + N * K + M * N))
+    return out
+
+
 def rowstats(x: torch.Tensor, eps: float, *, d: Optional[int] = None,
              out: Optional[torch.Tensor] = None) -> torch.Tensor:
     """LayerNorm statistics [rows, 2] fp32 = (mean, rsqrt(var + eps)) over the first d columns."""

@@ -205,6 +205,35 @@ def test_gemm_lnfold(cuda, M, N, K, act):
     assert e_fold <= 1.5 * e_unf + 1e-4, (e_fold, e_unf)
 
 
+# mme_gemm_res_stats: the residual GEMM's output is bit-identical to mme_gemm's, and the
+# row statistics reduced in its epilogue (128-column slices, Chan-combined) match a separate
+# mme_rowstats pass over that output up to fp32 summation order. Shapes: split grid
+# (N = 1152), whole 256-column tiles (N = 1280), the non-pipelined fallback (M * N < 1M),
+# and a shifted residual stream (mean >> std: the two-pass slices keep the variance exact).
+@pytest.mark.parametrize("M,N,K,shift", [(4096, 1152, 1152, 0.0), (3000, 1280, 512, 0.0), (100, 256, 64, 0.0),
+                                         (2048, 1152, 4352, 40.0)])
+def test_gemm_res_stats(cuda, M, N, K, shift):
+    g = torch.Generator(device="cuda").manual_seed(M + N + K)
+    a = rnd(M, K, gen=g)
+    w = rnd(N, K, scale=1 / math.sqrt(K), gen=g)
+    b = rnd(N, scale=0.1, gen=g)
+    x = (rnd(M, N, scale=2.0, gen=g).float() + shift).to(torch.bfloat16)
+    ref_out = ops.gemm(a, w, b, residual=x)
+    st = torch.empty(M, 2, dtype=torch.float32, device="cuda")
+    part = torch.full((M, N // 128, 2), float("nan"), dtype=torch.float32, device="cuda")
+    out = ops.gemm_res_stats(a, w, b, x.clone(), 1e-6, st, part)
+    assert torch.equal(out, ref_out), "mme_gemm_res_stats output differs from mme_gemm"
+    if M * N >= 1 << 20:  # the pipelined kernel's epilogue wrote every slice (not the fallback pass)
+        assert torch.isfinite(part).all(), "fused epilogue statistics not written"
+    ref_st = ops.rowstats(ref_out, 1e-6)
+    torch.testing.assert_close(st[:, 0], ref_st[:, 0], rtol=1e-5, atol=1e-5)
+    torch.testing.assert_close(st[:, 1], ref_st[:, 1], rtol=1e-4, atol=0)
+    # in place on the residual stream, as the encoder layers run it
+    xi = x.clone()
+    ops.gemm_res_stats(a, w, b, xi, 1e-6, st, part, out=xi)
+    assert torch.equal(xi, ref_out)
+
+
 def test_l2norm_bit_exact(cuda, golden):
     g = golden("l2norm")
     x = bits_to_bf16(g["x"]).cuda()
