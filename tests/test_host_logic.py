@@ -11,7 +11,7 @@ from mme import REGISTRY, TINY, get_spec
 from mme.colpali import chunk_zero_flags
 from mme.config import image_flops, text_flops
 from mme.harness import METRIC_KEYS, write_csv
-from mme.models import _seq_lens, plan_text_batches
+from mme.models import _gemm_tiles, _seq_lens, balanced, plan_text_batches, tail_aware_batch
 from mme.processor import Processor, image_geometry, synthetic_caption_ids
 from oracle import pil_bicubic
 
@@ -139,3 +139,31 @@ def test_layernorm_fold_algebra():
     ref = torch.nn.functional.layer_norm(x, (K,), gamma.float(), beta.float(), 1e-6) @ w.float().T + b.float()
     torch.testing.assert_close(out, ref, atol=2e-2, rtol=2e-2)
     assert fold.w.dtype == torch.bfloat16 and fold.cs.dtype == torch.float32 and fold.b.dtype == torch.float32
+
+
+def test_gemm_tiles_matches_dispatch():
+    # 256 x 256 tiles; N = 256 k + 128 -> the last 128 columns as 512 x 128 tiles (gemm.hip split grid)
+    assert _gemm_tiles(256 * 10, 1024) == 40
+    assert _gemm_tiles(256 * 10 + 1, 1024) == 44
+    assert _gemm_tiles(256 * 10, 1152) == 40 + 5
+    assert _gemm_tiles(256 * 9, 1152) == 36 + 5
+    assert _gemm_tiles(256 * 4, 1100) == 4 * 5
+
+
+@pytest.mark.parametrize("name", ["SigLIP-400M", "LAION-CLIP-H", "Apple-DFN5B-H", "OpenAI-CLIP-L"])
+@pytest.mark.parametrize("n", [1, 7, 625, 1250, 5000, 25000])
+def test_tail_aware_batch(name, n):
+    spec = get_spec(name)
+    for cfg, rows, batch in ((spec.vision, spec.vision.num_patches + 1, 256), (spec.text, spec.text.max_pos, 2048)):
+        b = tail_aware_batch(n, batch, rows, cfg)
+        assert 1 <= b <= batch
+        nb = -(-n // b)
+        assert -(-n // balanced(n, batch)) <= nb <= -(-n // batch) + 3  # equal split, at most 3 extra batches
+        assert -(-n // nb) == b  # batches as equal as they can be
+    assert tail_aware_batch(n, 256, 729, None) == balanced(n, 256)
+
+
+def test_tail_aware_batch_siglip_shapes():
+    spec = get_spec("SigLIP-400M")
+    assert tail_aware_batch(5000, 256, 729, spec.vision) == 239  # o_proj / fc2: 12.0 waves of 256 tiles
+    assert tail_aware_batch(25000, 2048, 64, spec.text) == 1563
