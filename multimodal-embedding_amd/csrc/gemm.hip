@@ -1227,6 +1227,8 @@ int gemm_dispatch(GemmArgs a, hipStream_t s) {
             if (a.N % 256 == 128) return launch_pipe6<Pipe256, 4, 1, 0, true>(a, s);
             return launch_pipe6<Pipe256, 4, 1>(a, s);
         case 46: return launch_pipe6<PCfg<256, 256, 2, 4, 3>, 4, 1>(a, s);  // dev: 3-deep ring (2 stages ahead)
+        case 54: return launch_pipe6<Pipe256, 2, 1>(a, s);   // dev: 2-row tile bands
+        case 55: return launch_pipe6<Pipe256, 16, 1>(a, s);  // dev: 16-row tile bands
         case 50: return launch_pipe7<Pipe256w, 4>(a, s);
         case 51: return launch_pipe7<Pipe256w, 8>(a, s);
         case 52: return launch_pipe7<Pipe256w, 4, 1>(a, s);  // diagnostic: no DMA
