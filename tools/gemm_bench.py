@@ -32,7 +32,8 @@ def main():
     p.add_argument("--shapes", default="qkv,o_proj,fc1,fc2")
     p.add_argument("--mx", action="store_true", help="also time the mx8 (block-scaled fp8) GEMM")
     p.add_argument("--torch", action="store_true", help="also time torch F.linear (hipBLASLt) on each shape")
-    p.add_argument("--epi", default="none", help="epilogue: none | bias | res (residual in place) | gelu (bias+gelu_tanh)")
+    p.add_argument("--epi", default="none", help="epilogue: none | bias | res (residual in place) | resstats (res + LayerNorm "
+                   "statistics, mme_gemm_res_stats) | gelu (bias+gelu_tanh)")
     a = p.parse_args()
     lib = _lib.load()
     has_var = hasattr(lib, "mme_gemm_variant")
@@ -49,28 +50,36 @@ def main():
         W = (torch.randn(N, K, device="cuda", generator=g) / K ** 0.5).to(torch.bfloat16)
         C = torch.randn(M, N, device="cuda", generator=g).to(torch.bfloat16)
         bias = (torch.randn(N, device="cuda", generator=g) * 0.1).to(torch.bfloat16)
-        kw = {"none": {}, "bias": {"bias": bias}, "res": {"bias": bias, "residual": C},
+        kw = {"none": {}, "bias": {"bias": bias}, "res": {"bias": bias, "residual": C}, "resstats": {},
               "gelu": {"bias": bias, "act": _lib.ACT_GELU_TANH}}[a.epi]
+        st = torch.empty(M, 2, device="cuda")
+        part = torch.empty(M, max(1, N // 128), 2, device="cuda")
+
+        def run():
+            if a.epi == "resstats":
+                ops.gemm_res_stats(A, W, bias, C, 1e-6, st, part, out=C)
+            else:
+                ops.gemm(A, W, out=C, **kw)
         ref = None
         for v in variants:
             if v >= 0:
                 lib.mme_gemm_variant(v)
-            ops.gemm(A, W, out=C, **kw)
-            if ref is None or a.epi == "res":
+            run()
+            if ref is None or a.epi in ("res", "resstats"):
                 ref = C.clone()
             else:
                 err = (C.float() - ref.float()).abs().max().item()
                 if v not in DIAG_VARIANTS:
                     assert err < 0.05, f"variant {v} differs: {err}"
             for _ in range(3):  # warm the clocks / caches for this variant
-                ops.gemm(A, W, out=C, **kw)
+                run()
             torch.cuda.synchronize()
             s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             ms = 1e30
             for rep in range(3):  # best of 3 timed groups
                 s.record()
                 for _ in range(a.iters):
-                    ops.gemm(A, W, out=C, **kw)
+                    run()
                 e.record()
                 torch.cuda.synchronize()
                 ms = min(ms, s.elapsed_time(e) / a.iters)
