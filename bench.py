@@ -54,6 +54,8 @@ def parse():
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline sample duration")
     p.add_argument("--no-kernel-timer", action="store_true")
+    p.add_argument("--no-parity", action="store_true",
+                   help="skip the post-run R@1 parity check of the job's embeddings against the oracle")
     p.add_argument("--host-inputs", action="store_true",
                    help="also time one job whose u8 images start in host memory (streamed H2D, SURVEY 8f-2); "
                         "reported as host_inputs_img_s, never as value")
@@ -83,35 +85,79 @@ def synth_inputs(spec, n, caps, device):
     return imgs, ids.to(torch.int64)
 
 
-def cpu_baseline(spec, seconds: float):
-    """The oracle's bf16 PyTorch-CPU restatement of the reference encoders, timed on
-    the host cores on a bounded sample, extrapolated to the job's images/sec."""
-    import numpy as np
+def cpu_baseline(spec, seconds: float, tables=None, caps_per_image: int = 5):
+    """The oracle's bf16 PyTorch-CPU restatement of the reference encoders (validated against the
+    reference's own main.encode_data in profiles/r02_cpu_baseline_check.json) at the reference's
+    batch size 32 (main.py:73,395), timed on the host cores on a bounded sample: whole batches of
+    images and captions until the time budget is spent (at least one of each), extrapolated to the
+    job's n images + 6n captions; plus the CPU retrieval of the job itself (oracle/retrieval.py:
+    fp32 matmul + ordered top-10 + recall, main.py:471-473,331-378), timed in full on the job's
+    own embedding tables."""
     from oracle import encoders as oe
+    from oracle import retrieval as R
     from mme.processor import synthetic_caption_ids, synthetic_images
     from mme.weights import random_state_dict
     sd = {k: v.cpu() for k, v in random_state_dict(spec, seed=0, device="cuda").items()}
     threads = torch.get_num_threads()
-    imgs = synthetic_images(64)
-    caps = synthetic_caption_ids(spec, 384).tolist()
-    bs = 8
+    bs = 32
+    imgs = synthetic_images(4 * bs)
+    caps = synthetic_caption_ids(spec, 32 * bs).tolist()
 
     def run(fn, items, budget):
         done, t0 = 0, time.time()
-        while done < len(items) and (time.time() - t0) < budget:
+        while done < len(items) and (done == 0 or (time.time() - t0) < budget):
             fn(items[done:done + bs])
             done += len(items[done:done + bs])
         return done, time.time() - t0
 
-    oe.encode_data(spec, sd, list(imgs[:1]), [], bs=1)  # warm the allocator / threads
+    oe.encode_data(spec, sd, list(imgs[:1]), caps[:1], bs=1)  # warm the allocator / threads
     ni, ti = run(lambda x: oe.encode_data(spec, sd, list(x), [], bs=bs), imgs, seconds * 0.6)
-    nc, tc = run(lambda x: oe.encode_data(spec, sd, [], x, bs=bs), caps, seconds * 0.4)
+    nc, tc = run(lambda x: oe.encode_data(spec, sd, [], x, bs=bs), caps, seconds * 0.25)
     img_s, cap_s = ni / ti, nc / tc
-    # whole job: n images + 6n captions (T2I + 5 per image); retrieval is < 1 % on the CPU here
-    per_img = 1.0 / img_s + 6.0 / cap_s
+    ret_s, n = 0.0, None
+    if tables is not None:
+        img, t2i, allc = (tables[k].float().cpu().numpy() for k in ("img", "t2i", "all"))
+        n = img.shape[0]
+        t0 = time.time()
+        for q, d, tc_ in ((t2i, img, 1), (img, allc, caps_per_image), (img, t2i, 1)):
+            R.recall(R.topk(R.scores(q, d), 10)[0], tc_)
+        ret_s = time.time() - t0
+    per_img = 1.0 / img_s + 6.0 / cap_s + (ret_s / n if n else 0.0)
     return {"value": round(1.0 / per_img, 4), "unit": "images/sec", "cores": threads, "kind": "port",
             "sample": f"oracle/encoders.py bf16 CPU, bs {bs}: {ni} images in {ti:.1f}s ({img_s:.2f} img/s) + "
-                      f"{nc} captions in {tc:.1f}s ({cap_s:.2f} cap/s), extrapolated to n images + 6n captions"}
+                      f"{nc} captions in {tc:.1f}s ({cap_s:.2f} cap/s), extrapolated to n images + 6n captions; "
+                      f"+ oracle retrieval of the job's own {n} x {caps_per_image * n if n else 0} tables "
+                      f"(T2I + I2T + Sym, top-10 + recall) {ret_s:.2f}s, timed in full",
+            "encode_img_s": round(img_s, 4), "encode_cap_s": round(cap_s, 3), "retrieval_s": round(ret_s, 3)}
+
+
+def retrieval_parity(tables, metrics, caps_per_image: int = 5):
+    """R@1 parity of the headline job (checker; runs after the timed region): the job's own
+    embedding tables ranked on the device (mme_sim_topk) vs the oracle (numpy fp32 matmul +
+    ordered top-k, oracle/retrieval.py restating main.py:471-473 and 331-378), row by row;
+    the job's device recall vs the oracle's recall of the same tables."""
+    sys.path.insert(0, ROOT)
+    from oracle import retrieval as R
+    from mme import ops
+    t0 = time.time()
+    host = {k: v.float().cpu().numpy() for k, v in tables.items()}
+    n = host["img"].shape[0]
+    rows = {}
+    ref_metrics = {}
+    for name, qk, dk, tc in (("T2I", "t2i", "img", 1), ("I2T", "img", "all", caps_per_image),
+                             ("I2T_Sym", "img", "t2i", 1)):
+        idx, _ = ops.sim_topk(tables[qk].contiguous(), tables[dk].contiguous(), 10)
+        ridx, rsc = R.topk(R.scores(host[qk], host[dk]), 11)
+        same, near = R.compare_topk(idx.cpu().numpy(), ridx, rsc)
+        rows[name] = {"rows_identical": f"{int(same.sum())}/{len(same)}", "near_tie_rows": int(near.sum()),
+                      "decisive_rows_differing": int((~same & ~near).sum())}
+        for k, h in zip((1, 5, 10), R.recall(ridx[:, :10], tc)):
+            ref_metrics[f"{name}_R@{k}"] = 100.0 * h / n
+    return {"recall_identical": all(ref_metrics[k] == metrics[k] for k in ref_metrics),
+            "oracle_recall": {k: round(v, 2) for k, v in ref_metrics.items()}, "rows": rows,
+            "near_tie_rule": "neighbouring oracle scores among the top 11 within 1e-5*|s1|",
+            "checker": "oracle/retrieval.py on the job's own embeddings (numpy fp32, host)",
+            "seconds": round(time.time() - t0, 2)}
 
 
 def colpali_captions(n: int, caps: int, seed: int = 1):
@@ -272,11 +318,20 @@ def main_colpali(args, rank, world, dev):
 
 def main():
     args = parse()
-    rank, world, local = (int(os.environ.get(k, d)) for k, d in (("RANK", 0), ("WORLD_SIZE", 1), ("LOCAL_RANK", 0)))
+    from mme import launch
+    if args.gpus > 1 and not launch.under_launcher():
+        # `python bench.py --gpus N` without torchrun: start N rank processes of this script
+        # BEFORE anything touches the GPU (this parent never initialises HIP), and exit with
+        # the first failing rank's status
+        sys.exit(launch.spawn_ranks(args.gpus, [os.path.abspath(__file__)] + sys.argv[1:]))
+    _, _, local = launch.env_rank_world()
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
-    if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+    try:
+        rank, world, local = launch.init_distributed(args.gpus, "nccl", dev)
+    except launch.LaunchError as e:
+        print(f"bench.py: {e}", file=sys.stderr, flush=True)
+        sys.exit(3)
     if args.model.startswith("ColPali"):
         if args.n_images == 5000 and "--n-images" not in sys.argv:
             args.n_images = 1000  # BASELINE configs[3]: 1 000 images x 5 000 captions
@@ -300,13 +355,24 @@ def main():
     torch.cuda.synchronize()
 
     last = {}
+    ev = {}
+
+    def mark(name):
+        e = torch.cuda.Event(enable_timing=True)
+        e.record()
+        ev[name] = e
 
     def step():
+        mark("t0")
         img = model.encode_images(my_imgs, batch=args.img_batch)
+        mark("img")
         t2i = model.encode_texts(my_t2i, exec_batch=args.txt_batch)
         allc = model.encode_texts(my_caps, exec_batch=args.txt_batch)
-        last.update(img=img, t2i=t2i, allc=allc)
-        return sharded_recall(img, t2i, allc, rank, world, n, caps)
+        mark("txt")
+        m, tables = sharded_recall(img, t2i, allc, rank, world, n, caps, return_tables=True)
+        mark("ret")
+        last.update(img=img, t2i=t2i, allc=allc, tables=tables)
+        return m
 
     for _ in range(args.warmup):
         metrics = step()
@@ -325,10 +391,15 @@ def main():
     barrier()
     dt = time.perf_counter() - t0
     ops.KernelTimer.stop()
+    # phases of the last timed step (device events on the launch stream), max over ranks
+    phases = torch.tensor([ev["t0"].elapsed_time(ev["img"]), ev["img"].elapsed_time(ev["txt"]),
+                           ev["txt"].elapsed_time(ev["ret"])], dtype=torch.float64, device=dev)
     if world > 1:
         t = torch.tensor([dt], device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
+        dist.all_reduce(phases, op=dist.ReduceOp.MAX)
+    phases = phases.tolist()
     kt = ops.KernelTimer.summary() if not args.no_kernel_timer else {}
 
     roofline = None
@@ -384,9 +455,16 @@ def main():
                    "image_size": spec.vision.image_size, "seq_len": spec.text.max_pos, "img_batch": args.img_batch,
                    "txt_batch": args.txt_batch, "global_batch": n, "parallelism": f"image-shard x{world}"},
         "recall": {k: round(v, 2) for k, v in metrics.items()},
+        # last timed step, device events, max over ranks; retrieval = all-gather (N > 1) + T2I / I2T /
+        # I2T-Sym similarity + fused top-10 + recall counters + counter all-reduce
+        "encode_images_s": round(phases[0] / 1e3, 4), "encode_texts_s": round(phases[1] / 1e3, 4),
+        "retrieval_s": round(phases[2] / 1e3, 4),
         "roofline": roofline,
+        "parity": None,
         "cpu_baseline": None,
     }
+    if rank == 0 and not args.no_parity:
+        out["parity"] = retrieval_parity(last["tables"], metrics, caps)
     if args.host_inputs:
         host_imgs = my_imgs.cpu().pin_memory()
         barrier()
@@ -412,7 +490,7 @@ def main():
                             "note": "full score matrices once + per-resample gather/top-10/recall on the device"}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         sys.path.insert(0, ROOT)
-        out["cpu_baseline"] = cpu_baseline(spec, args.cpu_seconds)
+        out["cpu_baseline"] = cpu_baseline(spec, args.cpu_seconds, last["tables"], caps)
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:

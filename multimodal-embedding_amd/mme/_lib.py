@@ -90,12 +90,17 @@ def load() -> ctypes.CDLL:
             f"libmme.so not found at {LIB_PATH}; build it with `make -C multimodal-embedding_amd` "
             "(or __graft_entry__.build()). There is no CPU fallback.")
     lib = ctypes.CDLL(LIB_PATH)
+    # version first: a stale library would otherwise fail below on a missing symbol
+    lib.mme_abi_version.restype, lib.mme_abi_version.argtypes = c_int, []
+    if lib.mme_abi_version() != ABI_VERSION:
+        raise MMEError(f"libmme ABI {lib.mme_abi_version()} at {LIB_PATH} != expected {ABI_VERSION}: stale "
+                       "library, rebuild with `make -C multimodal-embedding_amd`")
     for name, (res, args) in SIGNATURES.items():
-        fn = getattr(lib, name)
+        fn = getattr(lib, name, None)
+        if fn is None:
+            raise MMEError(f"{LIB_PATH} does not export {name}: rebuild with `make -C multimodal-embedding_amd`")
         fn.restype = res
         fn.argtypes = args
-    if lib.mme_abi_version() != ABI_VERSION:
-        raise MMEError(f"libmme ABI {lib.mme_abi_version()} != expected {ABI_VERSION}")
     _lib = lib
     return lib
 

@@ -63,43 +63,64 @@ class DeviceOps:
         return ops.recall_hits(idx, tgt_count, ks, row_offset=row_offset)
 
 
-def sharded_recall(img_l: torch.Tensor, t2i_l: torch.Tensor, all_l: torch.Tensor, rank: int, world: int,
-                   n_img: int, caps_per_image: int = 5, ks: Sequence[int] = KS, group=None,
-                   compute: Optional[object] = None) -> Dict[str, float]:
-    """Global R@k from per-rank shards (see module docstring)."""
+def rank_hit_counts(img_l: torch.Tensor, t2i_l: torch.Tensor, img_all: torch.Tensor, t2i_all: torch.Tensor,
+                    all_all: torch.Tensor, row_offset: int, caps_per_image: int = 5, ks: Sequence[int] = KS,
+                    compute: Optional[object] = None, return_idx: bool = False):
+    """One rank's share of the 9 hit counters: ITS rows ranked against the full tables.
+
+    T2I: the rank's caption-0 queries vs all images; I2T: its images vs all captions;
+    I2T-Sym: its images vs all T2I captions. ``row_offset`` = the rank's first global
+    image (targets are global indices). Returns int64 [3·len(ks)] (and the top-k
+    index tables when ``return_idx``)."""
     compute = compute or DeviceOps()
-    lo, _ = shard_range(n_img, rank, world)
-    img_all = all_gather_rows(img_l, world, group)
-    t2i_all = all_gather_rows(t2i_l, world, group)
-    all_all = all_gather_rows(all_l, world, group)
     kmax = max(ks)
-    res = []
+    res, idxs = [], {}
     for name, q, d, tcount in (("T2I", t2i_l, img_all, 1), ("I2T", img_l, all_all, caps_per_image),
                                ("I2T_Sym", img_l, t2i_all, 1)):
         k = min(kmax, d.shape[0])
         kk = [min(x, k) for x in ks]
         if q.shape[0]:
             idx = compute.topk(q, d, k)
-            h = compute.hits(idx, tcount, kk, lo)
+            h = compute.hits(idx, tcount, kk, row_offset)
+            idxs[name] = idx
         else:
             h = torch.zeros(len(ks), dtype=torch.int64, device=q.device)
         res.append(h.to(torch.int64))
     counts = torch.cat(res)
-    if world > 1:
-        dist.all_reduce(counts, op=dist.ReduceOp.SUM, group=group)
-    c = counts.tolist()
+    return (counts, idxs) if return_idx else counts
+
+
+def counts_to_metrics(counts: Sequence[int], n_img: int, ks: Sequence[int] = KS) -> Dict[str, float]:
+    """R@k = 100 · hits / n for the 9 counters in (T2I, I2T, I2T_Sym) × ks order (main.py:358,368,378)."""
+    c = [int(x) for x in counts]
     out = {}
     for j, name in enumerate(("T2I", "I2T", "I2T_Sym")):
-        denom = n_img
         for i, k in enumerate(ks):
-            out[f"{name}_R@{k}"] = 100.0 * c[j * len(ks) + i] / denom
+            out[f"{name}_R@{k}"] = 100.0 * c[j * len(ks) + i] / n_img
+    return out
+
+
+def sharded_recall(img_l: torch.Tensor, t2i_l: torch.Tensor, all_l: torch.Tensor, rank: int, world: int,
+                   n_img: int, caps_per_image: int = 5, ks: Sequence[int] = KS, group=None,
+                   compute: Optional[object] = None, return_tables: bool = False):
+    """Global R@k from per-rank shards (see module docstring)."""
+    lo, _ = shard_range(n_img, rank, world)
+    img_all = all_gather_rows(img_l, world, group)
+    t2i_all = all_gather_rows(t2i_l, world, group)
+    all_all = all_gather_rows(all_l, world, group)
+    counts = rank_hit_counts(img_l, t2i_l, img_all, t2i_all, all_all, lo, caps_per_image, ks, compute)
+    if world > 1:
+        dist.all_reduce(counts, op=dist.ReduceOp.SUM, group=group)
+    out = counts_to_metrics(counts.tolist(), n_img, ks)
+    if return_tables:
+        return out, {"img": img_all, "t2i": t2i_all, "all": all_all}
     return out
 
 
 def env_rank_world() -> Tuple[int, int, int]:
     """(rank, world_size, local_rank) from torchrun's environment (defaults 0/1/0)."""
-    import os
-    return int(os.environ.get("RANK", 0)), int(os.environ.get("WORLD_SIZE", 1)), int(os.environ.get("LOCAL_RANK", 0))
+    from .launch import env_rank_world as _erw
+    return _erw()
 
 
 class MaxSimOps:

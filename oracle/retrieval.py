@@ -25,12 +25,45 @@ def scores(q: np.ndarray, d: np.ndarray) -> np.ndarray:
     return q.astype(np.float32) @ d.astype(np.float32).T
 
 
-def topk(s: np.ndarray, k: int):
-    """(idx, score) of the k largest per row, ordered (score desc, column asc)."""
-    k = min(k, s.shape[1])
+def _topk_exact(s: np.ndarray, k: int):
     cols = np.arange(s.shape[1])
     order = np.lexsort((np.broadcast_to(cols, s.shape), -s), axis=1)[:, :k]
     return order.astype(np.int32), np.take_along_axis(s, order, 1)
+
+
+def topk(s: np.ndarray, k: int):
+    """(idx, score) of the k largest per row, ordered (score desc, column asc).
+
+    Wide rows: argpartition to k + 16 candidates, exact ordering among them; a row whose
+    last candidate ties the k-th value (a tie could straddle the cut) is re-ranked in full."""
+    k = min(k, s.shape[1])
+    kk = k + 16
+    if s.shape[1] <= 4 * kk:
+        return _topk_exact(s, k)
+    cand = np.argpartition(-s, kk - 1, axis=1)[:, :kk]
+    cs = np.take_along_axis(s, cand, 1)
+    order = np.lexsort((cand, -cs), axis=1)
+    cand, cs = np.take_along_axis(cand, order, 1), np.take_along_axis(cs, order, 1)
+    idx, sc = cand[:, :k].astype(np.int32), cs[:, :k].copy()
+    redo = np.nonzero(cs[:, kk - 1] >= cs[:, k - 1])[0]
+    if redo.size:
+        idx[redo], sc[redo] = _topk_exact(s[redo], k)
+    return idx, sc
+
+
+def compare_topk(idx: np.ndarray, ref_idx: np.ndarray, ref_score: np.ndarray, rel_tol: float = 1e-5):
+    """Row-wise parity of a top-k index table against the reference's.
+
+    ref_idx / ref_score hold the reference's top-(k+1) per row (score desc). A row is a
+    near-tie when two neighbouring scores among those k+1 differ by <= rel_tol·|s_1|:
+    a different fp32 summation order may legitimately swap them ("exact-index
+    parity"). Returns (identical [rows] bool, near_tie [rows] bool); every row that is
+    not a near-tie must be identical."""
+    k = idx.shape[1]
+    same = (idx == ref_idx[:, :k]).all(1)
+    gaps = ref_score[:, :k] - ref_score[:, 1:k + 1]
+    near = (gaps <= rel_tol * np.abs(ref_score[:, :1])).any(1)
+    return same, near
 
 
 def recall(idx: np.ndarray, tgt_count: int, ks: Sequence[int] = KS, row_offset: int = 0) -> np.ndarray:

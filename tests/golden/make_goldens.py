@@ -234,6 +234,37 @@ def make_retrieval(main):
     print("retrieval.npz:", dict(zip(keys, out["metric_values"].round(2))))
 
 
+def make_full_retrieval(main):
+    """BASELINE configs[1] geometry: n = 5 000 images, m = 25 000 captions, D = 1152,
+    planted noise 3.0, ranked by the reference's own compute_similarity_scores +
+    compute_metrics_detailed (v28 I2T orientation). Only the seed / checksums, each row's
+    top-11 indices and scores, and the 9 metrics are stored; the GPU test regenerates the
+    embeddings (tests/golden/planted.py) and checks their checksum first."""
+    from planted import bf16_sha, planted_np
+    n, caps, D, noise, seed = 5000, 5, 1152, 3.0, 0
+    img, all_txt = planted_np(n, caps, D, noise, seed)
+    t2i = all_txt[::caps].contiguous()
+    m_info = {"type": "dense"}
+    main.DEVICE = "cpu"
+    s_t2i = main.compute_similarity_scores(img, t2i, m_info, None)           # [n, n]  = t2i @ img.T
+    s_i2t = main.compute_similarity_scores(all_txt, img, m_info, None)       # [n, 5n] = img @ all.T (v28)
+    s_sym = s_t2i.t()
+    metrics = main.compute_metrics_detailed(s_t2i, s_i2t, s_sym, list(range(n)),
+                                            {i: list(range(caps * i, caps * i + caps)) for i in range(n)},
+                                            {i: i for i in range(n)}, [""] * n)
+    out = {"params": np.array([n, caps, D, seed], np.int64), "noise": np.float64(noise),
+           "img_sha": np.array(bf16_sha(img)), "txt_sha": np.array(bf16_sha(all_txt))}
+    for tag, s in (("t2i", s_t2i), ("i2t", s_i2t), ("sym", s_sym.contiguous())):
+        v, ix = torch.topk(s, 11, dim=1)
+        out[f"{tag}_idx"] = ix.numpy().astype(np.int32)
+        out[f"{tag}_score"] = v.numpy().astype(np.float32)
+    keys = [k for k in metrics if not k.startswith("_")]
+    out["metric_names"] = np.array(keys)
+    out["metric_values"] = np.array([metrics[k] for k in keys], np.float64)
+    np.savez_compressed(os.path.join(HERE, "full_retrieval.npz"), **out)
+    print("full_retrieval.npz:", dict(zip(keys, out["metric_values"].round(2))))
+
+
 # ------------------------------------------------------------------ maxsim + l2norm
 def make_maxsim(main):
     from transformers.models.colpali.processing_colpali import ColPaliProcessor
@@ -263,6 +294,56 @@ def make_maxsim(main):
         out[f"{case}_score"] = s.numpy().astype(np.float32)
     np.savez_compressed(os.path.join(HERE, "maxsim.npz"), **out)
     print("maxsim.npz:", {k: v.shape for k, v in out.items()})
+
+
+def make_colpali_recall(main):
+    """ColPali recall at a non-trivial size (SURVEY §8d config 4 geometry, n scaled to 64):
+    64 images x 1 030 planted doc tokens, 320 captions of 8..20 tokens left-padded per batch
+    of 4 (tests/golden/planted.py), scored by the reference's own colpali branch of
+    compute_similarity_scores (10 x 10 chunk loop, main.py:451-470; processor.score =
+    transformers' ColPaliProcessor.score_retrieval, the in-container colpali_engine stand-in)
+    and ranked by compute_metrics_detailed (main.py:305-383, per-row torch.topk for k = 1, 5, 10,
+    v28 I2T orientation). Stores both score matrices and the reference's per-row hit flags."""
+    from planted import bf16_sha, left_padded_items, planted_multivec
+    from transformers.models.colpali.processing_colpali import ColPaliProcessor
+
+    class Scorer:
+        def score(self, qs, ps):
+            return ColPaliProcessor.score_retrieval(None, qs, ps, output_dtype=torch.float32)
+
+    n, caps, Ld, qlens, noise, seed = 64, 5, 1030, (8, 21), 7.0, 0
+    img, cap, lens, pad = planted_multivec(n, caps, Ld, qlens, noise, seed=seed)
+    imgs = [img[i] for i in range(n)]
+    cap_items = left_padded_items(cap, lens, pad)
+    # T2I queries are caption 0 of each image, encoded in their own batches of 4 (main.py:554)
+    t2i_lens = lens[::caps].clone()
+    t2i_pad = torch.tensor([int(t2i_lens[s:s + 4].max()) for s in range(0, n, 4) for _ in range(min(4, n - s))],
+                           dtype=torch.int32)
+    t2i_items = left_padded_items(cap[::caps].contiguous(), t2i_lens, t2i_pad)
+    main.DEVICE = "cpu"
+    m_info = {"type": "colpali"}
+    s_t2i = main.compute_similarity_scores(imgs, t2i_items, m_info, Scorer())       # [n, n]
+    s_i2t = main.compute_similarity_scores(cap_items, imgs, m_info, Scorer())       # [n, 5n] (v28 orientation)
+    s_sym = s_t2i.t().contiguous()
+    metrics = main.compute_metrics_detailed(s_t2i, s_i2t, s_sym, list(range(n)),
+                                            {i: list(range(caps * i, caps * i + caps)) for i in range(n)},
+                                            {i: i for i in range(n)}, [""] * n)
+    hits = np.zeros((3, n, 3), bool)  # the reference's own per-row outcome (same torch.topk calls)
+    for p, (s, tgt) in enumerate(((s_t2i, lambda i: [i]), (s_i2t, lambda i: range(caps * i, caps * i + caps)),
+                                  (s_sym, lambda i: [i]))):
+        for i in range(n):
+            for j, k in enumerate((1, 5, 10)):
+                top = torch.topk(s[i], k=min(k, s.shape[1])).indices.tolist()
+                hits[p, i, j] = any(c in top for c in tgt(i))
+    keys = [k for k in metrics if not k.startswith("_")]
+    vals = np.array([metrics[k] for k in keys], np.float64)
+    assert np.allclose(vals.reshape(3, 3), 100.0 * hits.sum(1) / n)
+    out = {"params": np.array([n, caps, Ld, qlens[0], qlens[1], seed], np.int64), "noise": np.float64(noise),
+           "img_sha": np.array(bf16_sha(img)), "cap_sha": np.array(bf16_sha(cap)),
+           "t2i_score": s_t2i.numpy().astype(np.float32), "i2t_score": s_i2t.numpy().astype(np.float32),
+           "hits": hits, "metric_names": np.array(keys), "metric_values": vals}
+    np.savez_compressed(os.path.join(HERE, "colpali_recall.npz"), **out)
+    print("colpali_recall.npz:", dict(zip(keys, vals.round(2))))
 
 
 def make_l2norm(main):
@@ -485,7 +566,8 @@ if __name__ == "__main__":
     main = import_reference()
     only = sys.argv[1:]
     steps = {"preprocess": make_preprocess, "l2norm": lambda: make_l2norm(main),
-             "retrieval": lambda: make_retrieval(main), "maxsim": lambda: make_maxsim(main),
+             "retrieval": lambda: make_retrieval(main), "full_retrieval": lambda: make_full_retrieval(main),
+             "maxsim": lambda: make_maxsim(main), "colpali_recall": lambda: make_colpali_recall(main),
              "encoders": lambda: make_encoders(main), "colpali": lambda: make_colpali(main),
              "winoground": make_winoground, "bootstrap": lambda: make_bootstrap(main)}
     for name, fn in steps.items():

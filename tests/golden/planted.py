@@ -1,0 +1,74 @@
+"""Planted retrieval embeddings, regenerable bit-for-bit on any box.
+
+img_i = norm(base_i + noise·N), cap_{5i+j} = norm(base_i + noise·N), bf16.
+numpy's PCG64 + ziggurat normals (platform independent for one numpy version),
+norms in float64, one float32 rounding, then torch's round-to-nearest-even bf16
+cast. The fixture that pins the reference's ranking of these embeddings
+(full_retrieval.npz) also stores a checksum of the bf16 bits, so a test that
+regenerates them on the GPU box proves it ranks the very same inputs.
+"""
+from __future__ import annotations
+
+import hashlib
+
+import numpy as np
+import torch
+
+
+def _unit_bf16(x: np.ndarray) -> torch.Tensor:
+    nrm = np.sqrt((x.astype(np.float64) ** 2).sum(1, keepdims=True))
+    return torch.from_numpy((x / nrm).astype(np.float32)).to(torch.bfloat16)
+
+
+def planted_np(n: int, caps: int, D: int, noise: float, seed: int = 0):
+    """(img [n, D] bf16, all_txt [caps·n, D] bf16); T2I captions are all_txt[::caps]."""
+    rng = np.random.default_rng(seed)
+    base = rng.standard_normal((n, D), dtype=np.float32)
+    img = base + np.float32(noise) * rng.standard_normal((n, D), dtype=np.float32)
+    cap = np.repeat(base, caps, 0) + np.float32(noise) * rng.standard_normal((n * caps, D), dtype=np.float32)
+    return _unit_bf16(img), _unit_bf16(cap)
+
+
+def planted_multivec(n: int, caps: int, Ld: int, qlens: tuple, noise: float, batch: int = 4, seed: int = 0):
+    """ColPali-shaped planted multi-vectors (SURVEY §8d config 4 geometry, scaled down in n).
+
+    Image i: Ld unit tokens norm(base_i + noise·N) (every row valid, as for ColPali image
+    sequences). Caption c of image c // caps: len_c ∈ [qlens) unit tokens norm(base + noise·N).
+    As the reference's process_queries left-pads each batch of `batch` captions to its longest
+    query and the encoder zeroes padded rows (TF:models/colpali/modeling_colpali.py:139-140),
+    caption c's per-item tensor has pad_c - len_c leading zero rows (pad_c = its batch's longest).
+    Returns (img [n, Ld, 128] bf16, cap_valid [n·caps, max_len, 128] bf16 valid rows first,
+    cap_len [n·caps] int32, cap_pad [n·caps] int32)."""
+    rng = np.random.default_rng(seed)
+    base = rng.standard_normal((n, 128), dtype=np.float32)
+    img = base[:, None, :] + np.float32(noise) * rng.standard_normal((n, Ld, 128), dtype=np.float32)
+    m = n * caps
+    lens = rng.integers(qlens[0], qlens[1], m).astype(np.int32)
+    Lq = int(lens.max())
+    cap = np.zeros((m, Lq, 128), np.float32)
+    for c in range(m):
+        cap[c, : lens[c]] = base[c // caps] + np.float32(noise) * rng.standard_normal((int(lens[c]), 128),
+                                                                                      dtype=np.float32)
+    pad = np.array([int(lens[s:s + batch].max()) for s in range(0, m, batch) for _ in range(min(batch, m - s))],
+                   np.int32)
+
+    def unit(x):
+        nrm = np.sqrt((x.astype(np.float64) ** 2).sum(-1, keepdims=True))
+        return torch.from_numpy(np.where(nrm > 0, x / np.maximum(nrm, 1e-300), 0.0).astype(np.float32)).to(
+            torch.bfloat16)
+    return unit(img), unit(cap), torch.from_numpy(lens), torch.from_numpy(pad)
+
+
+def left_padded_items(cap: torch.Tensor, lens: torch.Tensor, pad: torch.Tensor):
+    """Per-item caption tensors as the reference's encode_data hands them to scoring: [pad_c, 128]
+    with the pad_c - len_c leading rows zero (left padding, masked to zero by the encoder)."""
+    out = []
+    for c in range(cap.shape[0]):
+        e = torch.zeros(int(pad[c]), cap.shape[2], dtype=cap.dtype)
+        e[int(pad[c]) - int(lens[c]):] = cap[c, : int(lens[c])]
+        out.append(e)
+    return out
+
+
+def bf16_sha(t: torch.Tensor) -> str:
+    return hashlib.sha256(t.contiguous().view(torch.int16).numpy().tobytes()).hexdigest()[:32]

@@ -55,23 +55,66 @@ def test_topk_merge_and_offsets(cuda):
     assert torch.equal(ms, full_s)
 
 
-@pytest.mark.slow
-def test_full_size_topk_vs_torch(cuda):
-    """BASELINE size (5 000 x 25 000, D = 1152): indices vs a torch fp32 matmul + topk,
-    checked on every row whose 10th/11th score margin exceeds the fp32 reordering noise."""
-    gen = torch.Generator(device="cuda").manual_seed(0)
-    n, D = 5000, 1152
-    base = torch.randn(n, D, device="cuda", generator=gen)
-    img = torch.nn.functional.normalize(base + 3 * torch.randn(n, D, device="cuda", generator=gen)).to(torch.bfloat16)
-    cap = torch.nn.functional.normalize(base.repeat_interleave(5, 0) + 3 * torch.randn(5 * n, D, device="cuda",
-                                                                                   generator=gen)).to(torch.bfloat16)
-    idx, sc = ops.sim_topk(img, cap, 10)
-    s = img.float() @ cap.float().T
-    v, ix = torch.topk(s, 11, dim=1)
-    ok = (v[:, 9] - v[:, 10]) > 1e-5
-    assert ok.float().mean() > 0.95  # rows whose top-10 boundary is not an fp32-noise near-tie
-    torch.testing.assert_close(sc, v[:, :10], atol=1e-4, rtol=0)
-    # identical index SETS on rows with a clear top-10 boundary
-    a = idx.sort(1).values[ok]
-    b = ix[:, :10].int().sort(1).values[ok]
-    assert torch.equal(a, b)
+@pytest.fixture(scope="module")
+def full_size(golden):
+    """BASELINE configs[1] geometry: planted 5 000 images x 25 000 captions at D = 1152, regenerated
+    here and proven identical to the embeddings the reference ranked (checksums in the fixture)."""
+    from planted import bf16_sha, planted_np
+    g = golden("full_retrieval")
+    n, caps, D, seed = (int(x) for x in g["params"])
+    img, allt = planted_np(n, caps, D, float(g["noise"]), seed)
+    assert bf16_sha(img) == str(g["img_sha"]) and bf16_sha(allt) == str(g["txt_sha"])
+    return g, img.cuda(), allt[::caps].contiguous().cuda(), allt.cuda()
+
+
+@pytest.mark.parametrize("tag", ["t2i", "i2t", "sym"])
+def test_full_size_topk_order_vs_reference(cuda, full_size, tag):
+    """Top-10 indices IN ORDER equal the reference's (main.compute_similarity_scores + torch.topk)
+    on every row; rows whose top-11 reference scores hold an fp32 near-tie (neighbouring scores
+    within 1e-5·|s|) may swap the tied pair and are counted, not skipped silently."""
+    from oracle import retrieval as R
+    g, img, t2i, allt = full_size
+    q, d = {"t2i": (t2i, img), "i2t": (img, allt), "sym": (img, t2i)}[tag]
+    idx, sc = ops.sim_topk(q, d, 10)
+    idx, sc = idx.cpu().numpy(), sc.cpu().numpy()
+    same, near = R.compare_topk(idx, g[tag + "_idx"], g[tag + "_score"])
+    bad = ~same & ~near
+    print(f"{tag}: {same.sum()}/{len(same)} rows identical, {near.sum()} near-tie rows, "
+          f"{(near & ~same).sum()} near-tie rows reordered")
+    assert not bad.any(), f"{bad.sum()} decisive rows differ, first {np.nonzero(bad)[0][:5]}"
+    # north-star tolerance: cosine scores within 1e-3 fp32 (observed ~1e-7)
+    assert np.abs(sc - g[tag + "_score"][:, :10]).max() < 1e-5
+
+
+def test_full_size_recall_identical(cuda, full_size):
+    g, img, t2i, allt = full_size
+    got = retrieval.compute_metrics(img, t2i, allt)
+    assert got == dict(zip([str(k) for k in g["metric_names"]], g["metric_values"]))
+
+
+def _emulated_shards(img, t2i, allt, world, caps=5):
+    """sharded_recall's per-rank device compute for every rank of a `world`-GPU job, on one GPU:
+    the all-gather is the concatenation of the shards (= the full tables), the all-reduce a sum."""
+    from mme.distributed import counts_to_metrics, rank_hit_counts, shard_range
+    n = img.shape[0]
+    total = torch.zeros(9, dtype=torch.int64, device="cuda")
+    for r in range(world):
+        lo, hi = shard_range(n, r, world)
+        total += rank_hit_counts(img[lo:hi].contiguous(), t2i[lo:hi].contiguous(), img, t2i, allt, lo, caps)
+    return counts_to_metrics(total.tolist(), n)
+
+
+@pytest.mark.parametrize("world", [2, 8])
+def test_sharded_device_compute_small(cuda, golden, world):
+    """DeviceOps with non-zero shard offsets (row_offset = lo) for all ranks == retrieval.npz."""
+    g = golden("retrieval")
+    img, t2i, allt = _emb(g)
+    ref = dict(zip([str(k) for k in g["metric_names"]], g["metric_values"]))
+    assert _emulated_shards(img, t2i, allt, world) == ref
+
+
+@pytest.mark.parametrize("world", [8])
+def test_sharded_device_compute_full_size(cuda, full_size, world):
+    g, img, t2i, allt = full_size
+    assert _emulated_shards(img, t2i, allt, world) == dict(zip([str(k) for k in g["metric_names"]],
+                                                               g["metric_values"]))
