@@ -199,8 +199,10 @@ def tail_aware_batch(n: int, batch: int, rows_per_item: int, cfg: Optional[Tower
     least modelled time (sum over launches of waves x K; ties -> fewer batches).
     SigLIP-400M: 5 000 images -> 21 x 239 (o_proj / fc2 in 12.0 waves) instead of
     20 x 250 (12.5 -> 13 waves); 25 000 captions -> 14 x 1 786 instead of 13 x 1 924.
-    Without `cfg` it is `balanced` (equal batches, no tail model). Results never depend on
-    the batch (items do not interact)."""
+    Without `cfg` it is `balanced` (equal batches, no tail model). Items never interact, but the
+    batch picks the GEMM kernel (the pipelined one from M·N >= 2^20, the generic one below), so
+    the fp32 summation order, and with it the output bits, may change with the batch: results
+    agree within tolerance (cos >= 0.9999, tests/test_gpu_encoders.py), not bit for bit."""
     if cfg is None or n <= 0 or os.environ.get("MME_TAIL_AWARE_BATCH", "1") == "0":
         return balanced(n, batch)
     d, ff = cfg.hidden, cfg.inter_pad
@@ -344,8 +346,9 @@ class DualEncoder:
         """u8 [n,H,W,3] images -> L2-normalised bf16 embeddings [n, D].
 
         Fuses the processor (PIL-exact bicubic + normalise) into an im2col
-        kernel feeding the patch GEMM. Batch size does not change results
-        (images never interact). Images in host memory (the
+        kernel feeding the patch GEMM. Images never interact; the batch size only
+        selects GEMM kernels (see tail_aware_batch), so results agree across batch sizes
+        within tolerance. Images in host memory (the
         reference's loader hands over host buffers) are streamed: batch i+1 is
         copied host -> HBM on a side stream (pinned staging, two device buffers)
         while batch i is encoded, so the PCIe transfer hides under the encoder."""

@@ -3,7 +3,7 @@
 Follows the transformers 5.15 modules the reference instantiates through
 from_pretrained (main.py:808-820):
   * SiglipVisionEmbeddings / SiglipTextEmbeddings  TF:models/siglip/modeling_siglip.py:116-224
-  * eager attention (fp32 softmax)                TF:models/siglip/modeling_siglip.py:228-247
+  * attention (SDPA, fp32 softmax)               TF:models/siglip/modeling_siglip.py:228-247
   * SiglipEncoderLayer (pre-LN)                    TF:models/siglip/modeling_siglip.py:325-357
   * SiglipTextTransformer pooling h[:, -1] + head  TF:models/siglip/modeling_siglip.py:520-546
   * post_layernorm + MAP head                      TF:models/siglip/modeling_siglip.py:611-644
@@ -46,11 +46,11 @@ def _attn(x, p, cfg, mask: Optional[torch.Tensor]):
     q = F.linear(x, p["self_attn.q_proj.weight"], p["self_attn.q_proj.bias"]).view(B, T, H, hd).transpose(1, 2)
     k = F.linear(x, p["self_attn.k_proj.weight"], p["self_attn.k_proj.bias"]).view(B, T, H, hd).transpose(1, 2)
     v = F.linear(x, p["self_attn.v_proj.weight"], p["self_attn.v_proj.bias"]).view(B, T, H, hd).transpose(1, 2)
-    w = torch.matmul(q, k.transpose(-1, -2)) * hd ** -0.5
-    if mask is not None:
-        w = w + mask
-    w = torch.softmax(w, dim=-1, dtype=torch.float32).to(q.dtype)
-    o = torch.matmul(w, v).transpose(1, 2).reshape(B, T, d)
+    # scaled_dot_product_attention: the attention the reference's from_pretrained models run by
+    # default (attn_implementation="sdpa", TF:models/siglip/modeling_siglip.py:228-247 is its eager
+    # twin); its CPU kernel keeps the softmax in fp32 and never materialises [B, H, T, T]
+    o = F.scaled_dot_product_attention(q, k, v, attn_mask=mask, scale=hd ** -0.5)
+    o = o.transpose(1, 2).reshape(B, T, d)
     return F.linear(o, p["self_attn.out_proj.weight"], p["self_attn.out_proj.bias"])
 
 

@@ -197,6 +197,52 @@ def make_encoders(main):
         print(f"{name}.npz:", {k: v.shape for k, v in out.items()})
 
 
+def make_config0(main):
+    """BASELINE configs[0]: OpenAI-CLIP-L (336 px, full architecture, deterministic random weights),
+    64 images x 320 captions through the reference's own CPU path: main.encode_data at the default
+    --batch-size 32 (main.py:73,131-136) for the images + all captions (main.py:551,557) and for the
+    caption-0 T2I queries (main.py:554), then compute_similarity_scores + compute_metrics_detailed.
+    Stores the embeddings (bf16 and fp32 runs) and each row's top-11 of the reference's scores."""
+    from PIL import Image
+    from transformers.models.clip.image_processing_pil_clip import CLIPImageProcessorPil
+    from mme.config import get_spec
+    from planted import config0_inputs
+    spec = get_spec("OpenAI-CLIP-L")
+    S = spec.vision.image_size
+    imgs, cap_rows = config0_inputs(spec)
+    n, caps = imgs.shape[0], len(cap_rows) // imgs.shape[0]
+    pil = [Image.fromarray(a) for a in imgs]
+    proc = RefProcessor(CLIPImageProcessorPil(size={"shortest_edge": S}, crop_size={"height": S, "width": S}),
+                        spec.text.pad_id)
+    m_info = {"name": "OpenAI-CLIP-L", "type": "dense", "batch_size": 32}
+    out = {"params": np.array([n, caps, 21], np.int64)}
+    torch.set_num_threads(os.cpu_count() or 8)
+    for tag, dtype in (("bf16", torch.bfloat16), ("f32", torch.float32)):
+        hf = RefAdapter(hf_model(spec, dtype))
+        main.DEVICE, main.DTYPE = "cpu", dtype
+        with torch.no_grad():
+            img_e, all_e = main.encode_data(hf, proc, m_info, pil, cap_rows)
+            _, t2i_e = main.encode_data(hf, proc, m_info, [], cap_rows[::caps])
+        if tag == "bf16":
+            out["img_bf16"], out["all_bf16"], out["t2i_bf16"] = bf16_bits(img_e), bf16_bits(all_e), bf16_bits(t2i_e)
+            s_t2i = main.compute_similarity_scores(img_e, t2i_e, {"type": "dense"}, None)
+            s_i2t = main.compute_similarity_scores(all_e, img_e, {"type": "dense"}, None)
+            metrics = main.compute_metrics_detailed(s_t2i, s_i2t, s_t2i.t(), list(range(n)),
+                                                    {i: list(range(caps * i, caps * i + caps)) for i in range(n)},
+                                                    {i: i for i in range(n)}, [""] * n)
+            for key, s in (("t2i", s_t2i), ("i2t", s_i2t), ("sym", s_t2i.t().contiguous())):
+                v, ix = torch.topk(s, 11, dim=1)
+                out[f"{key}_idx"], out[f"{key}_score"] = ix.numpy().astype(np.int32), v.numpy()
+            keys = [k for k in metrics if not k.startswith("_")]
+            out["metric_names"] = np.array(keys)
+            out["metric_values"] = np.array([metrics[k] for k in keys], np.float64)
+        else:
+            out["img_f32"], out["all_f32"], out["t2i_f32"] = img_e.numpy(), all_e.numpy(), t2i_e.numpy()
+        del hf
+    np.savez_compressed(os.path.join(HERE, "config0_clip_l.npz"), **out)
+    print("config0_clip_l.npz:", {k: v.shape for k, v in out.items()})
+
+
 # ------------------------------------------------------------------ retrieval
 def planted(n, caps, D, noise, seed=0):
     """SURVEY.md §8d planted embeddings: img = norm(base + noise*N), cap_{5i+j} = norm(base_i + noise*N)."""
@@ -569,6 +615,7 @@ if __name__ == "__main__":
              "retrieval": lambda: make_retrieval(main), "full_retrieval": lambda: make_full_retrieval(main),
              "maxsim": lambda: make_maxsim(main), "colpali_recall": lambda: make_colpali_recall(main),
              "encoders": lambda: make_encoders(main), "colpali": lambda: make_colpali(main),
+             "config0": lambda: make_config0(main),
              "winoground": make_winoground, "bootstrap": lambda: make_bootstrap(main)}
     for name, fn in steps.items():
         if not only or name in only:

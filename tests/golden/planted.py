@@ -70,5 +70,17 @@ def left_padded_items(cap: torch.Tensor, lens: torch.Tensor, pad: torch.Tensor):
     return out
 
 
+def config0_inputs(spec, n_img: int = 64, caps: int = 5, seed: int = 21):
+    """BASELINE configs[0] inputs: n_img synthetic 224² u8 images and caps·n_img CLIP caption id rows
+    ([bos] + 3..75 ids + [eos], ragged, so every batch of 32 pads differently)."""
+    from mme.processor import synthetic_images
+    t = spec.text
+    imgs = synthetic_images(n_img, seed=seed)
+    rng = np.random.default_rng(seed + 1)
+    lens = rng.integers(3, t.max_pos - 1, caps * n_img)
+    cap_rows = [[t.bos_id] + rng.integers(1, min(t.bos_id, t.eos_id), int(L)).tolist() + [t.eos_id] for L in lens]
+    return imgs, cap_rows
+
+
 def bf16_sha(t: torch.Tensor) -> str:
     return hashlib.sha256(t.contiguous().view(torch.int16).numpy().tobytes()).hexdigest()[:32]

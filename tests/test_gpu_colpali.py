@@ -239,3 +239,62 @@ def test_colpali_recall_vs_oracle(cuda):
         idx, _ = orr.topk(s, k)
         ref = orr.recall(idx, tc, [min(x, k) for x in ks])
         assert [counts[f"{name}_R@{x}"] for x in ks] == [100.0 * r / n for r in ref], name
+
+
+def test_colpali_recall_vs_reference_scores(cuda, golden):
+    """ColPali recall pinned to the reference's OWN scores (tests/golden/colpali_recall.npz: 64 images
+    x 1 030 planted doc tokens, 320 left-padded captions, scored by main.compute_similarity_scores'
+    colpali chunk loop and ranked by compute_metrics_detailed's per-row torch.topk).
+
+    Scores: device MaxSim vs the reference matrices, at most 1 bf16 ulp apart (processor.score
+    rounds every dot product to bf16; fp32 summation order may move one across a rounding
+    boundary). Recall: every row whose hit/miss differs from the reference's own outcome must be
+    explained by (a) an exact score tie at the k-th place involving a target (torch.topk's CPU
+    tie order is implementation defined; the device breaks ties by lowest column) or
+    (b) a 1-ulp score difference on that row; such rows are counted and printed. The device
+    recall must equal the lowest-column ranking of the device scores exactly."""
+    from planted import bf16_sha, planted_multivec
+    from mme.colpali import colpali_recall, pack_multivectors
+    from oracle import retrieval as orr
+    g = golden("colpali_recall")
+    n, caps, Ld, q0, q1, seed = (int(x) for x in g["params"])
+    img, cap, lens, pad = planted_multivec(n, caps, Ld, (q0, q1), float(g["noise"]), seed=seed)
+    assert bf16_sha(img) == str(g["img_sha"]) and bf16_sha(cap) == str(g["cap_sha"])
+    D, dl = pack_multivectors([img[i] for i in range(n)], device="cuda")
+    Lq = -(-cap.shape[1] // 16) * 16
+    Qa = torch.zeros(n * caps, Lq, 128, dtype=BF)
+    Qa[:, : cap.shape[1]] = cap
+    t2i_lens = lens[::caps].clone()
+    counts, sc = colpali_recall(D, dl, Qa[::caps].contiguous().cuda(), t2i_lens.cuda(), Qa.cuda(), lens.cuda(),
+                                pad.cuda(), caps_per_image=caps)
+    got = {"t2i": sc["t2i"].cpu().numpy(), "i2t": sc["i2t"].cpu().numpy()}
+    ref = {"t2i": g["t2i_score"], "i2t": g["i2t_score"]}
+    for tag in ("t2i", "i2t"):
+        a = torch.from_numpy(got[tag]).to(BF).view(torch.int16).int()
+        b = torch.from_numpy(ref[tag]).to(BF).view(torch.int16).int()
+        assert np.array_equal(torch.from_numpy(got[tag]).to(BF).float().numpy(), got[tag])  # bf16-quantised
+        ulp = (a - b).abs()
+        print(f"{tag}: {(ulp == 0).float().mean().item():.5f} of scores bit-identical, max {ulp.max().item()} ulp")
+        assert ulp.max().item() <= 1
+        assert (ulp == 0).float().mean().item() >= 0.99
+    ks = (1, 5, 10)
+    protos = (("T2I", "t2i", False, 1), ("I2T", "i2t", False, caps), ("I2T_Sym", "t2i", True, 1))
+    for p, (name, tag, transpose, tc) in enumerate(protos):
+        s_dev = got[tag].T if transpose else got[tag]
+        s_ref = ref[tag].T if transpose else ref[tag]
+        idx, _ = orr.topk(s_dev, 10)
+        dev_rows = np.stack([(idx[:, :k] // tc == np.arange(n)[:, None]).any(1) for k in ks], 1)   # [n, 3]
+        # the device counters == the lowest-column ranking of the device scores
+        assert [counts[f"{name}_R@{k}"] for k in ks] == [100.0 * c / n for c in dev_rows.sum(0)]
+        ref_rows = g["hits"][p]
+        diff = dev_rows != ref_rows
+        kth = -np.sort(-s_ref, 1)[:, [k - 1 for k in ks]]                                       # [n, 3]
+        tgt_best = np.stack([s_ref[i, tc * i: tc * i + tc].max() for i in range(n)])
+        tie = tgt_best[:, None] == kth
+        ulp_row = (s_dev != s_ref).any(1)[:, None]
+        unexplained = diff & ~tie & ~ulp_row
+        print(f"{name}: {int(diff.any(1).sum())} rows differ from the reference's own outcome "
+              f"({int((diff & tie).any(1).sum())} target ties at the k-th place, "
+              f"{int((diff & ~tie & ulp_row).any(1).sum())} 1-ulp rows); reference R@k "
+              f"{[round(100.0 * c / n, 2) for c in ref_rows.sum(0)]}, device {[counts[f'{name}_R@{k}'] for k in ks]}")
+        assert not unexplained.any(), f"{name}: rows {np.nonzero(unexplained.any(1))[0]} differ without a tie"

@@ -126,24 +126,52 @@ def test_fp8_towers_tiny_vs_reference(cuda, golden, name):
 
 
 @pytest.mark.slow
-def test_fp8_dfn5b_full_size_vs_oracle(cuda):
-    """BASELINE configs[4] architecture (DFN5B-H, 378 px, quick_gelu) in fp8 vs the fp32 oracle."""
+def test_fp8_dfn5b_full_size_vs_oracle(cuda, monkeypatch):
+    """BASELINE configs[4] architecture (DFN5B-H, 378 px, quick_gelu) in fp8 vs the fp32 oracle, alone
+    and inside one production execution batch (the bench's tail-aware batch; oracle items at the first
+    and last rows). Drift of fp8 against bf16 on that production batch is reported: per-row cosine of
+    the embeddings and the agreement of the I2T top-1 / top-10 rankings (random weights make recall
+    itself chance-level, so ranking agreement is the measurable drift)."""
     from helpers import row_cos
     from mme import get_spec
     from mme.models import CLIPModel
     from mme.processor import synthetic_caption_ids, synthetic_images
     from mme.weights import random_state_dict
     from oracle import encoders as oracle_enc
+    from test_gpu_encoders import production_batches
     spec = get_spec("Apple-DFN5B-H")
     sd = random_state_dict(spec, seed=0, device="cuda")
+    bf = CLIPModel.from_spec(spec, device="cuda", state_dict=sd)
     model = CLIPModel.from_spec(spec, device="cuda", state_dict=sd).enable_fp8()
     imgs = synthetic_images(1)
     ids = synthetic_caption_ids(spec, 2)
     gi = model.encode_images(torch.from_numpy(imgs).cuda()).cpu()
     gt = model.encode_texts(torch.from_numpy(ids).cuda()).cpu()
+    bi, bt = production_batches(spec)
+    bt = min(bt, 5 * bi)
+    monkeypatch.setenv("MME_TAIL_AWARE_BATCH", "0")
+    big_imgs = torch.from_numpy(synthetic_images(bi, seed=9)).cuda()
+    big_imgs[bi - 1] = torch.from_numpy(imgs[0])
+    big_ids = torch.from_numpy(synthetic_caption_ids(spec, bt, seed=9)).cuda()
+    big_ids[0], big_ids[bt - 1] = torch.from_numpy(ids[0]), torch.from_numpy(ids[1])
+    pi8 = model.encode_images(big_imgs, batch=bi)
+    pt8 = model.encode_texts(big_ids, exec_batch=bt)
+    pi16 = bf.encode_images(big_imgs, batch=bi)
+    pt16 = bf.encode_texts(big_ids, exec_batch=bt)
+    ci, ct = row_cos(pi8.cpu(), pi16.cpu()), row_cos(pt8.cpu(), pt16.cpu())
+    i8, _ = ops.sim_topk(pi8, pt8, 10)
+    i16, _ = ops.sim_topk(pi16, pt16, 10)
+    top1 = (i8[:, 0] == i16[:, 0]).float().mean().item()
+    over = np.mean([len(set(a) & set(b)) / 10 for a, b in zip(i8.cpu().tolist(), i16.cpu().tolist())])
+    print(f"fp8 vs bf16 on {bi} images x {bt} captions: cos img min {ci.min():.4f} mean {ci.mean():.4f}, "
+          f"txt min {ct.min():.4f} mean {ct.mean():.4f}; I2T top-1 agreement {top1:.3f}, top-10 overlap {over:.3f}")
+    assert ci.min() >= COS_FP8 and ct.min() >= COS_FP8
+    del bf
     sd_cpu = {k: v.float().cpu() for k, v in sd.items()}
     del sd
     torch.set_num_threads(16)
     oi, ot = oracle_enc.encode_data(spec, sd_cpu, list(imgs), ids.tolist(), bs=1, out_dtype=torch.float32)
     assert row_cos(gi, oi).min() >= COS_FP8
     assert row_cos(gt, ot).min() >= COS_FP8
+    assert row_cos(pi8[bi - 1:].cpu(), oi).min() >= COS_FP8
+    assert row_cos(pt8[[0, bt - 1]].cpu(), ot).min() >= COS_FP8
