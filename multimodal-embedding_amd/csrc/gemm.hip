@@ -688,9 +688,15 @@ __device__ __forceinline__ void gemm_epilogue_direct(const GemmArgs& p, f32x4 (&
     }
 }
 
+// dev (DIAG 12): per-tile timestamps (s_memrealtime, 100 MHz) -> g_gemm_dbg[tile][4]:
+// entry, main loop done, epilogue issued, epilogue stores retired (tools/gemm_stamps.py)
+__device__ unsigned long long* g_gemm_dbg;
+
 template <class C, int ACT, int STAG, int DIAG>
 __device__ __forceinline__ void pipe6_tile(const GemmArgs& p, char* lds, const int m0, const int n0) {
     const int tid = threadIdx.x, lane = tid & 63;
+    unsigned long long st0 = 0, st1 = 0;
+    if (DIAG == 12) st0 = __builtin_amdgcn_s_memrealtime();
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int wm = wave / C::WN, wn = wave % C::WN;
     const int g = lane >> 4, li = lane & 15;
@@ -793,11 +799,22 @@ __device__ __forceinline__ void pipe6_tile(const GemmArgs& p, char* lds, const i
         __builtin_amdgcn_s_barrier();
     }
     if (STAG && !late) __builtin_amdgcn_s_barrier();
+    if (DIAG == 12) st1 = __builtin_amdgcn_s_memrealtime();
 
     if constexpr (DIAG == 11)
         gemm_epilogue_direct<C, ACT>(p, acc, m0, n0, wm, wn, g, li);
     else
         gemm_epilogue_lds<C, ACT, (DIAG >= 6 && DIAG <= 8 ? DIAG - 5 : 0)>(p, lds, acc, m0, n0, wm, wn, g, li, tid);
+    if (DIAG == 12) {
+        const unsigned long long st2 = __builtin_amdgcn_s_memrealtime();
+        vm_wait<0>();
+        const unsigned long long st3 = __builtin_amdgcn_s_memrealtime();
+        if (tid == 0) {
+            const int tile = xcd_remap(blockIdx.x, gridDim.x);
+            unsigned long long* d = g_gemm_dbg + 4 * (size_t)tile;
+            d[0] = st0, d[1] = st1, d[2] = st2, d[3] = st3;
+        }
+    }
 }
 
 // Split grid for N = 256 k + 128 (SigLIP: o_proj / fc2 N = 1152, QKV N = 3456): the
@@ -873,6 +890,297 @@ int launch_pipe6(const GemmArgs& a, hipStream_t s) {
             break;
     }
     return mme_check_launch("mme_gemm");
+}
+
+// ---------------------------------------------------------------------------
+// pers: persistent pipe6. One 8-wave workgroup per CU walks its XCD's share of
+// the tile sequence (the same 4-row-band order as pipe6, each XCD a contiguous
+// range), and the per-tile fixed cost of pipe6 (prologue fill, LDS-staged
+// epilogue, store tail: ~6 us of a ~35 us K = 1152 tile) overlaps the MFMAs:
+//   * the LDS stage stream runs on across tile boundaries: the memory phases of
+//     a tile's last PF stages issue the NEXT tile's first PF stages, so a tile
+//     starts with its operands landed;
+//   * the epilogue stores straight from the accumulators (per 16 x 16 block a
+//     lane owns 4 consecutive columns of one row; v_permlane16_swap pairs two
+//     blocks into 8 columns = one 16-B store), no LDS and no barrier: with the
+//     wave rows one barrier apart (pipe6's ping-pong), one row's epilogue runs
+//     beside the other row's last MFMAs;
+//   * the stores are not waited for: they stay in flight under the next tile's
+//     first two stages (the counted vmcnt of those phases leaves them out).
+// Epilogue arithmetic is pipe6's LDS-staged epilogue step for step (same
+// fp32 ops in the same order, same roundings), and the K loop is pipe6's, so
+// the outputs are bit-identical to pipe6 (tools/gemm_debug.py, tests).
+// Handles N % 256 == 0 (no split grid), bf16 output, bias / LayerNorm-fold /
+// residual epilogues; vmcnt counting assumes every wave issues exactly NST
+// stores per tile, so a tile with rows past M drains everything after its
+// epilogue (vmcnt(0); the last row band only).
+// ---------------------------------------------------------------------------
+template <class C, int ACT, int DIAG = 0>
+__device__ __forceinline__ void pers_epilogue(const GemmArgs& p, f32x4 (&acc)[C::FM][C::FN], int m0, int n0,
+                                              int wm, int wn, int g, int li) {
+    static_assert(C::FN == 4, "pers: 128 x 64 wave tiles");
+    if (DIAG == 2) {  // dev: no epilogue (one reduced value keeps every MFMA live)
+        float sum = 0.f;
+#pragma unroll
+        for (int i = 0; i < C::FM; ++i)
+#pragma unroll
+            for (int j = 0; j < C::FN; ++j) sum += acc[i][j][0] + acc[i][j][1] + acc[i][j][2] + acc[i][j][3];
+        asm volatile("" ::"v"(sum));
+        return;
+    }
+    bf16* Cout = reinterpret_cast<bf16*>(p.C);
+    const bool odd = g & 1;
+    const int rbase = m0 + wm * C::TM + li;
+    const int cw = n0 + wn * C::TN;
+    // per-column terms of this lane's 4 blocks (4 consecutive columns each)
+    float bv[C::FN][4], cs[C::FN][4];
+#pragma unroll
+    for (int j = 0; j < C::FN; ++j) {
+        const int c4 = cw + j * 16 + 4 * g;
+        if (p.ln_stats) {
+            const float4 b4 = *reinterpret_cast<const float4*>(p.ln_b + c4);
+            const float4 s4 = *reinterpret_cast<const float4*>(p.ln_cs + c4);
+            bv[j][0] = b4.x, bv[j][1] = b4.y, bv[j][2] = b4.z, bv[j][3] = b4.w;
+            cs[j][0] = s4.x, cs[j][1] = s4.y, cs[j][2] = s4.z, cs[j][3] = s4.w;
+        } else {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                bv[j][r] = p.bias ? bf2f(p.bias[c4 + r]) : 0.f;
+                cs[j][r] = 0.f;
+            }
+        }
+    }
+#pragma unroll
+    for (int i = 0; i < C::FM; ++i) {
+        const int gr = rbase + i * 16;
+        const int grc = min(gr, p.M - 1);
+        float lr = 0.f, lm = 0.f;
+        if (p.ln_stats) {
+            const float2 st = *reinterpret_cast<const float2*>(p.ln_stats + 2 * grc);
+            lr = st.y;
+            lm = -st.y * st.x;
+        }
+        const int rr = p.res_period ? grc % p.res_period : grc;
+#pragma unroll
+        for (int jp = 0; jp < C::FN; jp += 2) {
+            bf16x4 o[2];
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                const int j = jp + h;
+#pragma unroll
+                for (int r = 0; r < 4; r += 2) {
+                    f32x2 y;
+                    if (p.ln_stats)
+                        y = apply_act2(pk_fma(f32x2{lr, lr}, f32x2{acc[i][j][r], acc[i][j][r + 1]},
+                                              pk_fma(f32x2{lm, lm}, f32x2{cs[j][r], cs[j][r + 1]},
+                                                     f32x2{bv[j][r], bv[j][r + 1]})),
+                                       ACT);
+                    else
+                        y = apply_act2(f32x2{acc[i][j][r], acc[i][j][r + 1]} + f32x2{bv[j][r], bv[j][r + 1]}, ACT);
+                    o[h][r] = f2bf(y.x);
+                    o[h][r + 1] = f2bf(y.y);
+                }
+            }
+            const auto x = __builtin_bit_cast(uint2, o[0]), y = __builtin_bit_cast(uint2, o[1]);
+            const auto s0 = __builtin_amdgcn_permlane16_swap(x.x, y.x, false, false);
+            const auto s1 = __builtin_amdgcn_permlane16_swap(x.y, y.y, false, false);
+            // even g: (own block jp, partner's block jp); odd g: (partner's jp + 1, own jp + 1)
+            u16x8 v = __builtin_bit_cast(u16x8, uint4{s0[0], s1[0], s0[1], s1[1]});
+            const int gc = cw + (jp + (odd ? 1 : 0)) * 16 + 4 * (g & 2);
+            if (p.res) {
+                const u16x8 rv = *reinterpret_cast<const u16x8*>(p.res + (size_t)rr * p.ldr + gc);
+#pragma unroll
+                for (int e = 0; e < 8; ++e) v[e] = __builtin_bit_cast(unsigned short, f2bf(bits2f(v[e]) + bits2f(rv[e])));
+            }
+            if (DIAG == 1)
+                asm volatile("" ::"v"(v));
+            else if (gr < p.M)
+                __builtin_nontemporal_store(v, reinterpret_cast<u16x8*>(Cout + (size_t)gr * p.ldc + gc));
+        }
+    }
+}
+
+template <class C, int GROUP_M, int ACT, int DIAG = 0>
+__global__ __launch_bounds__(C::NT, 2) void gemm_pers_kernel(GemmArgs p) {
+    __shared__ __attribute__((aligned(16))) char lds[C::LDS_MAIN];
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wm = wave / C::WN, wn = wave % C::WN;
+    const int g = lane >> 4, li = lane & 15;
+    static_assert(C::FN == 4 && C::FM == 8 && C::NW == 8, "pers geometry: 8 waves of 128 x 64");
+    constexpr int PF = C::NSTAGE - 1;
+    constexpr int NST = C::FM * C::FN / 2;  // 16-B stores per lane per tile
+    const bool late = wave >= C::NW / 2;
+
+    // this block's tiles: its XCD's contiguous range of the banded order, strided by the XCD's blocks
+    const int nbm = (p.M + C::BM - 1) / C::BM, nbn = p.N / C::BN;
+    const int ntiles = nbm * nbn;
+    const int xcd = blockIdx.x & 7, loc = blockIdx.x >> 3;
+    const int q = ntiles >> 3, r8 = ntiles & 7;
+    const int t_begin = xcd < r8 ? xcd * (q + 1) : r8 * (q + 1) + (xcd - r8) * q;
+    const int t_end = t_begin + q + (xcd < r8 ? 1 : 0);
+    const int nb = gridDim.x, bstride = (nb >> 3) + ((nb & 7) > xcd ? 1 : 0);
+    int tile = t_begin + loc;
+    if (tile >= t_end) return;  // uniform over the block: no barrier is ever reached
+
+    auto coords = [&](int t, int& m0, int& n0) {
+        int bm, bn;
+        tile_coords<GROUP_M>(t, nbm, nbn, bm, bn);
+        m0 = bm * C::BM;
+        n0 = bn * C::BN;
+    };
+    auto set_src = [&](int m0, int n0, const bf16* (&s)[C::PPW]) {
+#pragma unroll
+        for (int qq = 0; qq < C::PPW; ++qq) {
+            const int piece = wave * C::PPW + qq;
+            const bool isA = piece < C::A_PIECES;
+            const int prow = (isA ? piece : piece - C::A_PIECES) * 16 + (lane >> 2);
+            const int logical = pswz(prow, lane & 3);
+            s[qq] = isA ? p.A + (size_t)min(m0 + prow, p.M - 1) * p.lda + logical * 8
+                        : p.B + (size_t)min(n0 + prow, p.N - 1) * p.ldb + logical * 8;
+        }
+    };
+    const bf16* src[C::PPW];
+    const bf16* nsrc[C::PPW];
+    int dst[C::PPW];
+#pragma unroll
+    for (int qq = 0; qq < C::PPW; ++qq) dst[qq] = (wave * C::PPW + qq) * 1024;
+    auto issue = [&](const bf16* const (&s)[C::PPW], int kst, int slot) {
+        char* base = lds + slot * C::STAGE;
+        const int k0 = kst * C::BKS;
+#pragma unroll
+        for (int qq = 0; qq < C::PPW; ++qq) glds16(s[qq] + k0, base + dst[qq]);
+    };
+    const unsigned lds0 = (unsigned)(uintptr_t)(LDS_AS char*)lds;
+    const unsigned b_lane = lds0 + C::A_ST + (wn * C::TN + li) * 64 + (pswz(li, g) << 4);
+    const unsigned a_lane = lds0 + (wm * C::TM + li) * 64 + (pswz(li, g) << 4);
+    const int nk = p.K / C::BKS;  // host guarantees nk > PF
+
+    int m0, n0;
+    coords(tile, m0, n0);
+    set_src(m0, n0, src);
+    for (int st = 0; st < PF; ++st) issue(src, st, st);
+    vm_wait<(PF - 1) * C::PPW>();
+    __builtin_amdgcn_s_barrier();
+    if (late) __builtin_amdgcn_s_barrier();
+
+    int slot = 0;          // ring slot of the stage being read
+    bool stores = false;   // the previous tile's NST stores may still be in flight
+    f32x4 acc[C::FM][C::FN];
+    bf16x8 b[C::FN], a[8];
+    while (true) {
+        const int ntile = tile + bstride;
+        const bool has_next = ntile < t_end;
+        int nm0 = 0, nn0 = 0;
+        if (has_next) {
+            coords(ntile, nm0, nn0);
+            set_src(nm0, nn0, nsrc);
+        }
+#pragma unroll
+        for (int i = 0; i < C::FM; ++i)
+#pragma unroll
+            for (int j = 0; j < C::FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+        for (int t = 0; t < nk; ++t) {
+            // ---- memory phase
+            const unsigned so = slot * C::STAGE;
+            const unsigned bb = b_lane + so, aa = a_lane + so;
+            ds_read16<0>(b[0], bb);
+            ds_read16<1024>(b[1], bb);
+            ds_read16<2048>(b[2], bb);
+            ds_read16<3072>(b[3], bb);
+            ds_read16<0>(a[0], aa);
+            ds_read16<1024>(a[1], aa);
+            ds_read16<2048>(a[2], aa);
+            ds_read16<3072>(a[3], aa);
+            ds_read16<4096>(a[4], aa);
+            ds_read16<5120>(a[5], aa);
+            ds_read16<6144>(a[6], aa);
+            ds_read16<7168>(a[7], aa);
+            int islot = slot + PF;
+            if (islot >= C::NSTAGE) islot -= C::NSTAGE;
+            if (t + PF < nk) {
+                issue(src, t + PF, islot);
+            } else if (has_next) {
+                issue(nsrc, t + PF - nk, islot);
+            }
+            if (t + PF < nk || has_next) {
+                // retire stage t + 1; the previous tile's stores are younger than stages < PF
+                if (stores && t + 1 < PF)
+                    vm_wait<(PF - 1) * C::PPW + NST>();
+                else
+                    vm_wait<(PF - 1) * C::PPW>();
+            } else {
+                const int rem = nk - 2 - t;  // no next tile: stages t+2 .. nk-1 may stay in flight
+                if (rem >= 2) vm_wait<2 * C::PPW>();
+                else if (rem == 1) vm_wait<C::PPW>();
+                else vm_wait<0>();
+            }
+            lgkm_wait<0>();
+            __builtin_amdgcn_s_barrier();
+            // ---- compute phase
+            __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+            for (int i = 0; i < 8; ++i)
+#pragma unroll
+                for (int j = 0; j < C::FN; ++j)
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b[j], a[i], acc[i][j], 0, 0, 0);
+            __builtin_amdgcn_s_setprio(0);
+            __builtin_amdgcn_sched_barrier(0);
+            __builtin_amdgcn_s_barrier();
+            slot = slot + 1 == C::NSTAGE ? 0 : slot + 1;
+        }
+        pers_epilogue<C, ACT, DIAG>(p, acc, m0, n0, wm, wn, g, li);
+        stores = DIAG == 0;
+        if (m0 + C::BM > p.M) {  // predicated-off stores: the NST count no longer holds
+            vm_wait<0>();
+            stores = false;
+        }
+        if (!has_next) break;
+        tile = ntile;
+        m0 = nm0;
+        n0 = nn0;
+#pragma unroll
+        for (int qq = 0; qq < C::PPW; ++qq) src[qq] = nsrc[qq];
+    }
+    if (!late) __builtin_amdgcn_s_barrier();
+}
+
+int g_num_cus = 0;
+
+template <class C, int GROUP_M, int DIAG = 0>
+int launch_pers(const GemmArgs& a, hipStream_t s) {
+    if (g_num_cus == 0) {
+        int dev = 0, n = 0;
+        if (hipGetDevice(&dev) == hipSuccess && hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) ==
+                                                     hipSuccess && n > 0)
+            g_num_cus = n;
+        else
+            g_num_cus = 256;
+    }
+    const int ntiles = ((a.M + C::BM - 1) / C::BM) * (a.N / C::BN);
+    const dim3 grid(min(ntiles, g_num_cus)), block(C::NT);
+    switch (a.act) {
+        case MME_ACT_GELU_TANH:
+            hipLaunchKernelGGL((gemm_pers_kernel<C, GROUP_M, MME_ACT_GELU_TANH, DIAG>), grid, block, 0, s, a);
+            break;
+        case MME_ACT_QUICK_GELU:
+            hipLaunchKernelGGL((gemm_pers_kernel<C, GROUP_M, MME_ACT_QUICK_GELU, DIAG>), grid, block, 0, s, a);
+            break;
+        case MME_ACT_GELU_ERF:
+            hipLaunchKernelGGL((gemm_pers_kernel<C, GROUP_M, MME_ACT_GELU_ERF, DIAG>), grid, block, 0, s, a);
+            break;
+        default:
+            hipLaunchKernelGGL((gemm_pers_kernel<C, GROUP_M, MME_ACT_NONE, DIAG>), grid, block, 0, s, a);
+            break;
+    }
+    return mme_check_launch("mme_gemm");
+}
+
+// whether the persistent kernel takes this launch (host-side shape / layout checks)
+bool pers_ok(const GemmArgs& a) {
+    return !a.out_f32 && a.act != MME_ACT_GEGLU_TANH && a.N % 256 == 0 && a.K % 32 == 0 && a.K / 32 > 3 &&
+           a.ldc % 8 == 0 && ((uintptr_t)a.C & 15) == 0 && (!a.res || (a.ldr % 8 == 0 && ((uintptr_t)a.res & 15) == 0)) &&
+           !a.row_part && (long)a.M * a.N >= 1024L * 1024;
 }
 
 // ---------------------------------------------------------------------------
@@ -1081,6 +1389,10 @@ int gemm_dispatch(GemmArgs a, hipStream_t s);
 
 }  // namespace
 
+extern "C" int mme_gemm_debug_buffer(void* p) {  // dev: device buffer for variant 63's timestamps
+    return hipMemcpyToSymbol(HIP_SYMBOL(g_gemm_dbg), &p, sizeof(p)) == hipSuccess ? MME_OK : MME_ERR_HIP;
+}
+
 extern "C" int mme_gemm_variant(int v) {
     g_variant = v;
     return MME_OK;
@@ -1227,6 +1539,18 @@ int gemm_dispatch(GemmArgs a, hipStream_t s) {
             if (a.N % 256 == 128) return launch_pipe6<Pipe256, 4, 1, 0, true>(a, s);
             return launch_pipe6<Pipe256, 4, 1>(a, s);
         case 46: return launch_pipe6<PCfg<256, 256, 2, 4, 3>, 4, 1>(a, s);  // dev: 3-deep ring (2 stages ahead)
+        case 63:  // diagnostic: production pipe6 with per-tile timestamps (DIAG 12; needs mme_gemm_debug_buffer)
+            if (N % 256 == 128) return launch_pipe6<Pipe256, 4, 1, 12, true>(a, s);
+            return launch_pipe6<Pipe256, 4, 1, 12>(a, s);
+        case 60:  // dev: persistent pipe6 where it applies
+            if (pers_ok(a)) return launch_pers<Pipe256, 4>(a, s);
+            break;
+        case 61:  // diagnostic: persistent, epilogue without its global stores
+            if (pers_ok(a)) return launch_pers<Pipe256, 4, 1>(a, s);
+            break;
+        case 62:  // diagnostic: persistent, no epilogue
+            if (pers_ok(a)) return launch_pers<Pipe256, 4, 2>(a, s);
+            break;
         case 54: return launch_pipe6<Pipe256, 2, 1>(a, s);   // dev: 2-row tile bands
         case 55: return launch_pipe6<Pipe256, 16, 1>(a, s);  // dev: 16-row tile bands
         case 50: return launch_pipe7<Pipe256w, 4>(a, s);

@@ -132,8 +132,9 @@ def gemm(a: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None, 
     ev = KernelTimer.begin()
     call("mme_gemm", a.data_ptr(), lda, w.data_ptr(), ldb, out.data_ptr(), ldc, M, N, K, _ptr(bias),
          _ptr(residual), ldr, res_period, act, int(out_f32), _stream())
+    res_bytes = 2.0 * M * N if residual is not None else 0.0
     KernelTimer.end(ev, "gemm", algo_flops if algo_flops is not None else 2.0 * M * N * K,
-                    2.0 * (M * K + N * K + M * n_out))
+                    2.0 * (M * K + N * K + M * n_out) + res_bytes)
     return out
 
 
@@ -159,8 +160,11 @@ def gemm_res_stats(a: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor
     call("mme_gemm_res_stats", a.data_ptr(), _rowmajor(a, "a"), w.data_ptr(), _rowmajor(w, "w"), out.data_ptr(),
          _rowmajor(out, "out"), M, N, K, _ptr(bias), residual.data_ptr(), _rowmajor(residual, "residual"),
          float(eps), part.data_ptr(), stats.data_ptr(), _stream())
+    # the "gemm" family's time includes the statistics combine pass (row_part_combine_kernel, one
+    # launch inside this C-ABI call); its bytes: residual read, the per-slice (mean, M2) pairs
+    # written by the GEMM epilogue and read back by the combine, and the [M, 2] statistics
     KernelTimer.end(ev, "gemm", algo_flops if algo_flops is not None else 2.0 * M * N * K,
-                    2.0 * (M * K + N * K + M * N))
+                    2.0 * (M * K + N * K + M * N) + 2.0 * M * N + 2 * 8.0 * M * (N // 128) + 8.0 * M)
     return out
 
 

@@ -152,3 +152,29 @@ def test_encode_images_from_host_memory(cuda, golden):
     dev = model.encode_images(imgs.cuda(), batch=4).cpu()
     host = model.encode_images(imgs, batch=4).cpu()
     assert torch.equal(dev, host)
+
+
+@pytest.mark.slow
+def test_fused_statistics_at_production_geometry(cuda, monkeypatch):
+    """The residual-GEMM LayerNorm statistics (mme_gemm_res_stats: split grid, tail tiles, the stats
+    hand-off between layers) against the separate mme_rowstats pass, at the bench's execution batches
+    (SigLIP-400M: 239 images = 174 231 rows, 1 563 captions): same embeddings within fp32 summation
+    noise (the statistics differ only in summation order)."""
+    from mme import models
+    from mme.processor import synthetic_caption_ids, synthetic_images
+    from mme.weights import random_state_dict
+    spec = get_spec("SigLIP-400M")
+    model = SiglipModel.from_spec(spec, device="cuda", state_dict=random_state_dict(spec, seed=0, device="cuda"))
+    bi, bt = production_batches(spec)
+    monkeypatch.setenv("MME_TAIL_AWARE_BATCH", "0")
+    imgs = torch.from_numpy(synthetic_images(bi, seed=4)).cuda()
+    ids = torch.from_numpy(synthetic_caption_ids(spec, bt, seed=4)).cuda()
+    out = {}
+    for fused in (True, False):
+        monkeypatch.setattr(models, "FUSED_STATS", fused)
+        out[fused] = (model.encode_images(imgs, batch=bi).cpu(), model.encode_texts(ids, exec_batch=bt).cpu())
+    for k, what in ((0, "images"), (1, "captions")):
+        c = row_cos(out[True][k], out[False][k])
+        print(f"{what}: fused vs separate statistics cos min {c.min().item():.6f}, "
+              f"{torch.equal(out[True][k], out[False][k])=}")
+        assert c.min() >= 0.9999

@@ -50,7 +50,9 @@ def main():
         W = (torch.randn(N, K, device="cuda", generator=g) / K ** 0.5).to(torch.bfloat16)
         C = torch.randn(M, N, device="cuda", generator=g).to(torch.bfloat16)
         bias = (torch.randn(N, device="cuda", generator=g) * 0.1).to(torch.bfloat16)
+        R256 = C[:256].clone()  # "resper": residual rows r % 256 (an L2-resident residual table)
         kw = {"none": {}, "bias": {"bias": bias}, "res": {"bias": bias, "residual": C}, "resstats": {},
+              "resper": {"bias": bias, "residual": R256, "res_period": 256},
               "gelu": {"bias": bias, "act": _lib.ACT_GELU_TANH}}[a.epi]
         st = torch.empty(M, 2, device="cuda")
         part = torch.empty(M, max(1, N // 128), 2, device="cuda")
@@ -62,8 +64,8 @@ def main():
                 ops.gemm(A, W, out=C, **kw)
         ref = None
         for v in variants:
-            if v >= 0:
-                lib.mme_gemm_variant(v)
+            if has_var:
+                lib.mme_gemm_variant(v)  # -1 = production dispatch
             run()
             if ref is None or a.epi in ("res", "resstats"):
                 ref = C.clone()
