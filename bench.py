@@ -62,6 +62,10 @@ def parse():
     p.add_argument("--bootstrap", type=int, default=0,
                    help="also time N bootstrap resamples of the recall on the device (main.py:586-634; untimed "
                         "by the headline metric, reported separately)")
+    p.add_argument("--backend", default="nccl", help="process-group backend for N > 1 (nccl = RCCL on ROCm; "
+                   "gloo = rehearsal of the multi-rank path, e.g. with --same-device)")
+    p.add_argument("--same-device", action="store_true",
+                   help="every rank on cuda:0 (rehearse N ranks on a one-GPU box; needs --backend gloo)")
     p.add_argument("--fp8", action="store_true",
                    help="mx8 encoder GEMMs (BASELINE configs[4]: DFN5B-H fp8 weights on the fp8 MFMA)")
     return p.parse_args()
@@ -219,7 +223,7 @@ def main_colpali(args, rank, world, dev):
     T2I / I2T / I2T-Sym + top-10 recall. value = images / job second."""
     from mme import get_spec, ops
     from mme.colpali_encoder import ColPaliModel
-    from mme.distributed import shard_range, sharded_colpali_recall
+    from mme.distributed import all_reduce_, shard_range, sharded_colpali_recall
     spec = get_spec(args.model)
     model = ColPaliModel.from_spec(spec, seed=0, device=dev)
     n, caps = args.n_images, args.caps
@@ -275,7 +279,7 @@ def main_colpali(args, rank, world, dev):
               "maxsim_recall_ms": ev["txt"].elapsed_time(ev["score"])}
     if world > 1:
         t = torch.tensor([dt], device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        all_reduce_(t, dist.ReduceOp.MAX)
         dt = float(t.item())
     kt = ops.KernelTimer.summary() if not args.no_kernel_timer else {}
     roofline = None
@@ -307,6 +311,8 @@ def main_colpali(args, rank, world, dev):
         "recall": {k: round(v, 2) for k, v in metrics.items()},
         "roofline": roofline, "cpu_baseline": None,
     }
+    out["process_group"] = ({"backend": dist.get_backend(), "ranks": dist.get_world_size(),
+                             "same_device": bool(args.same_device)} if world > 1 else None)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         sys.path.insert(0, ROOT)
         out["cpu_baseline"] = cpu_baseline_colpali(spec, args.cpu_seconds)
@@ -325,10 +331,12 @@ def main():
         # the first failing rank's status
         sys.exit(launch.spawn_ranks(args.gpus, [os.path.abspath(__file__)] + sys.argv[1:]))
     _, _, local = launch.env_rank_world()
+    if args.same_device:
+        local = 0
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     try:
-        rank, world, local = launch.init_distributed(args.gpus, "nccl", dev)
+        rank, world, _ = launch.init_distributed(args.gpus, args.backend, dev)
     except launch.LaunchError as e:
         print(f"bench.py: {e}", file=sys.stderr, flush=True)
         sys.exit(3)
@@ -340,7 +348,7 @@ def main():
         return main_colpali(args, rank, world, dev)
 
     from mme import get_spec, ops
-    from mme.distributed import shard_range, sharded_recall
+    from mme.distributed import all_reduce_, shard_range, sharded_recall
     from mme.models import load_model
 
     spec = get_spec(args.model)
@@ -396,9 +404,9 @@ def main():
                            ev["txt"].elapsed_time(ev["ret"])], dtype=torch.float64, device=dev)
     if world > 1:
         t = torch.tensor([dt], device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        all_reduce_(t, dist.ReduceOp.MAX)
         dt = float(t.item())
-        dist.all_reduce(phases, op=dist.ReduceOp.MAX)
+        all_reduce_(phases, dist.ReduceOp.MAX)
     phases = phases.tolist()
     kt = ops.KernelTimer.summary() if not args.no_kernel_timer else {}
 
@@ -463,6 +471,8 @@ def main():
         "parity": None,
         "cpu_baseline": None,
     }
+    out["process_group"] = ({"backend": dist.get_backend(), "ranks": dist.get_world_size(),
+                             "same_device": bool(args.same_device)} if world > 1 else None)
     if rank == 0 and not args.no_parity:
         out["parity"] = retrieval_parity(last["tables"], metrics, caps)
     if args.host_inputs:

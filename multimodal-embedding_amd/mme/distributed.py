@@ -34,6 +34,8 @@ def all_gather_rows(x: torch.Tensor, world: int, group=None) -> torch.Tensor:
     """Concatenate every rank's [n_r, D] rows in rank order (ragged n_r allowed)."""
     if world == 1:
         return x
+    if x.is_cuda and dist.get_backend(group) == "gloo":  # gloo gathers host tensors (CPU rehearsal of N > 1)
+        return all_gather_rows(x.cpu(), world, group).to(x.device)
     n = torch.tensor([x.shape[0]], dtype=torch.int64, device=x.device)
     sizes = [torch.zeros_like(n) for _ in range(world)]
     dist.all_gather(sizes, n, group=group)
@@ -49,6 +51,17 @@ def all_gather_rows(x: torch.Tensor, world: int, group=None) -> torch.Tensor:
         parts = [torch.empty_like(xp) for _ in range(world)]
         dist.all_gather(parts, xp, group=group)
     return torch.cat([p[:s] for p, s in zip(parts, sizes)])
+
+
+def all_reduce_(t: torch.Tensor, op=dist.ReduceOp.SUM, group=None) -> torch.Tensor:
+    """In-place all-reduce; gloo (CPU rehearsal of the N > 1 path) reduces a host copy of device tensors."""
+    if t.is_cuda and dist.get_backend(group) == "gloo":
+        h = t.cpu()
+        dist.all_reduce(h, op=op, group=group)
+        t.copy_(h)
+        return t
+    dist.all_reduce(t, op=op, group=group)
+    return t
 
 
 class DeviceOps:
@@ -110,7 +123,7 @@ def sharded_recall(img_l: torch.Tensor, t2i_l: torch.Tensor, all_l: torch.Tensor
     all_all = all_gather_rows(all_l, world, group)
     counts = rank_hit_counts(img_l, t2i_l, img_all, t2i_all, all_all, lo, caps_per_image, ks, compute)
     if world > 1:
-        dist.all_reduce(counts, op=dist.ReduceOp.SUM, group=group)
+        all_reduce_(counts, dist.ReduceOp.SUM, group)
     out = counts_to_metrics(counts.tolist(), n_img, ks)
     if return_tables:
         return out, {"img": img_all, "t2i": t2i_all, "all": all_all}
@@ -180,7 +193,7 @@ def sharded_colpali_recall(img_D: torch.Tensor, img_len: torch.Tensor, t2i_Q: to
             res.append(torch.zeros(len(ks), dtype=torch.int64, device=s.device))
     counts = torch.cat(res)
     if world > 1:
-        dist.all_reduce(counts, op=dist.ReduceOp.SUM, group=group)
+        all_reduce_(counts, dist.ReduceOp.SUM, group)
     c = counts.tolist()
     out = {}
     for j, name in enumerate(("T2I", "I2T", "I2T_Sym")):

@@ -1,0 +1,37 @@
+"""bench.py's multi-rank path with real device compute, rehearsed on one GPU.
+
+`bench.py --gpus N` spawns its own N ranks (mme.launch), each rank encodes its image shard and
+the captions of those images, all-gathers the embedding tables and ranks its own rows; the 9
+hit counters are all-reduced. On a one-GPU box every rank runs on cuda:0 over a gloo process
+group (--same-device --backend gloo): everything but the RCCL transport itself is exercised
+(sharding, non-zero row offsets in the device recall, gather order, counter reduction, timing
+max over ranks). The N-rank recall must equal the single-rank recall of the same job."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _bench(*args):
+    env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "LOCAL_WORLD_SIZE")}
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--model", "tiny-siglip", "--n-images", "203",
+                        "--steps", "1", "--warmup", "0", "--no-cpu-baseline", "--no-kernel-timer", *args],
+                       env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout[-2000:]
+    return json.loads(lines[0])
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_multirank_bench_equals_single_rank(cuda, world):
+    one = _bench()
+    many = _bench("--gpus", str(world), "--backend", "gloo", "--same-device")
+    assert many["n_gpus"] == world and many["process_group"]["ranks"] == world
+    assert many["recall"] == one["recall"]
+    assert many["parity"]["recall_identical"] and one["parity"]["recall_identical"]

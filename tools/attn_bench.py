@@ -26,6 +26,9 @@ CASES = [  # name, B, T, H, hd, causal
     ("dfn5b_vision", 128, 730, 16, 80, False),
     ("clip_text_causal", 1024, 77, 16, 64, True),
 ]
+if "--cases" in sys.argv:
+    _want = sys.argv[sys.argv.index("--cases") + 1].split(",")
+    CASES = [c for c in CASES if c[0] in _want]
 for (name, B, T, H, hd, causal), v in [(c, v) for c in CASES for v in VARIANTS]:
     if (1 <= v <= 4 or 21 <= v <= 26) and (hd != 72 or (v >= 21 and T < 256)):
         continue
