@@ -549,7 +549,7 @@ __device__ __forceinline__ float xsum32(float v) {
     return __uint_as_float(r[0]) + __uint_as_float(r[1]);
 }
 
-template <int HD, int NW, int NSTG, bool PIPE, bool ONES, bool LAZY, bool PING = false, int MINW = 1>
+template <int HD, int NW, int NSTG, bool PIPE, bool ONES, bool LAZY, bool PING = false, int MINW = 1, bool UNR = false>
 __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(MINW))) void attn_pipe_kernel(AttnArgs a) {
     static_assert(!PIPE || NSTG == 3, "the pipelined loop keeps tile t+1 resident while t+2 lands");
     static_assert(!PING || (!PIPE && NSTG == 4), "ping-pong: two tiles resident beside the one landing");
@@ -653,8 +653,7 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(MINW)))
         for (int i = 0; i < NDT; ++i) o[u][i] = f32x4{0.f, 0.f, 0.f, 0.f};
     float m[2] = {-1e30f, -1e30f}, lsum[2] = {0.f, 0.f};
 
-    auto qk = [&](int t, f32x4(&sc)[2][4]) {
-        const unsigned so = (t % NSTG) * TILE;
+    auto qk_at = [&](int t, const unsigned so, f32x4(&sc)[2][4]) {
 #pragma unroll
         for (int kt = 0; kt < 4; ++kt) {
             bf16x8 kf[NKS];
@@ -682,8 +681,8 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(MINW)))
             }
         }
     };
-    auto softmax_pv = [&](int t, f32x4(&sc)[2][4], auto&& before_pv) {
-        const unsigned so = (t % NSTG) * TILE;
+    auto qk = [&](int t, f32x4(&sc)[2][4]) { qk_at(t, (t % NSTG) * TILE, sc); };
+    auto softmax_pv_at = [&](int t, const unsigned so, f32x4(&sc)[2][4], auto&& before_pv) {
         float mnew[2];
         bool grew = false;
 #pragma unroll
@@ -742,8 +741,30 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(MINW)))
         }
     };
 
+    auto softmax_pv = [&](int t, f32x4(&sc)[2][4], auto&& before_pv) {
+        softmax_pv_at(t, (t % NSTG) * TILE, sc, before_pv);
+    };
+
     f32x4 sA[2][4], sB[2][4];
-    if (PIPE) {
+    if (UNR && !PIPE && !PING && NSTG == 2) {
+        // unrolled by the ring depth: the ring slot of every LDS access is a compile-time
+        // constant (immediate ds_read offsets, no per-tile address VALU)
+        if (nkt > 0) issue(0);
+        for (int t = 0; t < nkt; t += 2) {
+            vm_wait<0>();
+            __builtin_amdgcn_s_barrier();
+            if (t + 1 < nkt) issue(t + 1);
+            qk_at(t, 0, sA);
+            softmax_pv_at(t, 0, sA, [] {});
+            if (t + 1 < nkt) {
+                vm_wait<0>();
+                __builtin_amdgcn_s_barrier();
+                if (t + 2 < nkt) issue(t + 2);
+                qk_at(t + 1, TILE, sA);
+                softmax_pv_at(t + 1, TILE, sA, [] {});
+            }
+        }
+    } else if (PIPE) {
         // iteration t: [tile t+1 landed, barrier, issue t+2, S(t+1)] then softmax + PV of tile t
         auto iter = [&](int t, f32x4(&cur)[2][4], f32x4(&nxt)[2][4]) {
             if (t + 1 < nkt) {
@@ -1123,6 +1144,9 @@ void launch_attn(int kind, const AttnArgs& a, int B, int T, int H, hipStream_t s
         hipLaunchKernelGGL((attn_pipe_kernel<HD, 9, 3, false, HD == 72, true>), dim3(cdiv(T, 288) * H * B), dim3(576), 0, st, a);
     else if (kind == 22)  // dev: 5 waves = 160 queries per block
         hipLaunchKernelGGL((attn_pipe_kernel<HD, 5, 2, false, HD == 72, true>), dim3(cdiv(T, 160) * H * B), dim3(320), 0, st, a);
+    else if (kind == 27)  // kind 17 unrolled by the ring depth (compile-time ring slots)
+        hipLaunchKernelGGL((attn_pipe_kernel<HD, 8, 2, false, HD == 72, true, false, 4, true>), dim3(cdiv(T, 256) * H * B),
+                           dim3(512), 0, st, a);
     else if (kind == 12)  // dev: pipelined + lazy + ones
         hipLaunchKernelGGL((attn_pipe_kernel<HD, 8, 3, true, HD == 72, true>), dim3(cdiv(T, 256) * H * B), dim3(512), 0, st, a);
     else
@@ -1174,7 +1198,7 @@ extern "C" int mme_attention(const void* qkv, int ld_qkv, void* out, int ld_out,
                : (T <= 128 || hd == 64) ? 0
                : pad9 * 10 < min(pad8, pad4) * 9 ? 21
                : (hd == 80 && pad12 <= pad8 && pad12 * 10 <= pad4 * 11) ? 23
-               : (pad8 * 10 <= pad4 * 11 ? (hd == 72 ? 17 : 11) : 14);
+               : (pad8 * 10 <= pad4 * 11 ? (hd == 72 ? 27 : 11) : 14);
     if (g_attn_variant >= 1 && g_attn_variant <= 4 && hd == 72) {  // dev-only diagnostic builds
         const dim3 grid(cdiv(T, 128) * H * B);
         switch (g_attn_variant) {
