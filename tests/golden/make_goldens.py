@@ -280,6 +280,37 @@ def make_retrieval(main):
     print("retrieval.npz:", dict(zip(keys, out["metric_values"].round(2))))
 
 
+def make_edge(main):
+    """Edge cases of the reference's ranking (main.py:305-383, 440-475) and encode loop (main.py:386-438):
+    fewer columns than k (n = 1, 2 and 3 images: torch.topk(k = min(k, ncols))), a ragged last batch,
+    and empty inputs (encode_data on [] returns torch.empty(0))."""
+    out = {}
+    for n, D, noise in ((1, 64, 0.5), (2, 96, 1.0), (3, 128, 1.2), (7, 64, 1.5), (33, 128, 2.0)):
+        img, all_txt = planted(n, 5, D, noise=noise, seed=100 + n)
+        t2i = all_txt[::5].contiguous()
+        main.DEVICE = "cpu"
+        s_t2i = main.compute_similarity_scores(img, t2i, {"type": "dense"}, None)
+        s_i2t = main.compute_similarity_scores(all_txt, img, {"type": "dense"}, None)
+        m = main.compute_metrics_detailed(s_t2i, s_i2t, s_t2i.t(), list(range(n)),
+                                          {i: list(range(5 * i, 5 * i + 5)) for i in range(n)},
+                                          {i: i for i in range(n)}, [""] * n)
+        keys = [k for k in m if not k.startswith("_")]
+        out[f"n{n}_img"], out[f"n{n}_all_txt"] = bf16_bits(img), bf16_bits(all_txt)
+        out[f"n{n}_metrics"] = np.array([m[k] for k in keys], np.float64)
+    out["metric_names"] = np.array(keys)
+
+    class Feed:  # encode_data over empty lists never calls the model
+        def get_image_features(self, **_):
+            raise AssertionError("called on an empty list")
+
+        get_text_features = get_image_features
+    main.DEVICE, main.DTYPE = "cpu", torch.bfloat16
+    e_img, e_txt = main.encode_data(Feed(), None, {"type": "dense", "batch_size": 32}, [], [])
+    out["empty_shapes"] = np.array([list(e_img.shape), list(e_txt.shape)], np.int64)
+    np.savez_compressed(os.path.join(HERE, "edge.npz"), **out)
+    print("edge.npz:", {k: v.tolist() for k, v in out.items() if k.endswith("metrics")}, out["empty_shapes"].tolist())
+
+
 def make_full_retrieval(main):
     """BASELINE configs[1] geometry: n = 5 000 images, m = 25 000 captions, D = 1152,
     planted noise 3.0, ranked by the reference's own compute_similarity_scores +
@@ -615,7 +646,7 @@ if __name__ == "__main__":
              "retrieval": lambda: make_retrieval(main), "full_retrieval": lambda: make_full_retrieval(main),
              "maxsim": lambda: make_maxsim(main), "colpali_recall": lambda: make_colpali_recall(main),
              "encoders": lambda: make_encoders(main), "colpali": lambda: make_colpali(main),
-             "config0": lambda: make_config0(main),
+             "config0": lambda: make_config0(main), "edge": lambda: make_edge(main),
              "winoground": make_winoground, "bootstrap": lambda: make_bootstrap(main)}
     for name, fn in steps.items():
         if not only or name in only:
