@@ -441,6 +441,11 @@ def sim_topk(q: torch.Tensor, d: torch.Tensor, k: int, col_offset: int = 0):
     _dev(q, d)
     nq, D = q.shape
     nd = d.shape[0]
+    if D % 64:  # the kernel's K loop takes 64-deep steps: zero columns leave every dot product unchanged
+        Dp = -(-D // 64) * 64
+        q = torch.nn.functional.pad(q, (0, Dp - D))
+        d = torch.nn.functional.pad(d, (0, Dp - D))
+        D = Dp
     idx = torch.empty(nq, k, dtype=torch.int32, device=q.device)
     sc = torch.empty(nq, k, dtype=torch.float32, device=q.device)
     wsb = query("mme_sim_topk_workspace_bytes", nq, nd, k)

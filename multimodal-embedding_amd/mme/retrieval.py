@@ -33,6 +33,9 @@ def compute_similarity_scores(img_embeds: torch.Tensor, txt_embeds: torch.Tensor
     dev = img_embeds.device if img_embeds.is_cuda else torch.device("cuda")
     a = txt_embeds.to(dev, torch.bfloat16).contiguous()
     b = img_embeds.to(dev, torch.bfloat16).contiguous()
+    if a.shape[1] % 64:  # the GEMM's K steps are 64 deep; zero columns leave the dot products unchanged
+        pad = -a.shape[1] % 64
+        a, b = torch.nn.functional.pad(a, (0, pad)), torch.nn.functional.pad(b, (0, pad))
     return ops.gemm(a, b, out_f32=True)
 
 

@@ -56,3 +56,18 @@ def test_exact_ties_break_by_lowest_column(cuda):
     s = (q.float() @ docs.float().T).cuda()
     idx2, _ = ops.topk_rows(s.contiguous(), 10)
     assert np.array_equal(idx2.cpu().numpy(), ridx)
+
+
+@pytest.mark.parametrize("D", [8, 96, 200])
+def test_embedding_widths_off_the_tile_grid(cuda, D):
+    """Embedding widths that are not multiples of the 64-deep K step (zero-padded on the host)."""
+    from oracle import retrieval as R
+    g = torch.Generator().manual_seed(D)
+    q = torch.nn.functional.normalize(torch.randn(37, D, generator=g), dim=-1).to(torch.bfloat16)
+    d = torch.nn.functional.normalize(torch.randn(301, D, generator=g), dim=-1).to(torch.bfloat16)
+    idx, sc = ops.sim_topk(q.cuda(), d.cuda(), 10)
+    ridx, rsc = R.topk(R.scores(q.float().numpy(), d.float().numpy()), 11)
+    same, near = R.compare_topk(idx.cpu().numpy(), ridx, rsc)
+    assert (same | near).all()
+    s = retrieval.compute_similarity_scores(d.cuda(), q.cuda())
+    torch.testing.assert_close(s.cpu(), q.float() @ d.float().T, atol=1e-5, rtol=1e-5)
