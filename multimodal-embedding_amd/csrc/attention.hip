@@ -549,7 +549,8 @@ __device__ __forceinline__ float xsum32(float v) {
     return __uint_as_float(r[0]) + __uint_as_float(r[1]);
 }
 
-template <int HD, int NW, int NSTG, bool PIPE, bool ONES, bool LAZY, bool PING = false, int MINW = 1, bool UNR = false>
+template <int HD, int NW, int NSTG, bool PIPE, bool ONES, bool LAZY, bool PING = false, int MINW = 1, bool UNR = false,
+          bool ADMA = false>
 __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(MINW))) void attn_pipe_kernel(AttnArgs a) {
     static_assert(!PIPE || NSTG == 3, "the pipelined loop keeps tile t+1 resident while t+2 lands");
     static_assert(!PING || (!PIPE && NSTG == 4), "ping-pong: two tiles resident beside the one landing");
@@ -603,6 +604,12 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(MINW)))
 
     int nkt = (Tk + 63) / 64;
     if (a.causal) nkt = min(nkt, (min(T, qb * QB + QB) + 63) / 64);
+    if (ADMA) {  // Q landed before the tile loop: hipcc then never waits inside it (it cannot count the asm DMA)
+#pragma unroll
+        for (int u = 0; u < 2; ++u)
+#pragma unroll
+            for (int ks = 0; ks < NKS; ++ks) asm volatile("" ::"v"(qf[u][ks]));
+    }
 
     const int nmine = (NINS - wave + NW - 1) / NW;
     auto issue = [&](int t) {
@@ -615,7 +622,10 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(MINW)))
                 const int plane = isV ? idx - NCHL : idx;
                 const int key = isV && (plane & 1) ? lane ^ 8 : lane;
                 const bf16* src = base + (long)min(t * 64 + key, T - 1) * a.ld + (isV ? 2 : 1) * D + h * HD + plane * 8;
-                glds16(src, tb + idx * 1024);
+                if (ADMA)
+                    glds16_asm(src, tb + idx * 1024);
+                else
+                    glds16(src, tb + idx * 1024);
             }
         }
     };
@@ -1147,6 +1157,9 @@ void launch_attn(int kind, const AttnArgs& a, int B, int T, int H, hipStream_t s
     else if (kind == 27)  // kind 17 unrolled by the ring depth (compile-time ring slots)
         hipLaunchKernelGGL((attn_pipe_kernel<HD, 8, 2, false, HD == 72, true, false, 4, true>), dim3(cdiv(T, 256) * H * B),
                            dim3(512), 0, st, a);
+    else if (kind == 28)  // kind 27 with the K/V DMA issued from inline asm (no compiler vmcnt(0) before LDS reads)
+        hipLaunchKernelGGL((attn_pipe_kernel<HD, 8, 2, false, HD == 72, true, false, 4, true, true>),
+                           dim3(cdiv(T, 256) * H * B), dim3(512), 0, st, a);
     else if (kind == 12)  // dev: pipelined + lazy + ones
         hipLaunchKernelGGL((attn_pipe_kernel<HD, 8, 3, true, HD == 72, true>), dim3(cdiv(T, 256) * H * B), dim3(512), 0, st, a);
     else

@@ -65,6 +65,15 @@ __device__ __forceinline__ void glds16(const void* gsrc, void* lds_base) {
 
 __device__ __forceinline__ void wait_vmcnt0() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 
+// glds16 issued from inline asm: the same global_load_lds_dwordx4, but invisible to hipcc's
+// waitcnt pass, which otherwise drains it (vmcnt(0)) before any LDS read it cannot prove
+// disjoint from the DMA's destination. The caller retires it with its own counted vmcnt
+// wait + barrier before the bytes are read. `lds_base` must be wave-uniform (M0).
+__device__ __forceinline__ void glds16_asm(const void* gsrc, void* lds_base) {
+    const unsigned m0 = __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)(LDS_AS char*)lds_base);
+    asm volatile("s_mov_b32 m0, %1\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(gsrc), "s"(m0) : "memory", "m0");
+}
+
 // Activation codes shared by the GEMM epilogue and the host (mme.h MME_ACT_*).
 // The sigmoid forms run on the transcendental unit (v_exp_f32 + v_rcp_f32, ~1 ulp
 // each) instead of the libm tanhf / IEEE division sequences: in a GEMM epilogue the
