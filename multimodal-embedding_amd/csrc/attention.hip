@@ -549,9 +549,13 @@ __device__ __forceinline__ float xsum32(float v) {
     return __uint_as_float(r[0]) + __uint_as_float(r[1]);
 }
 
+// XF (dev extras, bit mask): 1 = K/V DMA from inline asm (ADMA), 2 = exp arguments as packed
+// FMAs (v_pk_fma_f32, half the issues; same per-element fma, bit-identical), 4 = s_setprio 1
+// for the second half of the waves before the tile loop (static priority)
 template <int HD, int NW, int NSTG, bool PIPE, bool ONES, bool LAZY, bool PING = false, int MINW = 1, bool UNR = false,
-          bool ADMA = false>
+          int XF = 0>
 __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(MINW))) void attn_pipe_kernel(AttnArgs a) {
+    constexpr bool ADMA = XF & 1, PKX = XF & 2, PRIO = XF & 4;
     static_assert(!PIPE || NSTG == 3, "the pipelined loop keeps tile t+1 resident while t+2 lands");
     static_assert(!PING || (!PIPE && NSTG == 4), "ping-pong: two tiles resident beside the one landing");
     static_assert(!ONES || HD == 72, "the ones column lives in the padding of the 80-wide V^T tiles");
@@ -720,14 +724,29 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(MINW)))
             m[u] = mnew[u];
             const float mc = mnew[u] * c;
             float psum = 0.f;
+            if (PKX) {
 #pragma unroll
-            for (int kt = 0; kt < 4; ++kt)
+                for (int kt = 0; kt < 4; ++kt)
 #pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    const float pv = __builtin_amdgcn_exp2f(sc[u][kt][r] * c - mc);
-                    sc[u][kt][r] = pv;
-                    if (!ONES) psum += pv;
-                }
+                    for (int r = 0; r < 4; r += 2) {
+                        const f32x2 x = pk_fma(f32x2{sc[u][kt][r], sc[u][kt][r + 1]}, f32x2{c, c}, f32x2{-mc, -mc});
+                        sc[u][kt][r] = __builtin_amdgcn_exp2f(x.x);
+                        sc[u][kt][r + 1] = __builtin_amdgcn_exp2f(x.y);
+                        if (!ONES) {
+                            psum += sc[u][kt][r];
+                            psum += sc[u][kt][r + 1];
+                        }
+                    }
+            } else {
+#pragma unroll
+                for (int kt = 0; kt < 4; ++kt)
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        const float pv = __builtin_amdgcn_exp2f(sc[u][kt][r] * c - mc);
+                        sc[u][kt][r] = pv;
+                        if (!ONES) psum += pv;
+                    }
+            }
             if (!ONES) lsum[u] += psum;
         }
         before_pv();
@@ -756,6 +775,7 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(MINW)))
     };
 
     f32x4 sA[2][4], sB[2][4];
+    if (PRIO && wave >= NW / 2) __builtin_amdgcn_s_setprio(1);
     if (UNR && !PIPE && !PING && NSTG == 2) {
         // unrolled by the ring depth: the ring slot of every LDS access is a compile-time
         // constant (immediate ds_read offsets, no per-tile address VALU)
@@ -1158,7 +1178,16 @@ void launch_attn(int kind, const AttnArgs& a, int B, int T, int H, hipStream_t s
         hipLaunchKernelGGL((attn_pipe_kernel<HD, 8, 2, false, HD == 72, true, false, 4, true>), dim3(cdiv(T, 256) * H * B),
                            dim3(512), 0, st, a);
     else if (kind == 28)  // kind 27 with the K/V DMA issued from inline asm (no compiler vmcnt(0) before LDS reads)
-        hipLaunchKernelGGL((attn_pipe_kernel<HD, 8, 2, false, HD == 72, true, false, 4, true, true>),
+        hipLaunchKernelGGL((attn_pipe_kernel<HD, 8, 2, false, HD == 72, true, false, 4, true, 1>),
+                           dim3(cdiv(T, 256) * H * B), dim3(512), 0, st, a);
+    else if (kind == 29)  // dev: kind 27 with packed exp-argument FMAs
+        hipLaunchKernelGGL((attn_pipe_kernel<HD, 8, 2, false, HD == 72, true, false, 4, true, 2>),
+                           dim3(cdiv(T, 256) * H * B), dim3(512), 0, st, a);
+    else if (kind == 30)  // dev: kind 27 with static priority for waves NW/2..
+        hipLaunchKernelGGL((attn_pipe_kernel<HD, 8, 2, false, HD == 72, true, false, 4, true, 4>),
+                           dim3(cdiv(T, 256) * H * B), dim3(512), 0, st, a);
+    else if (kind == 31)  // dev: both
+        hipLaunchKernelGGL((attn_pipe_kernel<HD, 8, 2, false, HD == 72, true, false, 4, true, 6>),
                            dim3(cdiv(T, 256) * H * B), dim3(512), 0, st, a);
     else if (kind == 12)  // dev: pipelined + lazy + ones
         hipLaunchKernelGGL((attn_pipe_kernel<HD, 8, 3, true, HD == 72, true>), dim3(cdiv(T, 256) * H * B), dim3(512), 0, st, a);
@@ -1223,7 +1252,7 @@ extern "C" int mme_attention(const void* qkv, int ld_qkv, void* out, int ld_out,
         return mme_check_launch("mme_attention");
     }
     if (g_attn_variant >= 9 && g_attn_variant <= 16) kind = g_attn_variant - 9;  // dev: force a kernel
-    if (g_attn_variant >= 30 && g_attn_variant <= 59) kind = g_attn_variant - 30;  // dev: force a kernel
+    if (g_attn_variant >= 30 && g_attn_variant <= 69) kind = g_attn_variant - 30;  // dev: force a kernel
     if ((kind == 16 || kind == 19) && T > 64) kind = 0;  // the short kernels hold one 64-key tile
     if (g_attn_variant >= 21 && g_attn_variant <= 26 && hd == 72) {  // dev: attn_dma_kernel<72,8,2> diagnostics
         const dim3 grid(cdiv(T, 256) * H * B), blk(512);

@@ -893,6 +893,179 @@ int launch_pipe6(const GemmArgs& a, hipStream_t s) {
 }
 
 // ---------------------------------------------------------------------------
+// pipe8: pipe6's ping-pong schedule on 64-deep stages of whole 128-B cache-line
+// rows. pipe6's DMA pieces are 16 rows x 64 B (half a line per row); a probe of
+// the LDS-DMA path alone (tools/probes/dma_bw.hip, same ring, waits and barriers)
+// moves 8-row x 128-B pieces twice as fast from L2 (126-134 vs 64-77 GB/s per CU).
+// The ring is five 32 KiB units (all 160 KiB of LDS): unit h holds A (h even) or
+// B (h odd) of 64-deep stage h / 2, 256 rows x 128 B, XOR-swizzled like pipe4
+// (logical chunk c of row r at chunk c ^ ((r >> 1) & 7)); unit h lives in slot
+// h % 5. Stage s runs as two 32-deep steps (ks = 0, 1), each a memory phase
+// (12 fragment reads) and a compute phase (32 MFMAs) between raw barriers, the
+// late wave row one barrier behind (pipe6). While stage s runs, the slots of
+// stage s - 1 take units 2s + 3 (B of s + 1; issued in the ks = 0 memory phase)
+// and 2s + 4 (A of s + 2; ks = 1), four 1 KiB pieces per wave each, so every
+// memory phase carries pipe6's four DMA issues. Unit 2s + 3 is read from the
+// early row's first memory phase of stage s + 1: each wave retires its own pieces
+// of it just before the barrier in front of that phase (late row: end of its
+// ks = 1 memory phase; early row: end of its ks = 1 compute phase), about three
+// phases after issuing them. K-step order and per-MFMA k ranges are pipe6's, so
+// the outputs are bit-identical to pipe6. Needs K % 64 == 0 and K >= 192.
+// ---------------------------------------------------------------------------
+template <class C, int ACT, int DIAG>
+__device__ __forceinline__ void pipe8_tile(const GemmArgs& p, char* lds, const int m0, const int n0) {
+    static_assert(C::BM == 256 && C::BN == 256 && C::FN == 4 && C::FM == 8 && C::NW == 8, "pipe8: 256 x 256, 8 waves");
+    constexpr int UNIT = 32768, NSLOT = 5;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wm = wave / C::WN, wn = wave % C::WN;
+    const int g = lane >> 4, li = lane & 15;
+    const bool late = wave >= C::NW / 2;
+
+    // this wave's 4 pieces of a unit: rows (4 wave + q) * 8 + lane / 8, physical chunk lane % 8;
+    // 32-bit byte offsets from the (uniform) operand base (pipe8_ok: operands < 4 GiB)
+    unsigned offA[4], offB[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const int prow = (wave * 4 + q) * 8 + (lane >> 3);
+        const int logical = swz(prow, lane & 7);
+        offA[q] = ((unsigned)min(m0 + prow, p.M - 1) * (unsigned)p.lda + logical * 8) * 2u;
+        offB[q] = ((unsigned)min(n0 + prow, p.N - 1) * (unsigned)p.ldb + logical * 8) * 2u;
+    }
+    const char* gA = reinterpret_cast<const char*>(p.A);
+    const char* gB = reinterpret_cast<const char*>(p.B);
+    auto issue_unit = [&](int h) {
+        char* base = lds + (h % NSLOT) * UNIT + wave * 4096;
+        const unsigned k0 = (unsigned)(h >> 1) * 128u;
+        if (h & 1) {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) glds16(gB + (offB[q] + k0), base + q * 1024);
+        } else {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) glds16(gA + (offA[q] + k0), base + q * 1024);
+        }
+    };
+    const unsigned lds0 = (unsigned)(uintptr_t)(LDS_AS char*)lds;
+    const int sw = (li >> 1) & 7;  // fragment rows differ by multiples of 16: the swizzle depends on li only
+    const unsigned a_row = lds0 + (wm * C::TM + li) * 128, b_row = lds0 + (wn * C::TN + li) * 128;
+    const unsigned c0 = ((0 + g) ^ sw) << 4, c1 = ((4 + g) ^ sw) << 4;
+
+    f32x4 acc[C::FM][C::FN];
+#pragma unroll
+    for (int i = 0; i < C::FM; ++i)
+#pragma unroll
+        for (int j = 0; j < C::FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    bf16x8 b[C::FN], a[8];
+    const int nk = p.K / 64, nunits = 2 * nk;
+
+    auto step = [&](unsigned aa, unsigned bb, int issue_h, int wait_mem, int wait_comp) {
+        // ---- memory phase
+        ds_read16<0>(b[0], bb);
+        ds_read16<2048>(b[1], bb);
+        ds_read16<4096>(b[2], bb);
+        ds_read16<6144>(b[3], bb);
+        ds_read16<0>(a[0], aa);
+        ds_read16<2048>(a[1], aa);
+        ds_read16<4096>(a[2], aa);
+        ds_read16<6144>(a[3], aa);
+        ds_read16<8192>(a[4], aa);
+        ds_read16<10240>(a[5], aa);
+        ds_read16<12288>(a[6], aa);
+        ds_read16<14336>(a[7], aa);
+        if (DIAG != 1 && issue_h >= 0) issue_unit(issue_h);
+        if (wait_mem == 0) vm_wait<0>();
+        else if (wait_mem == 4) vm_wait<4>();
+        lgkm_wait<0>();
+        __builtin_amdgcn_s_barrier();
+        // ---- compute phase
+        __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+#pragma unroll
+            for (int j = 0; j < C::FN; ++j)
+                if (DIAG == 2)
+                    asm volatile("" ::"v"(b[j]), "v"(a[i]));
+                else
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b[j], a[i], acc[i][j], 0, 0, 0);
+        __builtin_amdgcn_s_setprio(0);
+        __builtin_amdgcn_sched_barrier(0);
+        if (wait_comp == 0) vm_wait<0>();
+        else if (wait_comp == 4) vm_wait<4>();
+        __builtin_amdgcn_s_barrier();
+    };
+
+    for (int h = 0; h < NSLOT; ++h) issue_unit(h);
+    vm_wait<12>();  // units 0 and 1 (stage 0) landed
+    __builtin_amdgcn_s_barrier();
+    if (late) __builtin_amdgcn_s_barrier();
+
+    int slot_a = 0;  // (2 s) % 5
+    for (int s = 0; s < nk; ++s) {
+        const int slot_b = slot_a == 4 ? 0 : slot_a + 1;
+        const unsigned aa = a_row + slot_a * UNIT, bb = b_row + slot_b * UNIT;
+        // own pieces of units <= 2 s + 3 (stage s + 1) retired before the barrier in front of
+        // the early row's first memory phase of stage s + 1; unit 2 s + 4 may stay in flight
+        const int keep = 2 * s + 4 < nunits ? 4 : 0;
+        const int need = s + 1 < nk ? keep : -1;
+        step(aa + c0, bb + c0, s >= 1 && 2 * s + 3 < nunits ? 2 * s + 3 : -1, -1, -1);
+        step(aa + c1, bb + c1, s >= 1 && 2 * s + 4 < nunits ? 2 * s + 4 : -1, late ? need : -1, late ? -1 : need);
+        slot_a = slot_a >= 3 ? slot_a - 3 : slot_a + 2;
+    }
+    if (!late) __builtin_amdgcn_s_barrier();
+    vm_wait<0>();
+
+    gemm_epilogue_lds<C, ACT, (DIAG >= 6 && DIAG <= 8 ? DIAG - 5 : 0)>(p, lds, acc, m0, n0, wm, wn, g, li, tid);
+}
+
+template <class C, int GROUP_M, int ACT, int DIAG = 0, bool SPLIT = false>
+__global__ __launch_bounds__(C::NT, 2) void gemm_pipe8_kernel(GemmArgs p) {
+    __shared__ __attribute__((aligned(16))) char lds[5 * 32768];
+    static_assert(Pipe512x128::LDS <= 5 * 32768 && C::LDS_OUT <= 5 * 32768, "pipe8 LDS");
+    const int nbm = (p.M + C::BM - 1) / C::BM;
+    const int tile = xcd_remap(blockIdx.x, gridDim.x);
+    if constexpr (SPLIT) {
+        int m0, n0;
+        if (split_coords(tile, nbm, p.N / C::BN, m0, n0))
+            pipe6_tile<Pipe512x128, ACT, 1, DIAG>(p, lds, m0, n0);
+        else
+            pipe8_tile<C, ACT, DIAG>(p, lds, m0, n0);
+    } else {
+        const int nbn = (p.N + C::BN - 1) / C::BN;
+        int bm, bn;
+        tile_coords<GROUP_M>(tile, nbm, nbn, bm, bn);
+        pipe8_tile<C, ACT, DIAG>(p, lds, bm * C::BM, bn * C::BN);
+    }
+}
+
+__host__ inline bool pipe8_ok(const GemmArgs& a) {
+    return a.K % 64 == 0 && a.K >= 192 && (size_t)a.M * a.lda * 2 < (1ull << 32) && (size_t)a.N * a.ldb * 2 < (1ull << 32);
+}
+
+template <class C, int GROUP_M, int DIAG = 0, bool SPLIT = false>
+int launch_pipe8(const GemmArgs& a, hipStream_t s) {
+    const int nbm = (a.M + C::BM - 1) / C::BM, nbn = (a.N + C::BN - 1) / C::BN;
+    const dim3 grid(SPLIT ? split_tiles(nbm, a.N / C::BN) : nbm * nbn), block(C::NT);
+    switch (a.act) {
+        case MME_ACT_GELU_TANH:
+            hipLaunchKernelGGL((gemm_pipe8_kernel<C, GROUP_M, MME_ACT_GELU_TANH, DIAG, SPLIT>), grid, block, 0, s, a);
+            break;
+        case MME_ACT_QUICK_GELU:
+            hipLaunchKernelGGL((gemm_pipe8_kernel<C, GROUP_M, MME_ACT_QUICK_GELU, DIAG, SPLIT>), grid, block, 0, s, a);
+            break;
+        case MME_ACT_GELU_ERF:
+            hipLaunchKernelGGL((gemm_pipe8_kernel<C, GROUP_M, MME_ACT_GELU_ERF, DIAG, SPLIT>), grid, block, 0, s, a);
+            break;
+        case MME_ACT_GEGLU_TANH:
+            hipLaunchKernelGGL((gemm_pipe8_kernel<C, GROUP_M, MME_ACT_GEGLU_TANH, DIAG, SPLIT>), grid, block, 0, s, a);
+            break;
+        default:
+            hipLaunchKernelGGL((gemm_pipe8_kernel<C, GROUP_M, MME_ACT_NONE, DIAG, SPLIT>), grid, block, 0, s, a);
+            break;
+    }
+    return mme_check_launch("mme_gemm");
+}
+
+// ---------------------------------------------------------------------------
 // pers: persistent pipe6. One 8-wave workgroup per CU walks its XCD's share of
 // the tile sequence (the same 4-row-band order as pipe6, each XCD a contiguous
 // range), and the per-tile fixed cost of pipe6 (prologue fill, LDS-staged
@@ -1453,7 +1626,7 @@ extern "C" int mme_gemm_res_stats(const void* A, int lda, const void* B, int ldb
     hipStream_t s = as_stream(stream);
     GemmArgs a{(const bf16*)A, (const bf16*)B, Cp, (const bf16*)bias, (const bf16*)residual,
                lda, ldb, ldc, ldr, M, N, K, 0, MME_ACT_NONE, 0, 0, nullptr, nullptr, nullptr, row_part};
-    const bool fused = g_variant < 0 && ldc % 8 == 0 && ((uintptr_t)Cp & 15) == 0 && ldr % 8 == 0 &&
+    const bool fused = (g_variant < 0 || g_variant == 47) && ldc % 8 == 0 && ((uintptr_t)Cp & 15) == 0 && ldr % 8 == 0 &&
                        ((uintptr_t)residual & 15) == 0 && (long)M * N >= 1024L * 1024;
     if (!fused) {  // shapes the pipelined kernel does not take: GEMM, then the row statistics pass
         a.row_part = nullptr;
@@ -1461,10 +1634,10 @@ extern "C" int mme_gemm_res_stats(const void* A, int lda, const void* B, int ldb
         if (rc != MME_OK) return rc;
         return mme_rowstats(Cp, ldc, M, N, eps, row_stats, stream);
     }
-    if (N % 256 == 128)
-        launch_pipe6<Pipe256, 4, 1, 0, true>(a, s);
+    if (pipe8_ok(a) && g_variant != 47)  // variant 47: pipe6 (tests: pipe8 is bit-identical to it)
+        N % 256 == 128 ? launch_pipe8<Pipe256, 4, 0, true>(a, s) : launch_pipe8<Pipe256, 4>(a, s);
     else
-        launch_pipe6<Pipe256, 4, 1>(a, s);
+        N % 256 == 128 ? launch_pipe6<Pipe256, 4, 1, 0, true>(a, s) : launch_pipe6<Pipe256, 4, 1>(a, s);
     const int rc = mme_check_launch("mme_gemm_res_stats");
     if (rc != MME_OK) return rc;
     hipLaunchKernelGGL(row_part_combine_kernel, dim3(cdiv(M, 256)), dim3(256), 0, s, row_part, row_stats, M, N / 128,
@@ -1502,6 +1675,7 @@ int gemm_dispatch(GemmArgs a, hipStream_t s) {
     if (glu) {  // gated epilogue: the pipelined kernel only (its LDS-staged 16-B tile rows pair gate/up)
         MME_REQUIRE(N % 8 == 0 && ldc % 4 == 0 && !out_f32 && !residual && ((uintptr_t)Cp & 7) == 0,
                     "mme_gemm: GeGLU needs N %% 8 == 0, ldc %% 4 == 0, 8-B aligned bf16 C, no residual");
+        if (pipe8_ok(a) && g_variant != 47) return launch_pipe8<Pipe256, 4>(a, s);
         return launch_pipe6<Pipe256, 4, 1>(a, s);
     }
     switch (g_variant) {
@@ -1535,7 +1709,7 @@ int gemm_dispatch(GemmArgs a, hipStream_t s) {
         case 49:  // dev: epilogue stored straight from the accumulators (no LDS staging)
             if (a.N % 256 == 128) return launch_pipe6<Pipe256, 4, 1, 11, true>(a, s);
             return launch_pipe6<Pipe256, 4, 1, 11>(a, s);
-        case 47:  // split grid (512 x 128 tiles for the last 128 columns) where N = 256 k + 128
+        case 47:  // pipe6 as dispatched before pipe8: split grid (512 x 128 tiles for the last 128 columns) where N = 256 k + 128
             if (a.N % 256 == 128) return launch_pipe6<Pipe256, 4, 1, 0, true>(a, s);
             return launch_pipe6<Pipe256, 4, 1>(a, s);
         case 46: return launch_pipe6<PCfg<256, 256, 2, 4, 3>, 4, 1>(a, s);  // dev: 3-deep ring (2 stages ahead)
@@ -1551,6 +1725,19 @@ int gemm_dispatch(GemmArgs a, hipStream_t s) {
         case 62:  // diagnostic: persistent, no epilogue
             if (pers_ok(a)) return launch_pers<Pipe256, 4, 2>(a, s);
             break;
+        case 64:  // dev: pipe8 (64-deep stages of whole-line rows, 5-unit ring), split grid where N = 256 k + 128
+            if (!pipe8_ok(a)) break;
+            if (N % 256 == 128) return launch_pipe8<Pipe256, 4, 0, true>(a, s);
+            return launch_pipe8<Pipe256, 4>(a, s);
+        case 65:  // diagnostic: pipe8 without an epilogue
+            if (!pipe8_ok(a)) break;
+            return launch_pipe8<Pipe256, 4, 7>(a, s);
+        case 66:  // diagnostic: pipe8, prologue DMA only (the ring is never refilled)
+            if (!pipe8_ok(a)) break;
+            return launch_pipe8<Pipe256, 4, 1>(a, s);
+        case 67:  // diagnostic: pipe8 without MFMAs
+            if (!pipe8_ok(a)) break;
+            return launch_pipe8<Pipe256, 4, 2>(a, s);
         case 54: return launch_pipe6<Pipe256, 2, 1>(a, s);   // dev: 2-row tile bands
         case 55: return launch_pipe6<Pipe256, 16, 1>(a, s);  // dev: 16-row tile bands
         case 50: return launch_pipe7<Pipe256w, 4>(a, s);
@@ -1564,7 +1751,14 @@ int gemm_dispatch(GemmArgs a, hipStream_t s) {
     const bool vec_ok = !out_f32 && ldc % 8 == 0 && ((uintptr_t)Cp & 15) == 0 &&
                         (!residual || (ldr % 8 == 0 && ((uintptr_t)residual & 15) == 0)) && N % 8 == 0;
     if (vec_ok && (long)M * N >= 1024L * 1024) {
+        // pipe8 (64-deep stages of whole-line rows) where K allows: bit-identical to pipe6,
+        // fc1 1130 -> 1183, QKV 1112 -> 1155, o_proj 1028 -> 1082-1109, fc2 1192 -> 1291 TF/s
+        // (bias epilogue, M = 186 624; profiles/r02_pipe8_ab.log)
         // N = 256 k + 128: split grid (fc2 1144 -> 1200 TF/s, o_proj +5 %, QKV +1.6 %)
+        if (pipe8_ok(a)) {
+            if (N % 256 == 128) return launch_pipe8<Pipe256, 4, 0, true>(a, s);
+            return launch_pipe8<Pipe256, 4>(a, s);
+        }
         if (N % 256 == 128) return launch_pipe6<Pipe256, 4, 1, 0, true>(a, s);
         return launch_pipe6<Pipe256, 4, 1>(a, s);
     }

@@ -16,7 +16,7 @@ sys.path.insert(0, os.path.join(ROOT, "multimodal-embedding_amd"))
 import torch  # noqa: E402
 from mme import _lib, ops  # noqa: E402
 
-DIAG_VARIANTS = {22, 23, 26, 27, 33, 34, 35, 36, 37, 38, 39, 52, 53}  # diagnostic builds with deliberately wrong results
+DIAG_VARIANTS = {22, 23, 26, 27, 33, 34, 35, 36, 37, 38, 39, 52, 53, 65}  # diagnostic builds with deliberately wrong results
 SHAPES = {  # name: (N, K)  with M = rows (SigLIP vision: 256 images x 729 tokens)
     "qkv": (3456, 1152), "o_proj": (1152, 1152), "fc1": (4352, 1152), "fc2": (1152, 4352),
     # DFN5B-H / ViT-H (d 1280, I 5120): rows 256 x 730
@@ -67,6 +67,7 @@ def main():
             if has_var:
                 lib.mme_gemm_variant(v)  # -1 = production dispatch
             run()
+            err = float("nan")
             if ref is None or a.epi in ("res", "resstats"):
                 ref = C.clone()
             else:
@@ -87,7 +88,8 @@ def main():
                 ms = min(ms, s.elapsed_time(e) / a.iters)
             tf = 2.0 * M * N * K / ms / 1e9
             res[f"{name}/v{v}"] = {"ms": round(ms, 4), "tflops": round(tf, 1)}
-            print(f"{name:7s} v{v:<2d} M={M} N={N} K={K} epi={a.epi}: {ms:8.3f} ms  {tf:7.1f} TFLOP/s", flush=True)
+            print(f"{name:7s} v{v:<2d} M={M} N={N} K={K} epi={a.epi}: {ms:8.3f} ms  {tf:7.1f} TFLOP/s  "
+                  f"max|diff| vs first {err:.3g}", flush=True)
         if a.torch:  # vendor library baseline on the same operands (bias-free X @ W^T)
             Ct = torch.nn.functional.linear(A, W)
             err = (Ct.float() - ref.float()).abs().max().item() if (ref is not None and a.epi == "none") else 0.0

@@ -25,7 +25,7 @@ def load(d, counter):
 
 
 def family(name):
-    for k in ("gemm_pipe6_kernel", "gemm_pipe4_kernel", "gemm_pipe3_kernel", "gemm_tn_kernel", "attn_fwd_kernel",
+    for k in ("gemm_pipe8_kernel", "gemm_pipe6_kernel", "gemm_pipe4_kernel", "gemm_pipe3_kernel", "gemm_tn_kernel", "attn_fwd_kernel",
               "attn_pipe_kernel", "attn_dma_kernel", "layernorm_kernel", "sim_topk_kernel",
               "resample_v_patch_kernel", "probe_attn_kernel"):
         if k in name:
