@@ -555,7 +555,7 @@ __device__ __forceinline__ float xsum32(float v) {
 template <int HD, int NW, int NSTG, bool PIPE, bool ONES, bool LAZY, bool PING = false, int MINW = 1, bool UNR = false,
           int XF = 0>
 __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(MINW))) void attn_pipe_kernel(AttnArgs a) {
-    constexpr bool ADMA = XF & 1, PKX = XF & 2, PRIO = XF & 4;
+    constexpr bool ADMA = XF & 1, PKX = XF & 2, PRIO = XF & 4, NODMA = XF & 8;  // 8: diagnostic, no K/V DMA (wrong results)
     static_assert(!PIPE || NSTG == 3, "the pipelined loop keeps tile t+1 resident while t+2 lands");
     static_assert(!PING || (!PIPE && NSTG == 4), "ping-pong: two tiles resident beside the one landing");
     static_assert(!ONES || HD == 72, "the ones column lives in the padding of the 80-wide V^T tiles");
@@ -617,6 +617,7 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(MINW)))
 
     const int nmine = (NINS - wave + NW - 1) / NW;
     auto issue = [&](int t) {
+        if (NODMA && t > 0) return;
         char* tb = lds + (t % NSTG) * TILE;
 #pragma unroll
         for (int i = 0; i < MAXI; ++i) {
@@ -1185,6 +1186,9 @@ void launch_attn(int kind, const AttnArgs& a, int B, int T, int H, hipStream_t s
                            dim3(cdiv(T, 256) * H * B), dim3(512), 0, st, a);
     else if (kind == 30)  // dev: kind 27 with static priority for waves NW/2..
         hipLaunchKernelGGL((attn_pipe_kernel<HD, 8, 2, false, HD == 72, true, false, 4, true, 4>),
+                           dim3(cdiv(T, 256) * H * B), dim3(512), 0, st, a);
+    else if (kind == 32)  // diagnostic: kind 27 with only the first K/V tile staged (wrong results)
+        hipLaunchKernelGGL((attn_pipe_kernel<HD, 8, 2, false, HD == 72, true, false, 4, true, 8>),
                            dim3(cdiv(T, 256) * H * B), dim3(512), 0, st, a);
     else if (kind == 31)  // dev: both
         hipLaunchKernelGGL((attn_pipe_kernel<HD, 8, 2, false, HD == 72, true, false, 4, true, 6>),

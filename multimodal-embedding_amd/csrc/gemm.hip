@@ -1732,6 +1732,15 @@ int gemm_dispatch(GemmArgs a, hipStream_t s) {
         case 65:  // diagnostic: pipe8 without an epilogue
             if (!pipe8_ok(a)) break;
             return launch_pipe8<Pipe256, 4, 7>(a, s);
+        case 68:  // dev: pipe8, 2-row tile bands (no split grid)
+            if (!pipe8_ok(a)) break;
+            return launch_pipe8<Pipe256, 2>(a, s);
+        case 69:  // dev: pipe8, 8-row tile bands (no split grid)
+            if (!pipe8_ok(a)) break;
+            return launch_pipe8<Pipe256, 8>(a, s);
+        case 70:  // dev: pipe8, 4-row tile bands (no split grid)
+            if (!pipe8_ok(a)) break;
+            return launch_pipe8<Pipe256, 4>(a, s);
         case 66:  // diagnostic: pipe8, prologue DMA only (the ring is never refilled)
             if (!pipe8_ok(a)) break;
             return launch_pipe8<Pipe256, 4, 1>(a, s);

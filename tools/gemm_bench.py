@@ -16,7 +16,7 @@ sys.path.insert(0, os.path.join(ROOT, "multimodal-embedding_amd"))
 import torch  # noqa: E402
 from mme import _lib, ops  # noqa: E402
 
-DIAG_VARIANTS = {22, 23, 26, 27, 33, 34, 35, 36, 37, 38, 39, 52, 53, 65}  # diagnostic builds with deliberately wrong results
+DIAG_VARIANTS = {22, 23, 26, 27, 33, 34, 35, 36, 37, 38, 39, 52, 53, 65, 66, 67}  # diagnostic builds with deliberately wrong results
 SHAPES = {  # name: (N, K)  with M = rows (SigLIP vision: 256 images x 729 tokens)
     "qkv": (3456, 1152), "o_proj": (1152, 1152), "fc1": (4352, 1152), "fc2": (1152, 4352),
     # DFN5B-H / ViT-H (d 1280, I 5120): rows 256 x 730
