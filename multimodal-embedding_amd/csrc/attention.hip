@@ -556,6 +556,7 @@ template <int HD, int NW, int NSTG, bool PIPE, bool ONES, bool LAZY, bool PING =
           int XF = 0>
 __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(MINW))) void attn_pipe_kernel(AttnArgs a) {
     constexpr bool ADMA = XF & 1, PKX = XF & 2, PRIO = XF & 4, NODMA = XF & 8;  // 8: diagnostic, no K/V DMA (wrong results)
+    constexpr bool WIDE = XF & 16;  // 16: O stored as 16-B rows (v_permlane16_swap pairs of d-tiles)
     static_assert(!PIPE || NSTG == 3, "the pipelined loop keeps tile t+1 resident while t+2 lands");
     static_assert(!PING || (!PIPE && NSTG == 4), "ping-pong: two tiles resident beside the one landing");
     static_assert(!ONES || HD == 72, "the ones column lives in the padding of the 80-wide V^T tiles");
@@ -860,7 +861,38 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(MINW)))
             ltot = xsum32(xsum16(lsum[u]));
         const float inv = 1.0f / ltot;
         const int q = qw0 + u * 16 + li;
-        if (q < T) {
+        if (WIDE) {
+            // d-tile pairs (dt, dt + 1): after v_permlane16_swap of the packed halves, the lanes
+            // of lane-row g hold 8 consecutive columns 16 (dt + (g & 1)) + 8 (g >> 1) .. + 7
+            // (same values and addresses as the 8-B stores, half the store instructions)
+            bf16* orow = a.out + ((long)b * T + min(q, T - 1)) * a.ldo + h * HD;
+#pragma unroll
+            for (int dt = 0; dt + 1 < NDT && (dt + 2) * 16 <= HD; dt += 2) {
+                bf16x4 v0, v1;
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    v0[r] = f2bf(o[u][dt][r] * inv);
+                    v1[r] = f2bf(o[u][dt + 1][r] * inv);
+                }
+                uint2 x = __builtin_bit_cast(uint2, v0), y = __builtin_bit_cast(uint2, v1);
+                const auto sx = __builtin_amdgcn_permlane16_swap(x.x, y.x, false, false);
+                const auto sy = __builtin_amdgcn_permlane16_swap(x.y, y.y, false, false);
+                if (q < T)
+                    *reinterpret_cast<uint4*>(orow + 16 * (dt + (g & 1)) + 8 * (g >> 1)) =
+                        make_uint4(sx[0], sy[0], sx[1], sy[1]);
+            }
+            constexpr int DT0 = (HD / 32) * 2;  // first d-tile not covered by a whole pair
+#pragma unroll
+            for (int dt = DT0; dt < NDT; ++dt) {
+                const int d0 = dt * 16 + 4 * g;
+                if (q < T && d0 < HD) {
+                    bf16x4 v;
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) v[r] = f2bf(o[u][dt][r] * inv);
+                    *reinterpret_cast<bf16x4*>(orow + d0) = v;
+                }
+            }
+        } else if (q < T) {
             bf16* orow = a.out + ((long)b * T + q) * a.ldo + h * HD;
 #pragma unroll
             for (int dt = 0; dt < NDT; ++dt) {
@@ -1070,7 +1102,16 @@ __global__ __launch_bounds__(256) void probe_attn_kernel(const bf16* __restrict_
     __shared__ float qs[128];
     __shared__ float red[4][128];
     __shared__ float stat[8];
-    const int h = blockIdx.x, b = blockIdx.y, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    // XCD-aware: the H heads of one sequence (which share the 128-B lines of its K / V rows) run
+    // on one XCD; with blockIdx = head they were spread over all eight L2s and every line was
+    // fetched by two of them (2.7 GB fetched per 239-image launch for 0.8 GB of K / V)
+    int id;
+    {
+        const int bid = blockIdx.x, nwg = gridDim.x;
+        const int xcd = bid & 7, loc = bid >> 3, q8 = nwg >> 3, r8 = nwg & 7;
+        id = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + loc;
+    }
+    const int h = id % H, b = id / H, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int D = H * hd;
     if (tid < hd) qs[tid] = bf2f(qv[h * hd + tid]);
     __syncthreads();
@@ -1184,11 +1225,18 @@ void launch_attn(int kind, const AttnArgs& a, int B, int T, int H, hipStream_t s
     else if (kind == 29)  // dev: kind 27 with packed exp-argument FMAs
         hipLaunchKernelGGL((attn_pipe_kernel<HD, 8, 2, false, HD == 72, true, false, 4, true, 2>),
                            dim3(cdiv(T, 256) * H * B), dim3(512), 0, st, a);
-    else if (kind == 30)  // dev: kind 27 with static priority for waves NW/2..
+    else if (kind == 30)  // kind 27 with static priority (s_setprio 1) for waves NW/2..: production for hd 72,
+                          // +1-2 % per launch, bit-identical (profiles/r02_attn_wide_prio_ab.log)
         hipLaunchKernelGGL((attn_pipe_kernel<HD, 8, 2, false, HD == 72, true, false, 4, true, 4>),
                            dim3(cdiv(T, 256) * H * B), dim3(512), 0, st, a);
     else if (kind == 32)  // diagnostic: kind 27 with only the first K/V tile staged (wrong results)
         hipLaunchKernelGGL((attn_pipe_kernel<HD, 8, 2, false, HD == 72, true, false, 4, true, 8>),
+                           dim3(cdiv(T, 256) * H * B), dim3(512), 0, st, a);
+    else if (kind == 33)  // dev: kind 27 with 16-B O stores (slower: 615 vs 630-650 TF/s)
+        hipLaunchKernelGGL((attn_pipe_kernel<HD, 8, 2, false, HD == 72, true, false, 4, true, 16>),
+                           dim3(cdiv(T, 256) * H * B), dim3(512), 0, st, a);
+    else if (kind == 34)  // dev: kind 27 with 16-B O stores + static priority
+        hipLaunchKernelGGL((attn_pipe_kernel<HD, 8, 2, false, HD == 72, true, false, 4, true, 20>),
                            dim3(cdiv(T, 256) * H * B), dim3(512), 0, st, a);
     else if (kind == 31)  // dev: both
         hipLaunchKernelGGL((attn_pipe_kernel<HD, 8, 2, false, HD == 72, true, false, 4, true, 6>),
@@ -1232,6 +1280,8 @@ extern "C" int mme_attention(const void* qkv, int ld_qkv, void* out, int ld_out,
     // its 3 spilled registers live outside the tile loop), so two 8-wave blocks share a CU and
     // each SIMD interleaves 4 waves: 1.18 -> 0.98 ms per 256-image layer (532 -> 638 TF/s).
     // At head dim 80 the same cap spills inside the loop and gains nothing (DFN5B 0.628 / 0.622 ms).
+    // Round 2: the tile loop unrolled by the ring depth (kind 27: compile-time ring slots, 611-623 ->
+    // 637-639 TF/s) and static priority for the second half of the waves (kind 30, +1-2 %).
     // 9-wave blocks (288 queries, kind 21) when they pad far less than 256 / 128-query blocks: ViT-H
     // (T 257, hd 80) runs one block per batch-head, K/V staged once instead of three times and 288
     // padded query rows instead of 384: 0.342 -> 0.277 ms per 256-image layer (253 -> 313 TF/s).
@@ -1244,7 +1294,7 @@ extern "C" int mme_attention(const void* qkv, int ld_qkv, void* out, int ld_out,
                : (T <= 128 || hd == 64) ? 0
                : pad9 * 10 < min(pad8, pad4) * 9 ? 21
                : (hd == 80 && pad12 <= pad8 && pad12 * 10 <= pad4 * 11) ? 23
-               : (pad8 * 10 <= pad4 * 11 ? (hd == 72 ? 27 : 11) : 14);
+               : (pad8 * 10 <= pad4 * 11 ? (hd == 72 ? 30 : 11) : 14);
     if (g_attn_variant >= 1 && g_attn_variant <= 4 && hd == 72) {  // dev-only diagnostic builds
         const dim3 grid(cdiv(T, 128) * H * B);
         switch (g_attn_variant) {
@@ -1287,7 +1337,7 @@ extern "C" int mme_probe_attention(const void* q, const void* kv, int ld_kv, voi
     MME_REQUIRE(hd % 8 == 0 && hd <= 128, "mme_probe_attention: head_dim %d unsupported", hd);
     MME_REQUIRE(ld_kv % 8 == 0 && ld_kv >= 2 * H * hd, "mme_probe_attention: bad ld_kv");
     if (B == 0) return MME_OK;
-    hipLaunchKernelGGL(probe_attn_kernel, dim3(H, B), dim3(256), 0, as_stream(stream), (const bf16*)q,
+    hipLaunchKernelGGL(probe_attn_kernel, dim3(H * B), dim3(256), 0, as_stream(stream), (const bf16*)q,
                        (const bf16*)kv, ld_kv, (bf16*)out, ld_out, T, H, hd, scale);
     return mme_check_launch("mme_probe_attention");
 }

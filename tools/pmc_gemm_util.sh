@@ -1,8 +1,8 @@
 #!/bin/bash
 # Issue / MFMA-busy / clock counters of the production GEMM (pipe8) on one encoder shape
 # (tools/gemm_bench.py, default fc1 at M = 186 624), one rocprofv3 --pmc pass per counter
-# group (kernel trace only). Per dispatch: GRBM_GUI_ACTIVE / kernel time = the clock the chip
-# held; SQ_VALU_MFMA_BUSY_CYCLES / (SQ_BUSY_CYCLES x 4 SIMDs) ~ MFMA pipe utilisation.
+# group (kernel trace only). Per dispatch: GRBM_GUI_ACTIVE / 8 XCDs / kernel time = the clock
+# the chip held; SQ_VALU_MFMA_BUSY_CYCLES / (1024 SIMDs x those cycles) = MFMA pipe utilisation.
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 export TMPDIR=/tmp
 OUT=gpurun_out/pmc_gemm_util
@@ -27,22 +27,23 @@ for f in glob.glob("gpurun_out/pmc_gemm_util/**/*counter_collection.csv", recurs
             continue
         k = k[:100]
         acc[k][r["Counter_Name"]] += float(r["Counter_Value"])
-        cnt[k].add((f, r.get("Dispatch_Id")))
+        cnt[(k, r["Counter_Name"])].add((f, r.get("Dispatch_Id")))
 for f in glob.glob("gpurun_out/pmc_gemm_util/**/*kernel_trace.csv", recursive=True):
     for r in csv.DictReader(open(f)):
         if "gemm_pipe" in r["Kernel_Name"]:
             dur[r["Kernel_Name"][:100]].append(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
 out = {}
 for k, d in acc.items():
-    n = max(len(cnt[k]), 1)
-    row = {"dispatches": n, **{c: v / n for c, v in sorted(d.items())}}
+    # each counter comes from one pass: average over the dispatches of that pass
+    row = {"dispatches": max(len(cnt[(k, c)]) for c in d),
+           **{c: v / max(len(cnt[(k, c)]), 1) for c, v in sorted(d.items())}}
     if dur[k]:
         ns = sum(dur[k]) / len(dur[k])
         row["avg_ns"] = ns
-        if "GRBM_GUI_ACTIVE" in row:
-            row["clock_ghz"] = row["GRBM_GUI_ACTIVE"] / ns
-        if "SQ_BUSY_CYCLES" in row and "SQ_VALU_MFMA_BUSY_CYCLES" in row:
-            row["mfma_busy_frac"] = row["SQ_VALU_MFMA_BUSY_CYCLES"] / (4 * row["SQ_BUSY_CYCLES"])
+        if "GRBM_GUI_ACTIVE" in row:  # summed over the 8 XCDs
+            row["clock_ghz"] = row["GRBM_GUI_ACTIVE"] / 8 / ns
+            if "SQ_VALU_MFMA_BUSY_CYCLES" in row:  # over 256 CUs x 4 SIMDs at that clock
+                row["mfma_busy_frac"] = row["SQ_VALU_MFMA_BUSY_CYCLES"] / (1024 * row["GRBM_GUI_ACTIVE"] / 8)
     out[k] = row
 json.dump(out, open("gpurun_out/pmc_gemm_util/summary.json", "w"), indent=1)
 print(json.dumps(out, indent=1))
