@@ -892,6 +892,106 @@ int launch_pipe6(const GemmArgs& a, hipStream_t s) {
     return mme_check_launch("mme_gemm");
 }
 
+// Per-wave epilogue (pipe8 WEPI): each wave stages ONLY its own 128 x 64 sub-tile in its
+// own 18 KiB LDS region (row pitch 144 B), reads it back as 16-B row chunks (8 rows x 128 B
+// per store instruction) and stores it -- no workgroup barrier, so the early wave row's
+// epilogue runs beside the late row's last MFMAs and each wave leaves as soon as it is done.
+// Same arithmetic as gemm_epilogue_lds step for step (bit-identical outputs); no row
+// statistics (mme_gemm_res_stats keeps the block-wide epilogue).
+template <class C, int ACT>
+__device__ __forceinline__ void gemm_epilogue_wave(const GemmArgs& p, char* lds, f32x4 (&acc)[C::FM][C::FN], int m0,
+                                                   int n0, int wave, int wm, int wn, int g, int li, int lane) {
+    static_assert(C::TM == 128 && C::TN == 64 && C::FM == 8 && C::FN == 4, "per-wave epilogue: 128 x 64 wave tiles");
+    constexpr bool GLU = ACT == MME_ACT_GEGLU_TANH;
+    constexpr int RACT = GLU ? MME_ACT_NONE : ACT;
+    constexpr int PITCH = 144, REGION = 128 * PITCH;
+    char* reg = lds + wave * REGION;
+    const int rm0 = m0 + wm * C::TM, cn0 = n0 + wn * C::TN;  // this wave's sub-tile origin
+    const int rr = lane >> 3, cc = lane & 7;                 // store phase: row rr of 8, 16-B chunk cc
+    u16x8 rv[16];
+    if (!GLU && p.res) {  // residual rows first: their latency overlaps the staging below
+#pragma unroll
+        for (int q = 0; q < 16; ++q) {
+            const int gr = min(rm0 + q * 8 + rr, p.M - 1), gc = min(cn0 + cc * 8, p.N - 8);
+            const int r2 = p.res_period ? gr % p.res_period : gr;
+            rv[q] = *reinterpret_cast<const u16x8*>(p.res + (size_t)r2 * p.ldr + gc);
+        }
+    }
+    float lr[C::FM], lm[C::FM];
+    if (p.ln_stats) {
+#pragma unroll
+        for (int i = 0; i < C::FM; ++i) {
+            const int gr = min(rm0 + i * 16 + li, p.M - 1);
+            const float2 st = *reinterpret_cast<const float2*>(p.ln_stats + 2 * gr);
+            lr[i] = st.y;
+            lm[i] = -st.y * st.x;
+        }
+    }
+#pragma unroll
+    for (int j = 0; j < C::FN; ++j) {
+        const int nl = j * 16 + 4 * g;  // within the wave's 64 columns
+        float bv[4] = {0.f, 0.f, 0.f, 0.f}, cs[4] = {0.f, 0.f, 0.f, 0.f};
+        if (p.ln_stats) {
+            const int c4 = min(cn0 + nl, p.N - 4);
+            const float4 b4 = *reinterpret_cast<const float4*>(p.ln_b + c4);
+            const float4 s4 = *reinterpret_cast<const float4*>(p.ln_cs + c4);
+            bv[0] = b4.x, bv[1] = b4.y, bv[2] = b4.z, bv[3] = b4.w;
+            cs[0] = s4.x, cs[1] = s4.y, cs[2] = s4.z, cs[3] = s4.w;
+        } else if (p.bias) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) bv[r] = bf2f(p.bias[min(cn0 + nl + r, p.N - 1)]);
+        }
+#pragma unroll
+        for (int i = 0; i < C::FM; ++i) {
+            bf16x4 o;
+            if (p.ln_stats) {
+#pragma unroll
+                for (int r = 0; r < 4; r += 2) {
+                    const f32x2 y = apply_act2(
+                        pk_fma(f32x2{lr[i], lr[i]}, f32x2{acc[i][j][r], acc[i][j][r + 1]},
+                               pk_fma(f32x2{lm[i], lm[i]}, f32x2{cs[r], cs[r + 1]}, f32x2{bv[r], bv[r + 1]})),
+                        RACT);
+                    o[r] = f2bf(y.x);
+                    o[r + 1] = f2bf(y.y);
+                }
+            } else {
+#pragma unroll
+                for (int r = 0; r < 4; r += 2) {
+                    const f32x2 y =
+                        apply_act2(f32x2{acc[i][j][r], acc[i][j][r + 1]} + f32x2{bv[r], bv[r + 1]}, RACT);
+                    o[r] = f2bf(y.x);
+                    o[r + 1] = f2bf(y.y);
+                }
+            }
+            *reinterpret_cast<bf16x4*>(reg + (i * 16 + li) * PITCH + nl * 2) = o;
+        }
+    }
+    // the wave's own LDS writes precede its reads (LDS executes one wave's instructions in order)
+    bf16* Cout = reinterpret_cast<bf16*>(p.C);
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+        const int row = q * 8 + rr;
+        const int gr = rm0 + row, gc = cn0 + cc * 8;
+        const u16x8 v = *reinterpret_cast<const u16x8*>(reg + row * PITCH + cc * 16);
+        if (gr >= p.M || gc >= p.N) continue;
+        if (GLU) {
+            u16x4 o;
+#pragma unroll
+            for (int e = 0; e < 4; ++e)
+                o[e] = __builtin_bit_cast(unsigned short,
+                                          f2bf(bf2f(f2bf(apply_act(bits2f(v[e]), MME_ACT_GELU_TANH))) * bits2f(v[4 + e])));
+            __builtin_nontemporal_store(o, reinterpret_cast<u16x4*>(Cout + (size_t)gr * p.ldc + gc / 2));
+        } else if (p.res) {
+            u16x8 o;
+#pragma unroll
+            for (int e = 0; e < 8; ++e) o[e] = __builtin_bit_cast(unsigned short, f2bf(bits2f(v[e]) + bits2f(rv[q][e])));
+            __builtin_nontemporal_store(o, reinterpret_cast<u16x8*>(Cout + (size_t)gr * p.ldc + gc));
+        } else {
+            __builtin_nontemporal_store(v, reinterpret_cast<u16x8*>(Cout + (size_t)gr * p.ldc + gc));
+        }
+    }
+}
+
 // ---------------------------------------------------------------------------
 // pipe8: pipe6's ping-pong schedule on 64-deep stages of whole 128-B cache-line
 // rows. pipe6's DMA pieces are 16 rows x 64 B (half a line per row); a probe of
@@ -912,7 +1012,7 @@ int launch_pipe6(const GemmArgs& a, hipStream_t s) {
 // phases after issuing them. K-step order and per-MFMA k ranges are pipe6's, so
 // the outputs are bit-identical to pipe6. Needs K % 64 == 0 and K >= 192.
 // ---------------------------------------------------------------------------
-template <class C, int ACT, int DIAG>
+template <class C, int ACT, int DIAG, bool WEPI = false>
 __device__ __forceinline__ void pipe8_tile(const GemmArgs& p, char* lds, const int m0, const int n0) {
     static_assert(C::BM == 256 && C::BN == 256 && C::FN == 4 && C::FM == 8 && C::NW == 8, "pipe8: 256 x 256, 8 waves");
     constexpr int UNIT = 32768, NSLOT = 5;
@@ -958,7 +1058,7 @@ __device__ __forceinline__ void pipe8_tile(const GemmArgs& p, char* lds, const i
     bf16x8 b[C::FN], a[8];
     const int nk = p.K / 64, nunits = 2 * nk;
 
-    auto step = [&](unsigned aa, unsigned bb, int issue_h, int wait_mem, int wait_comp) {
+    auto step = [&](unsigned aa, unsigned bb, int issue_h, int wait_mem, int wait_comp, bool end_barrier = true) {
         // ---- memory phase
         ds_read16<0>(b[0], bb);
         ds_read16<2048>(b[1], bb);
@@ -991,7 +1091,7 @@ __device__ __forceinline__ void pipe8_tile(const GemmArgs& p, char* lds, const i
         __builtin_amdgcn_sched_barrier(0);
         if (wait_comp == 0) vm_wait<0>();
         else if (wait_comp == 4) vm_wait<4>();
-        __builtin_amdgcn_s_barrier();
+        if (end_barrier) __builtin_amdgcn_s_barrier();
     };
 
     for (int h = 0; h < NSLOT; ++h) issue_unit(h);
@@ -1008,16 +1108,24 @@ __device__ __forceinline__ void pipe8_tile(const GemmArgs& p, char* lds, const i
         const int keep = 2 * s + 4 < nunits ? 4 : 0;
         const int need = s + 1 < nk ? keep : -1;
         step(aa + c0, bb + c0, s >= 1 && 2 * s + 3 < nunits ? 2 * s + 3 : -1, -1, -1);
-        step(aa + c1, bb + c1, s >= 1 && 2 * s + 4 < nunits ? 2 * s + 4 : -1, late ? need : -1, late ? -1 : need);
+        // WEPI: the late row's last compute phase ends without the barrier the early row would
+        // otherwise wait in (equal barrier counts: the early row skips its closing one below)
+        step(aa + c1, bb + c1, s >= 1 && 2 * s + 4 < nunits ? 2 * s + 4 : -1, late ? need : -1, late ? -1 : need,
+             !(WEPI && late && s + 1 == nk));
         slot_a = slot_a >= 3 ? slot_a - 3 : slot_a + 2;
     }
-    if (!late) __builtin_amdgcn_s_barrier();
     vm_wait<0>();
-
-    gemm_epilogue_lds<C, ACT, (DIAG >= 6 && DIAG <= 8 ? DIAG - 5 : 0)>(p, lds, acc, m0, n0, wm, wn, g, li, tid);
+    if constexpr (WEPI) {
+        // no LDS hazard: every wave's last fragment reads precede the barrier closing the late
+        // row's last memory phase, which the early row passes before it starts writing
+        gemm_epilogue_wave<C, ACT>(p, lds, acc, m0, n0, wave, wm, wn, g, li, lane);
+    } else {
+        if (!late) __builtin_amdgcn_s_barrier();
+        gemm_epilogue_lds<C, ACT, (DIAG >= 6 && DIAG <= 8 ? DIAG - 5 : 0)>(p, lds, acc, m0, n0, wm, wn, g, li, tid);
+    }
 }
 
-template <class C, int GROUP_M, int ACT, int DIAG = 0, bool SPLIT = false>
+template <class C, int GROUP_M, int ACT, int DIAG = 0, bool SPLIT = false, bool WEPI = false>
 __global__ __launch_bounds__(C::NT, 2) void gemm_pipe8_kernel(GemmArgs p) {
     __shared__ __attribute__((aligned(16))) char lds[5 * 32768];
     static_assert(Pipe512x128::LDS <= 5 * 32768 && C::LDS_OUT <= 5 * 32768, "pipe8 LDS");
@@ -1028,12 +1136,12 @@ __global__ __launch_bounds__(C::NT, 2) void gemm_pipe8_kernel(GemmArgs p) {
         if (split_coords(tile, nbm, p.N / C::BN, m0, n0))
             pipe6_tile<Pipe512x128, ACT, 1, DIAG>(p, lds, m0, n0);
         else
-            pipe8_tile<C, ACT, DIAG>(p, lds, m0, n0);
+            pipe8_tile<C, ACT, DIAG, WEPI>(p, lds, m0, n0);
     } else {
         const int nbn = (p.N + C::BN - 1) / C::BN;
         int bm, bn;
         tile_coords<GROUP_M>(tile, nbm, nbn, bm, bn);
-        pipe8_tile<C, ACT, DIAG>(p, lds, bm * C::BM, bn * C::BN);
+        pipe8_tile<C, ACT, DIAG, WEPI>(p, lds, bm * C::BM, bn * C::BN);
     }
 }
 
@@ -1041,25 +1149,25 @@ __host__ inline bool pipe8_ok(const GemmArgs& a) {
     return a.K % 64 == 0 && a.K >= 192 && (size_t)a.M * a.lda * 2 < (1ull << 32) && (size_t)a.N * a.ldb * 2 < (1ull << 32);
 }
 
-template <class C, int GROUP_M, int DIAG = 0, bool SPLIT = false>
+template <class C, int GROUP_M, int DIAG = 0, bool SPLIT = false, bool WEPI = false>
 int launch_pipe8(const GemmArgs& a, hipStream_t s) {
     const int nbm = (a.M + C::BM - 1) / C::BM, nbn = (a.N + C::BN - 1) / C::BN;
     const dim3 grid(SPLIT ? split_tiles(nbm, a.N / C::BN) : nbm * nbn), block(C::NT);
     switch (a.act) {
         case MME_ACT_GELU_TANH:
-            hipLaunchKernelGGL((gemm_pipe8_kernel<C, GROUP_M, MME_ACT_GELU_TANH, DIAG, SPLIT>), grid, block, 0, s, a);
+            hipLaunchKernelGGL((gemm_pipe8_kernel<C, GROUP_M, MME_ACT_GELU_TANH, DIAG, SPLIT, WEPI>), grid, block, 0, s, a);
             break;
         case MME_ACT_QUICK_GELU:
-            hipLaunchKernelGGL((gemm_pipe8_kernel<C, GROUP_M, MME_ACT_QUICK_GELU, DIAG, SPLIT>), grid, block, 0, s, a);
+            hipLaunchKernelGGL((gemm_pipe8_kernel<C, GROUP_M, MME_ACT_QUICK_GELU, DIAG, SPLIT, WEPI>), grid, block, 0, s, a);
             break;
         case MME_ACT_GELU_ERF:
-            hipLaunchKernelGGL((gemm_pipe8_kernel<C, GROUP_M, MME_ACT_GELU_ERF, DIAG, SPLIT>), grid, block, 0, s, a);
+            hipLaunchKernelGGL((gemm_pipe8_kernel<C, GROUP_M, MME_ACT_GELU_ERF, DIAG, SPLIT, WEPI>), grid, block, 0, s, a);
             break;
         case MME_ACT_GEGLU_TANH:
-            hipLaunchKernelGGL((gemm_pipe8_kernel<C, GROUP_M, MME_ACT_GEGLU_TANH, DIAG, SPLIT>), grid, block, 0, s, a);
+            hipLaunchKernelGGL((gemm_pipe8_kernel<C, GROUP_M, MME_ACT_GEGLU_TANH, DIAG, SPLIT, WEPI>), grid, block, 0, s, a);
             break;
         default:
-            hipLaunchKernelGGL((gemm_pipe8_kernel<C, GROUP_M, MME_ACT_NONE, DIAG, SPLIT>), grid, block, 0, s, a);
+            hipLaunchKernelGGL((gemm_pipe8_kernel<C, GROUP_M, MME_ACT_NONE, DIAG, SPLIT, WEPI>), grid, block, 0, s, a);
             break;
     }
     return mme_check_launch("mme_gemm");
@@ -1675,7 +1783,7 @@ int gemm_dispatch(GemmArgs a, hipStream_t s) {
     if (glu) {  // gated epilogue: the pipelined kernel only (its LDS-staged 16-B tile rows pair gate/up)
         MME_REQUIRE(N % 8 == 0 && ldc % 4 == 0 && !out_f32 && !residual && ((uintptr_t)Cp & 7) == 0,
                     "mme_gemm: GeGLU needs N %% 8 == 0, ldc %% 4 == 0, 8-B aligned bf16 C, no residual");
-        if (pipe8_ok(a) && g_variant != 47) return launch_pipe8<Pipe256, 4>(a, s);
+        if (pipe8_ok(a) && g_variant != 47) return launch_pipe8<Pipe256, 4, 0, false, true>(a, s);
         return launch_pipe6<Pipe256, 4, 1>(a, s);
     }
     switch (g_variant) {
@@ -1732,6 +1840,10 @@ int gemm_dispatch(GemmArgs a, hipStream_t s) {
         case 65:  // diagnostic: pipe8 without an epilogue
             if (!pipe8_ok(a)) break;
             return launch_pipe8<Pipe256, 4, 7>(a, s);
+        case 71:  // dev: pipe8 with the per-wave epilogue (split grid where N = 256 k + 128; no row statistics)
+            if (!pipe8_ok(a)) break;
+            if (N % 256 == 128) return launch_pipe8<Pipe256, 4, 0, true, true>(a, s);
+            return launch_pipe8<Pipe256, 4, 0, false, true>(a, s);
         case 68:  // dev: pipe8, 2-row tile bands (no split grid)
             if (!pipe8_ok(a)) break;
             return launch_pipe8<Pipe256, 2>(a, s);
@@ -1764,9 +1876,11 @@ int gemm_dispatch(GemmArgs a, hipStream_t s) {
         // fc1 1130 -> 1183, QKV 1112 -> 1155, o_proj 1028 -> 1082-1109, fc2 1192 -> 1291 TF/s
         // (bias epilogue, M = 186 624; profiles/r02_pipe8_ab.log)
         // N = 256 k + 128: split grid (fc2 1144 -> 1200 TF/s, o_proj +5 %, QKV +1.6 %)
+        // with the per-wave epilogue (no workgroup barrier; +1-2 %, bit-identical,
+        // profiles/r02_pipe8_wave_epilogue_ab.log); mme_gemm_res_stats keeps the block-wide one
         if (pipe8_ok(a)) {
-            if (N % 256 == 128) return launch_pipe8<Pipe256, 4, 0, true>(a, s);
-            return launch_pipe8<Pipe256, 4>(a, s);
+            if (N % 256 == 128) return launch_pipe8<Pipe256, 4, 0, true, true>(a, s);
+            return launch_pipe8<Pipe256, 4, 0, false, true>(a, s);
         }
         if (N % 256 == 128) return launch_pipe6<Pipe256, 4, 1, 0, true>(a, s);
         return launch_pipe6<Pipe256, 4, 1>(a, s);
