@@ -107,8 +107,8 @@ int mme_gemm_lnfold(const void* A, int lda, const void* B, int ldb, void* C, int
 /* Residual GEMM that also leaves the next LayerNorm's statistics: C = A . B^T + bias +
  * residual (bf16, as mme_gemm with res_period 0, act NONE) and row_stats = [M][2]
  * (mean, rsqrt(var + eps)) of the bf16 rows of C, i.e. what mme_rowstats(C) returns
- * up to fp32 summation order. The pipelined kernel's epilogue reduces each 128-column
- * slice of every output row two-pass into row_part = [M][N / 128][2] (mean, M2;
+ * up to fp32 summation order. The pipelined kernel's epilogue reduces each 64-column
+ * slice of every output row two-pass into row_part = [M][N / 64][2] (mean, M2;
  * caller-provided scratch) and a per-row pass combines the slices (Chan), so the
  * residual stream is not re-read. Replaces the o_proj / fc2 residual adds followed by
  * layer_norm2 / the next layer's layer_norm1 (TF:models/siglip/modeling_siglip.py:341-357)

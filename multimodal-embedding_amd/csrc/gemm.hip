@@ -40,8 +40,8 @@ struct GemmArgs {
     const float* ln_stats;  // [M][2] (mean, rstd) of the A rows, or null
     const float* ln_cs;     // [N] column sums of the folded weight
     const float* ln_b;      // [N] folded bias (fp32)
-    // mme_gemm_res_stats: per 128-column slice of every output row, (mean, M2) of the
-    // bf16 outputs -> row_part[M][N / 128][2] (pipelined kernel, residual epilogue only)
+    // mme_gemm_res_stats: per 64-column slice of every output row, (mean, M2) of the
+    // bf16 outputs -> row_part[M][N / 64][2] (pipelined kernels, residual epilogue only)
     float* row_part;
 };
 
@@ -146,6 +146,15 @@ __device__ __forceinline__ float row16_sum(float v) {
     v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x4E, 0xF, 0xF, false));
     v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x141, 0xF, 0xF, false));
     v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x140, 0xF, 0xF, false));
+    return v;
+}
+
+// Sum over the 8 lanes of a DPP half-row (every lane gets the total): quad_perm [1,0,3,2],
+// [2,3,0,1], row_half_mirror.
+__device__ __forceinline__ float row8_sum(float v) {
+    v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0xB1, 0xF, 0xF, false));
+    v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x4E, 0xF, 0xF, false));
+    v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x141, 0xF, 0xF, false));
     return v;
 }
 
@@ -263,19 +272,19 @@ __device__ __forceinline__ void gemm_epilogue_lds(const GemmArgs& p, char* lds, 
             for (int e = 0; e < 8; ++e) o[e] = __builtin_bit_cast(unsigned short, f2bf(bits2f(v[e]) + bits2f(rv[q][e])));
             __builtin_nontemporal_store(o, reinterpret_cast<u16x8*>(Cout + (size_t)gr * p.ldc + gc));
             if (p.row_part) {
-                // LayerNorm statistics of the next layer, two-pass per 128-column slice: the 16
-                // lanes of a DPP row hold one slice of one output row (16 B each; slices align
-                // with lane groups because CPR and NT are multiples of 16, and N % 128 == 0)
+                // LayerNorm statistics of the next layer, two-pass per 64-column slice: the 8
+                // lanes of a DPP half-row hold one slice of one output row (16 B each; slices
+                // align with lane groups because CPR and NT are multiples of 8, and N % 64 == 0)
                 float xf[8], sum = 0.f;
 #pragma unroll
                 for (int e = 0; e < 8; ++e) sum += (xf[e] = bits2f(o[e]));
-                const float mean = row16_sum(sum) * (1.f / 128.f);
+                const float mean = row8_sum(sum) * (1.f / 64.f);
                 float m2 = 0.f;
 #pragma unroll
                 for (int e = 0; e < 8; ++e) m2 += (xf[e] - mean) * (xf[e] - mean);
-                m2 = row16_sum(m2);
-                if ((cc & 15) == 0)
-                    *reinterpret_cast<float2*>(p.row_part + 2 * ((size_t)gr * (p.N >> 7) + (gc >> 7))) =
+                m2 = row8_sum(m2);
+                if ((cc & 7) == 0)
+                    *reinterpret_cast<float2*>(p.row_part + 2 * ((size_t)gr * (p.N >> 6) + (gc >> 6))) =
                         make_float2(mean, m2);
             }
         } else if (EDIAG == 1) {
@@ -896,8 +905,8 @@ int launch_pipe6(const GemmArgs& a, hipStream_t s) {
 // own 18 KiB LDS region (row pitch 144 B), reads it back as 16-B row chunks (8 rows x 128 B
 // per store instruction) and stores it -- no workgroup barrier, so the early wave row's
 // epilogue runs beside the late row's last MFMAs and each wave leaves as soon as it is done.
-// Same arithmetic as gemm_epilogue_lds step for step (bit-identical outputs); no row
-// statistics (mme_gemm_res_stats keeps the block-wide epilogue).
+// Same arithmetic as gemm_epilogue_lds step for step (bit-identical outputs and row
+// statistics: a wave's 64 columns of a row are one 64-column slice).
 template <class C, int ACT>
 __device__ __forceinline__ void gemm_epilogue_wave(const GemmArgs& p, char* lds, f32x4 (&acc)[C::FM][C::FN], int m0,
                                                    int n0, int wave, int wm, int wn, int g, int li, int lane) {
@@ -986,6 +995,19 @@ __device__ __forceinline__ void gemm_epilogue_wave(const GemmArgs& p, char* lds,
 #pragma unroll
             for (int e = 0; e < 8; ++e) o[e] = __builtin_bit_cast(unsigned short, f2bf(bits2f(v[e]) + bits2f(rv[q][e])));
             __builtin_nontemporal_store(o, reinterpret_cast<u16x8*>(Cout + (size_t)gr * p.ldc + gc));
+            if (p.row_part) {  // the wave's 64 columns of this row = one statistics slice (gemm_epilogue_lds)
+                float xf[8], sum = 0.f;
+#pragma unroll
+                for (int e = 0; e < 8; ++e) sum += (xf[e] = bits2f(o[e]));
+                const float mean = row8_sum(sum) * (1.f / 64.f);
+                float m2 = 0.f;
+#pragma unroll
+                for (int e = 0; e < 8; ++e) m2 += (xf[e] - mean) * (xf[e] - mean);
+                m2 = row8_sum(m2);
+                if (cc == 0)
+                    *reinterpret_cast<float2*>(p.row_part + 2 * ((size_t)gr * (p.N >> 6) + (gc >> 6))) =
+                        make_float2(mean, m2);
+            }
         } else {
             __builtin_nontemporal_store(v, reinterpret_cast<u16x8*>(Cout + (size_t)gr * p.ldc + gc));
         }
@@ -1698,8 +1720,8 @@ extern "C" int mme_gemm(const void* A, int lda, const void* B, int ldb, void* Cp
 }
 
 namespace {
-// (mean_i, M2_i) of the N / 128 slices of a row -> (mean, rstd), Chan's pairwise combination
-// for equal slice counts: mean = avg(mean_i), M2 = sum M2_i + 128 * sum (mean_i - mean)^2.
+// (mean_i, M2_i) of the N / 64 slices of a row -> (mean, rstd), Chan's pairwise combination
+// for equal slice counts: mean = avg(mean_i), M2 = sum M2_i + 64 * sum (mean_i - mean)^2.
 __global__ __launch_bounds__(256) void row_part_combine_kernel(const float* __restrict__ part, float* __restrict__ st,
                                                                int rows, int nparts, float eps) {
     const int r = blockIdx.x * 256 + threadIdx.x;
@@ -1714,7 +1736,7 @@ __global__ __launch_bounds__(256) void row_part_combine_kernel(const float* __re
         m2 += v.y;
         dev += (v.x - mean) * (v.x - mean);
     }
-    const float var = (m2 + 128.f * dev) / (128.f * nparts);
+    const float var = (m2 + 64.f * dev) / (64.f * nparts);  // nparts slices of 64 columns
     *reinterpret_cast<float2*>(st + 2 * (size_t)r) = make_float2(mean, rsqrtf(var + eps));
 }
 }  // namespace
@@ -1743,12 +1765,12 @@ extern "C" int mme_gemm_res_stats(const void* A, int lda, const void* B, int ldb
         return mme_rowstats(Cp, ldc, M, N, eps, row_stats, stream);
     }
     if (pipe8_ok(a) && g_variant != 47)  // variant 47: pipe6 (tests: pipe8 is bit-identical to it)
-        N % 256 == 128 ? launch_pipe8<Pipe256, 4, 0, true>(a, s) : launch_pipe8<Pipe256, 4>(a, s);
+        N % 256 == 128 ? launch_pipe8<Pipe256, 4, 0, true, true>(a, s) : launch_pipe8<Pipe256, 4, 0, false, true>(a, s);
     else
         N % 256 == 128 ? launch_pipe6<Pipe256, 4, 1, 0, true>(a, s) : launch_pipe6<Pipe256, 4, 1>(a, s);
     const int rc = mme_check_launch("mme_gemm_res_stats");
     if (rc != MME_OK) return rc;
-    hipLaunchKernelGGL(row_part_combine_kernel, dim3(cdiv(M, 256)), dim3(256), 0, s, row_part, row_stats, M, N / 128,
+    hipLaunchKernelGGL(row_part_combine_kernel, dim3(cdiv(M, 256)), dim3(256), 0, s, row_part, row_stats, M, N / 64,
                        eps);
     return mme_check_launch("mme_gemm_res_stats");
 }
@@ -1877,7 +1899,7 @@ int gemm_dispatch(GemmArgs a, hipStream_t s) {
         // (bias epilogue, M = 186 624; profiles/r02_pipe8_ab.log)
         // N = 256 k + 128: split grid (fc2 1144 -> 1200 TF/s, o_proj +5 %, QKV +1.6 %)
         // with the per-wave epilogue (no workgroup barrier; +1-2 %, bit-identical,
-        // profiles/r02_pipe8_wave_epilogue_ab.log); mme_gemm_res_stats keeps the block-wide one
+        // profiles/r02_pipe8_wave_epilogue_ab.log); mme_gemm_res_stats uses it too
         if (pipe8_ok(a)) {
             if (N % 256 == 128) return launch_pipe8<Pipe256, 4, 0, true, true>(a, s);
             return launch_pipe8<Pipe256, 4, 0, false, true>(a, s);

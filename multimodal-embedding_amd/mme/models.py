@@ -45,8 +45,8 @@ class _Bufs:
         self.hq = mx.MXTensor.empty(rows, d, device) if fp8 else None
         self.midq = mx.MXTensor.empty(rows, cfg.inter_pad, device) if fp8 else None
         self.stats = torch.empty(rows, 2, dtype=torch.float32, device=device)
-        # per-128-column (mean, M2) slices of the residual GEMMs' output rows (mme_gemm_res_stats)
-        self.part = torch.empty(rows, max(1, d // 128), 2, dtype=torch.float32, device=device) \
+        # per-64-column (mean, M2) slices of the residual GEMMs' output rows (mme_gemm_res_stats)
+        self.part = torch.empty(rows, max(1, d // 64), 2, dtype=torch.float32, device=device) \
             if FUSED_STATS and d % 128 == 0 else None
 
 

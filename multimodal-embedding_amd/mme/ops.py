@@ -142,14 +142,14 @@ def gemm_res_stats(a: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor
                    eps: float, stats: torch.Tensor, part: torch.Tensor, *, out: Optional[torch.Tensor] = None,
                    algo_flops: Optional[float] = None) -> torch.Tensor:
     """out = a @ w.T + bias + residual (bf16) and stats = rowstats(out, eps), the statistics
-    reduced in the GEMM epilogue (mme_gemm_res_stats). part: fp32 scratch >= [M, N / 128, 2]."""
+    reduced in the GEMM epilogue (mme_gemm_res_stats). part: fp32 scratch >= [M, N / 64, 2]."""
     _dev(a, w, bias, residual, stats, part, out)
     M, K = a.shape
     N = w.shape[0]
     if w.shape[1] != K or residual.shape[0] < M or stats.shape[0] < M:
         raise ValueError(f"gemm_res_stats: a {tuple(a.shape)} vs w {tuple(w.shape)} / residual / stats")
-    if N % 128 or part.dtype != torch.float32 or not part.is_contiguous() or part.numel() < M * (N // 128) * 2:
-        raise ValueError("gemm_res_stats: N % 128 != 0 or part is not contiguous fp32 >= [M, N / 128, 2]")
+    if N % 128 or part.dtype != torch.float32 or not part.is_contiguous() or part.numel() < M * (N // 64) * 2:
+        raise ValueError("gemm_res_stats: N % 128 != 0 or part is not contiguous fp32 >= [M, N / 64, 2]")
     if stats.dtype != torch.float32 or not stats.is_contiguous():
         raise ValueError("gemm_res_stats: stats must be contiguous fp32 [M, 2]")
     if bias is not None and bias.numel() < N:
@@ -164,7 +164,7 @@ def gemm_res_stats(a: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor
     # launch inside this C-ABI call); its bytes: residual read, the per-slice (mean, M2) pairs
     # written by the GEMM epilogue and read back by the combine, and the [M, 2] statistics
     KernelTimer.end(ev, "gemm", algo_flops if algo_flops is not None else 2.0 * M * N * K,
-                    2.0 * (M * K + N * K + M * N) + 2.0 * M * N + 2 * 8.0 * M * (N // 128) + 8.0 * M)
+                    2.0 * (M * K + N * K + M * N) + 2.0 * M * N + 2 * 8.0 * M * (N // 64) + 8.0 * M)
     return out
 
 

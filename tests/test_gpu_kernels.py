@@ -206,7 +206,7 @@ def test_gemm_lnfold(cuda, M, N, K, act):
 
 
 # mme_gemm_res_stats: the residual GEMM's output is bit-identical to mme_gemm's, and the
-# row statistics reduced in its epilogue (128-column slices, Chan-combined) match a separate
+# row statistics reduced in its epilogue (64-column slices, Chan-combined) match a separate
 # mme_rowstats pass over that output up to fp32 summation order. Shapes: split grid
 # (N = 1152), whole 256-column tiles (N = 1280), the non-pipelined fallback (M * N < 1M),
 # and a shifted residual stream (mean >> std: the two-pass slices keep the variance exact).
@@ -220,7 +220,7 @@ def test_gemm_res_stats(cuda, M, N, K, shift):
     x = (rnd(M, N, scale=2.0, gen=g).float() + shift).to(torch.bfloat16)
     ref_out = ops.gemm(a, w, b, residual=x)
     st = torch.empty(M, 2, dtype=torch.float32, device="cuda")
-    part = torch.full((M, N // 128, 2), float("nan"), dtype=torch.float32, device="cuda")
+    part = torch.full((M, N // 64, 2), float("nan"), dtype=torch.float32, device="cuda")
     out = ops.gemm_res_stats(a, w, b, x.clone(), 1e-6, st, part)
     assert torch.equal(out, ref_out), "mme_gemm_res_stats output differs from mme_gemm"
     if M * N >= 1 << 20:  # the pipelined kernel's epilogue wrote every slice (not the fallback pass)
@@ -269,7 +269,7 @@ def test_gemm_pipe8_bit_identical_to_pipe6(cuda, M, N, K, epi):
         if epi == "geglu":
             return (ops.gemm(a, w, b, act=_lib.ACT_GEGLU_TANH),)
         st = torch.empty(M, 2, dtype=torch.float32, device="cuda")
-        part = torch.empty(M, N // 128, 2, dtype=torch.float32, device="cuda")
+        part = torch.empty(M, N // 64, 2, dtype=torch.float32, device="cuda")
         out = ops.gemm_res_stats(a, w, b, x.clone(), 1e-6, st, part)
         return out, st
 

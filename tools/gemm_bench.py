@@ -55,7 +55,7 @@ def main():
               "resper": {"bias": bias, "residual": R256, "res_period": 256},
               "gelu": {"bias": bias, "act": _lib.ACT_GELU_TANH}}[a.epi]
         st = torch.empty(M, 2, device="cuda")
-        part = torch.empty(M, max(1, N // 128), 2, device="cuda")
+        part = torch.empty(M, max(1, N // 64), 2, device="cuda")
 
         def run():
             if a.epi == "resstats":
