@@ -1038,6 +1038,9 @@ template <class C, int ACT, int DIAG, bool WEPI = false>
 __device__ __forceinline__ void pipe8_tile(const GemmArgs& p, char* lds, const int m0, const int n0) {
     static_assert(C::BM == 256 && C::BN == 256 && C::FN == 4 && C::FM == 8 && C::NW == 8, "pipe8: 256 x 256, 8 waves");
     constexpr int UNIT = 32768, NSLOT = 5;
+    // dev (DIAG 20 / 21): the last 2 / all 4 of a step's DMA pieces issued inside its compute
+    // phase (between MFMA groups) instead of its memory phase
+    constexpr int DMAQ = DIAG == 20 ? 2 : DIAG == 21 ? 4 : 0;
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int wm = wave / C::WN, wn = wave % C::WN;
@@ -1056,16 +1059,17 @@ __device__ __forceinline__ void pipe8_tile(const GemmArgs& p, char* lds, const i
     }
     const char* gA = reinterpret_cast<const char*>(p.A);
     const char* gB = reinterpret_cast<const char*>(p.B);
-    auto issue_unit = [&](int h) {
+    auto issue_piece = [&](int h, int q) {
         char* base = lds + (h % NSLOT) * UNIT + wave * 4096;
         const unsigned k0 = (unsigned)(h >> 1) * 128u;
-        if (h & 1) {
+        if (h & 1)
+            glds16(gB + (offB[q] + k0), base + q * 1024);
+        else
+            glds16(gA + (offA[q] + k0), base + q * 1024);
+    };
+    auto issue_unit = [&](int h) {
 #pragma unroll
-            for (int q = 0; q < 4; ++q) glds16(gB + (offB[q] + k0), base + q * 1024);
-        } else {
-#pragma unroll
-            for (int q = 0; q < 4; ++q) glds16(gA + (offA[q] + k0), base + q * 1024);
-        }
+        for (int q = 0; q < 4; ++q) issue_piece(h, q);
     };
     const unsigned lds0 = (unsigned)(uintptr_t)(LDS_AS char*)lds;
     const int sw = (li >> 1) & 7;  // fragment rows differ by multiples of 16: the swizzle depends on li only
@@ -1094,21 +1098,31 @@ __device__ __forceinline__ void pipe8_tile(const GemmArgs& p, char* lds, const i
         ds_read16<10240>(a[5], aa);
         ds_read16<12288>(a[6], aa);
         ds_read16<14336>(a[7], aa);
-        if (DIAG != 1 && issue_h >= 0) issue_unit(issue_h);
+        if (DIAG != 1 && issue_h >= 0) {
+#pragma unroll
+            for (int q = 0; q < 4 - DMAQ; ++q) issue_piece(issue_h, q);
+        }
+        // wait_mem == 4: the pieces of this step's unit issued so far may stay in flight
         if (wait_mem == 0) vm_wait<0>();
-        else if (wait_mem == 4) vm_wait<4>();
+        else if (wait_mem == 4) vm_wait<4 - DMAQ>();
         lgkm_wait<0>();
         __builtin_amdgcn_s_barrier();
         // ---- compute phase
         __builtin_amdgcn_s_setprio(1);
 #pragma unroll
-        for (int i = 0; i < 8; ++i)
+        for (int i = 0; i < 8; ++i) {
 #pragma unroll
             for (int j = 0; j < C::FN; ++j)
                 if (DIAG == 2)
                     asm volatile("" ::"v"(b[j]), "v"(a[i]));
                 else
                     acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b[j], a[i], acc[i][j], 0, 0, 0);
+            if (DMAQ > 0 && i < DMAQ && issue_h >= 0) {
+                __builtin_amdgcn_sched_barrier(0);
+                issue_piece(issue_h, 4 - DMAQ + i);
+                __builtin_amdgcn_sched_barrier(0);
+            }
+        }
         __builtin_amdgcn_s_setprio(0);
         __builtin_amdgcn_sched_barrier(0);
         if (wait_comp == 0) vm_wait<0>();
@@ -1866,6 +1880,14 @@ int gemm_dispatch(GemmArgs a, hipStream_t s) {
             if (!pipe8_ok(a)) break;
             if (N % 256 == 128) return launch_pipe8<Pipe256, 4, 0, true, true>(a, s);
             return launch_pipe8<Pipe256, 4, 0, false, true>(a, s);
+        case 72:  // dev: production pipe8 (per-wave epilogue) with 2 of 4 DMA pieces per step in the compute phase
+            if (!pipe8_ok(a)) break;
+            if (N % 256 == 128) return launch_pipe8<Pipe256, 4, 20, true, true>(a, s);
+            return launch_pipe8<Pipe256, 4, 20, false, true>(a, s);
+        case 73:  // dev: ... all 4 DMA pieces per step in the compute phase
+            if (!pipe8_ok(a)) break;
+            if (N % 256 == 128) return launch_pipe8<Pipe256, 4, 21, true, true>(a, s);
+            return launch_pipe8<Pipe256, 4, 21, false, true>(a, s);
         case 68:  // dev: pipe8, 2-row tile bands (no split grid)
             if (!pipe8_ok(a)) break;
             return launch_pipe8<Pipe256, 2>(a, s);
