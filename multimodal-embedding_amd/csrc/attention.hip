@@ -1238,6 +1238,13 @@ void launch_attn(int kind, const AttnArgs& a, int B, int T, int H, hipStream_t s
     else if (kind == 34)  // dev: kind 27 with 16-B O stores + static priority
         hipLaunchKernelGGL((attn_pipe_kernel<HD, 8, 2, false, HD == 72, true, false, 4, true, 20>),
                            dim3(cdiv(T, 256) * H * B), dim3(512), 0, st, a);
+    else if (kind == 35)  // kind 21 (9 waves) with static priority for waves 4..8: production (ViT-H T 257,
+                          // +1-4 %, bit-identical; profiles/r02_attn_prio_hd80_ab.log)
+        hipLaunchKernelGGL((attn_pipe_kernel<HD, 9, 2, false, HD == 72, true, false, 1, false, 4>),
+                           dim3(cdiv(T, 288) * H * B), dim3(576), 0, st, a);
+    else if (kind == 36)  // dev: kind 23 (12 waves) with static priority (DFN5B T 730: within noise)
+        hipLaunchKernelGGL((attn_pipe_kernel<HD, 12, 2, false, HD == 72, true, false, 1, false, 4>),
+                           dim3(cdiv(T, 384) * H * B), dim3(768), 0, st, a);
     else if (kind == 31)  // dev: both
         hipLaunchKernelGGL((attn_pipe_kernel<HD, 8, 2, false, HD == 72, true, false, 4, true, 6>),
                            dim3(cdiv(T, 256) * H * B), dim3(512), 0, st, a);
@@ -1292,7 +1299,7 @@ extern "C" int mme_attention(const void* qkv, int ld_qkv, void* out, int ld_out,
     const long pad12 = (long)cdiv(T, 384) * 384;
     int kind = T <= 64 ? 16
                : (T <= 128 || hd == 64) ? 0
-               : pad9 * 10 < min(pad8, pad4) * 9 ? 21
+               : pad9 * 10 < min(pad8, pad4) * 9 ? 35
                : (hd == 80 && pad12 <= pad8 && pad12 * 10 <= pad4 * 11) ? 23
                : (pad8 * 10 <= pad4 * 11 ? (hd == 72 ? 30 : 11) : 14);
     if (g_attn_variant >= 1 && g_attn_variant <= 4 && hd == 72) {  // dev-only diagnostic builds
