@@ -557,6 +557,8 @@ template <int HD, int NW, int NSTG, bool PIPE, bool ONES, bool LAZY, bool PING =
 __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(MINW))) void attn_pipe_kernel(AttnArgs a) {
     constexpr bool ADMA = XF & 1, PKX = XF & 2, PRIO = XF & 4, NODMA = XF & 8;  // 8: diagnostic, no K/V DMA (wrong results)
     constexpr bool WIDE = XF & 16;  // 16: O stored as 16-B rows (v_permlane16_swap pairs of d-tiles)
+    constexpr bool PAIR = XF & 32;  // 32: 4-tile ring, one barrier per PAIR of key tiles (UNR, NSTG 4)
+    static_assert(!PAIR || (UNR && NSTG == 4 && !PIPE && !PING), "paired tiles: unrolled 4-slot ring");
     static_assert(!PIPE || NSTG == 3, "the pipelined loop keeps tile t+1 resident while t+2 lands");
     static_assert(!PING || (!PIPE && NSTG == 4), "ping-pong: two tiles resident beside the one landing");
     static_assert(!ONES || HD == 72, "the ones column lives in the padding of the 80-wide V^T tiles");
@@ -778,7 +780,38 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(MINW)))
 
     f32x4 sA[2][4], sB[2][4];
     if (PRIO && wave >= NW / 2) __builtin_amdgcn_s_setprio(1);
-    if (UNR && !PIPE && !PING && NSTG == 2) {
+    if (PAIR) {
+        // two key tiles per barrier: tiles t, t+1 landed -> barrier -> issue t+2, t+3 into the
+        // slots of t-2, t-1 (read before this barrier) -> QK / softmax / PV of t, then t+1;
+        // waves drift within a pair instead of meeting at every tile, and each tile has two
+        // tiles of compute to land. Unrolled by the ring (slot offsets are immediates).
+        if (nkt > 0) issue(0);
+        if (nkt > 1) issue(1);
+        for (int t = 0; t < nkt; t += 4) {
+            vm_wait<0>();
+            __builtin_amdgcn_s_barrier();
+            if (t + 2 < nkt) issue(t + 2);
+            if (t + 3 < nkt) issue(t + 3);
+            qk_at(t, 0, sA);
+            softmax_pv_at(t, 0, sA, [] {});
+            if (t + 1 < nkt) {
+                qk_at(t + 1, TILE, sA);
+                softmax_pv_at(t + 1, TILE, sA, [] {});
+            }
+            if (t + 2 < nkt) {
+                vm_wait<0>();
+                __builtin_amdgcn_s_barrier();
+                if (t + 4 < nkt) issue(t + 4);
+                if (t + 5 < nkt) issue(t + 5);
+                qk_at(t + 2, 2 * TILE, sA);
+                softmax_pv_at(t + 2, 2 * TILE, sA, [] {});
+                if (t + 3 < nkt) {
+                    qk_at(t + 3, 3 * TILE, sA);
+                    softmax_pv_at(t + 3, 3 * TILE, sA, [] {});
+                }
+            }
+        }
+    } else if (UNR && !PIPE && !PING && NSTG == 2) {
         // unrolled by the ring depth: the ring slot of every LDS access is a compile-time
         // constant (immediate ds_read offsets, no per-tile address VALU)
         if (nkt > 0) issue(0);
@@ -1245,6 +1278,9 @@ void launch_attn(int kind, const AttnArgs& a, int B, int T, int H, hipStream_t s
     else if (kind == 36)  // dev: kind 23 (12 waves) with static priority (DFN5B T 730: within noise)
         hipLaunchKernelGGL((attn_pipe_kernel<HD, 12, 2, false, HD == 72, true, false, 1, false, 4>),
                            dim3(cdiv(T, 384) * H * B), dim3(768), 0, st, a);
+    else if (kind == 37)  // dev: kind 30 with a 4-tile ring and one barrier per pair of key tiles
+        hipLaunchKernelGGL((attn_pipe_kernel<HD, 8, 4, false, HD == 72, true, false, 4, true, 36>),
+                           dim3(cdiv(T, 256) * H * B), dim3(512), 0, st, a);
     else if (kind == 31)  // dev: both
         hipLaunchKernelGGL((attn_pipe_kernel<HD, 8, 2, false, HD == 72, true, false, 4, true, 6>),
                            dim3(cdiv(T, 256) * H * B), dim3(512), 0, st, a);
