@@ -1181,6 +1181,43 @@ __global__ __launch_bounds__(C::NT, 2) void gemm_pipe8_kernel(GemmArgs p) {
     }
 }
 
+// pers8: persistent pipe8. One 8-wave workgroup per CU walks its XCD's contiguous range
+// of the tile order (pers' schedule); each tile is pipe8_tile with the per-wave epilogue
+// (or pipe6's 512 x 128 tile for the split grid's last column), then one barrier: every
+// wave's epilogue LDS reads are done (their results feed its stores), so the next tile's
+// prologue DMA may overwrite the staging regions while the stores are still in flight.
+// vmcnt stays correct across tiles: LDS-DMA loads retire in order, and outstanding stores
+// only make every counted wait stricter.
+template <class C, int GROUP_M, int ACT, bool SPLIT>
+__global__ __launch_bounds__(C::NT, 2) void gemm_pers8_kernel(GemmArgs p) {
+    __shared__ __attribute__((aligned(16))) char lds[5 * 32768];
+    const int nbm = (p.M + C::BM - 1) / C::BM, nfn = p.N / C::BN;
+    const int nbn = (p.N + C::BN - 1) / C::BN;
+    const int ntiles = SPLIT ? split_tiles(nbm, nfn) : nbm * nbn;
+    const int xcd = blockIdx.x & 7, loc = blockIdx.x >> 3;
+    const int q = ntiles >> 3, r8 = ntiles & 7;
+    const int t_begin = xcd < r8 ? xcd * (q + 1) : r8 * (q + 1) + (xcd - r8) * q;
+    const int t_end = t_begin + q + (xcd < r8 ? 1 : 0);
+    const int nb = gridDim.x, bstride = (nb >> 3) + ((nb & 7) > xcd ? 1 : 0);
+    for (int tile = t_begin + loc; tile < t_end; tile += bstride) {  // uniform over the block
+        int m0, n0;
+        if constexpr (SPLIT) {
+            if (split_coords(tile, nbm, nfn, m0, n0)) {
+                pipe6_tile<Pipe512x128, ACT, 1, 0>(p, lds, m0, n0);
+                __builtin_amdgcn_s_barrier();
+                continue;
+            }
+        } else {
+            int bm, bn;
+            tile_coords<GROUP_M>(tile, nbm, nbn, bm, bn);
+            m0 = bm * C::BM;
+            n0 = bn * C::BN;
+        }
+        pipe8_tile<C, ACT, 0, true>(p, lds, m0, n0);
+        __builtin_amdgcn_s_barrier();
+    }
+}
+
 __host__ inline bool pipe8_ok(const GemmArgs& a) {
     return a.K % 64 == 0 && a.K >= 192 && (size_t)a.M * a.lda * 2 < (1ull << 32) && (size_t)a.N * a.ldb * 2 < (1ull << 32);
 }
@@ -1204,6 +1241,41 @@ int launch_pipe8(const GemmArgs& a, hipStream_t s) {
             break;
         default:
             hipLaunchKernelGGL((gemm_pipe8_kernel<C, GROUP_M, MME_ACT_NONE, DIAG, SPLIT, WEPI>), grid, block, 0, s, a);
+            break;
+    }
+    return mme_check_launch("mme_gemm");
+}
+
+int g_num_cus = 0;  // CUs of the current device (persistent grids), queried once
+
+template <class C, int GROUP_M, bool SPLIT>
+int launch_pers8(const GemmArgs& a, hipStream_t s) {
+    if (g_num_cus == 0) {
+        int dev = 0, n = 0;
+        if (hipGetDevice(&dev) == hipSuccess && hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) ==
+                                                     hipSuccess && n > 0)
+            g_num_cus = n;
+        else
+            g_num_cus = 256;
+    }
+    const int nbm = (a.M + C::BM - 1) / C::BM, nbn = (a.N + C::BN - 1) / C::BN;
+    const int ntiles = SPLIT ? split_tiles(nbm, a.N / C::BN) : nbm * nbn;
+    const dim3 grid(min(ntiles, g_num_cus)), block(C::NT);
+    switch (a.act) {
+        case MME_ACT_GELU_TANH:
+            hipLaunchKernelGGL((gemm_pers8_kernel<C, GROUP_M, MME_ACT_GELU_TANH, SPLIT>), grid, block, 0, s, a);
+            break;
+        case MME_ACT_QUICK_GELU:
+            hipLaunchKernelGGL((gemm_pers8_kernel<C, GROUP_M, MME_ACT_QUICK_GELU, SPLIT>), grid, block, 0, s, a);
+            break;
+        case MME_ACT_GELU_ERF:
+            hipLaunchKernelGGL((gemm_pers8_kernel<C, GROUP_M, MME_ACT_GELU_ERF, SPLIT>), grid, block, 0, s, a);
+            break;
+        case MME_ACT_GEGLU_TANH:
+            hipLaunchKernelGGL((gemm_pers8_kernel<C, GROUP_M, MME_ACT_GEGLU_TANH, SPLIT>), grid, block, 0, s, a);
+            break;
+        default:
+            hipLaunchKernelGGL((gemm_pers8_kernel<C, GROUP_M, MME_ACT_NONE, SPLIT>), grid, block, 0, s, a);
             break;
     }
     return mme_check_launch("mme_gemm");
@@ -1462,7 +1534,6 @@ __global__ __launch_bounds__(C::NT, 2) void gemm_pers_kernel(GemmArgs p) {
     if (!late) __builtin_amdgcn_s_barrier();
 }
 
-int g_num_cus = 0;
 
 template <class C, int GROUP_M, int DIAG = 0>
 int launch_pers(const GemmArgs& a, hipStream_t s) {
@@ -1888,6 +1959,10 @@ int gemm_dispatch(GemmArgs a, hipStream_t s) {
             if (!pipe8_ok(a)) break;
             if (N % 256 == 128) return launch_pipe8<Pipe256, 4, 21, true, true>(a, s);
             return launch_pipe8<Pipe256, 4, 21, false, true>(a, s);
+        case 74:  // dev: persistent pipe8 (per-wave epilogue; split grid where N = 256 k + 128)
+            if (!pipe8_ok(a)) break;
+            if (N % 256 == 128) return launch_pers8<Pipe256, 4, true>(a, s);
+            return launch_pers8<Pipe256, 4, false>(a, s);
         case 68:  // dev: pipe8, 2-row tile bands (no split grid)
             if (!pipe8_ok(a)) break;
             return launch_pipe8<Pipe256, 2>(a, s);
