@@ -112,7 +112,7 @@ int mme_gemm_lnfold(const void* A, int lda, const void* B, int ldb, void* C, int
  * caller-provided scratch) and a per-row pass combines the slices (Chan), so the
  * residual stream is not re-read. Replaces the o_proj / fc2 residual adds followed by
  * layer_norm2 / the next layer's layer_norm1 (TF:models/siglip/modeling_siglip.py:341-357)
- * on the LayerNorm-folded path. N % 128 == 0. */
+ * on the LayerNorm-folded path. N % 64 == 0. */
 int mme_gemm_res_stats(const void* A, int lda, const void* B, int ldb, void* C, int ldc, int M, int N, int K,
                        const void* bias, const void* residual, int ldr, float eps, float* row_part,
                        float* row_stats, void* stream);

@@ -1832,7 +1832,7 @@ extern "C" int mme_gemm_res_stats(const void* A, int lda, const void* B, int ldb
     MME_REQUIRE(A && B && Cp && residual && row_part && row_stats, "mme_gemm_res_stats: null operand");
     MME_REQUIRE(M > 0 && N > 0 && K > 0, "mme_gemm_res_stats: empty shape M=%d N=%d K=%d", M, N, K);
     MME_REQUIRE(K % BK == 0, "mme_gemm_res_stats: K=%d must be a multiple of %d", K, BK);
-    MME_REQUIRE(N % 128 == 0, "mme_gemm_res_stats: N=%d must be a multiple of 128", N);
+    MME_REQUIRE(N % 64 == 0, "mme_gemm_res_stats: N=%d must be a multiple of 64", N);
     MME_REQUIRE(lda % 8 == 0 && ldb % 8 == 0 && lda >= K && ldb >= K && ldc >= N && ldr >= N,
                 "mme_gemm_res_stats: bad leading dims");
     MME_REQUIRE(((uintptr_t)A & 15) == 0 && ((uintptr_t)B & 15) == 0, "mme_gemm_res_stats: A/B must be 16-byte aligned");

@@ -47,7 +47,7 @@ class _Bufs:
         self.stats = torch.empty(rows, 2, dtype=torch.float32, device=device)
         # per-64-column (mean, M2) slices of the residual GEMMs' output rows (mme_gemm_res_stats)
         self.part = torch.empty(rows, max(1, d // 64), 2, dtype=torch.float32, device=device) \
-            if FUSED_STATS and d % 128 == 0 else None
+            if FUSED_STATS and d % 64 == 0 else None
 
 
 def encoder_layer(x: torch.Tensor, L: LayerW, cfg: TowerConfig, B: int, T: int, bufs: _Bufs, *,

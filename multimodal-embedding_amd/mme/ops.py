@@ -148,8 +148,8 @@ def gemm_res_stats(a: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor
     N = w.shape[0]
     if w.shape[1] != K or residual.shape[0] < M or stats.shape[0] < M:
         raise ValueError(f"gemm_res_stats: a {tuple(a.shape)} vs w {tuple(w.shape)} / residual / stats")
-    if N % 128 or part.dtype != torch.float32 or not part.is_contiguous() or part.numel() < M * (N // 64) * 2:
-        raise ValueError("gemm_res_stats: N % 128 != 0 or part is not contiguous fp32 >= [M, N / 64, 2]")
+    if N % 64 or part.dtype != torch.float32 or not part.is_contiguous() or part.numel() < M * (N // 64) * 2:
+        raise ValueError("gemm_res_stats: N % 64 != 0 or part is not contiguous fp32 >= [M, N / 64, 2]")
     if stats.dtype != torch.float32 or not stats.is_contiguous():
         raise ValueError("gemm_res_stats: stats must be contiguous fp32 [M, 2]")
     if bias is not None and bias.numel() < N:
