@@ -35,7 +35,7 @@ extern "C" {
 #define MME_ERR_HIP 2         /* HIP runtime error at launch               */
 #define MME_ERR_UNSUPPORTED 3 /* valid request this build does not handle  */
 
-#define MME_ABI_VERSION 5
+#define MME_ABI_VERSION 6  /* 6: mme_gemm_res_stats row_part is [M][N / 64][2] */
 
 /* activation codes for mme_gemm (HF config.hidden_act) */
 #define MME_ACT_NONE 0

@@ -16,7 +16,7 @@ LIB_PATH = os.environ.get("MME_LIB", os.path.join(_HERE, "libmme.so"))
 # MME_ACT_* / MME_PIX_* from include/mme.h
 ACT_NONE, ACT_GELU_TANH, ACT_QUICK_GELU, ACT_GELU_ERF, ACT_GEGLU_TANH = 0, 1, 2, 3, 4
 PIX_F32_NCHW, PIX_PATCHES = 0, 1
-ABI_VERSION = 5
+ABI_VERSION = 6
 
 # name -> (restype, argtypes)
 _P = c_void_p
