@@ -1126,6 +1126,280 @@ __global__ __launch_bounds__(256, 3) void attn_short_kernel(AttnArgs a, int unit
     }
 }
 
+// ---------------------------------------------------------------------------
+// attn_m32_kernel: the LDS-DMA flash loop on v_mfma_f32_32x32x16_bf16 (round 2).
+// attn_pipe_kernel's counters (profiles/r02_pmc_attn_siglip_vision.json) put the
+// hd-72 loop at the SIMD's vector-issue limit: per wave and 64-key tile 44
+// 16x16x32 MFMAs hold the issue port 8 cycles each (352) beside ~600 cycles of
+// softmax VALU, against 704 cycles of MFMA pipe work. A 32x32x16 MFMA does twice
+// the work per issue (8 of its 32 cycles), so the same tile takes 22 MFMAs and
+// 176 issue cycles, and the reduction depth is 16: head dim 72 / 80 runs the
+// QK^T product 80 deep (5 steps) instead of 96.
+//   * S^T = K . Q^T (A = K rows, B = Q^T): lane (r, h) = (lane & 31, lane >> 5)
+//     holds query r and keys (reg & 3) + 8 (reg >> 2) + 4 h of each 32-key block,
+//     so the row max is lane-local plus one v_permlane32_swap;
+//   * registers 8 s' .. 8 s' + 7 of a key block, packed to bf16, are directly the
+//     B operand (P^T) of O^T = V^T . P^T for the keys 16 s' .. 16 s' + 15 of that
+//     block (cdna_hip_programming.md §3 'accumulator tile as the next operand');
+//     the V^T operand takes the same permuted key order from two
+//     ds_read_b64_tr_b16 (keys +4h + 0..3 and +8 + 4h + 0..3);
+//   * K / V tiles of 64 keys land by LDS-DMA as "chunk planes" (plane c = 16-B
+//     column chunk c of all 64 keys, 1 KiB, lane = key). V plane c stores key k
+//     in slot k ^ (4 (c & 3)) (through the per-lane DMA source row), which makes
+//     the transposed reads of a 32-lane half (4 planes x 4 keys) hit 64
+//     distinct banks; the K reads (512 contiguous bytes per half) are
+//     conflict-free unswizzled;
+//   * O^T covers ceil((HD + 1) / 32) d-blocks of 32: at head dims 72 / 80 the
+//     V^T row HD (inside the padding) is a plane of ones, so O^T row HD is the
+//     softmax weight sum Σ bf16(p) and the per-tile sums disappear (HD 64: f32 adds);
+//   * lazy rescale (alpha == 1 exactly when no row max of the wave grew), static
+//     priority for the second half of the waves, tile loop unrolled by the 2-deep
+//     ring (every LDS address a lane base + immediate), 16-B O stores after a
+//     v_permlane32_swap of the two lane halves.
+// ---------------------------------------------------------------------------
+template <int HD, int NW, int MINW, bool PRIO, bool DPV = false>
+__global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(MINW))) void attn_m32_kernel(AttnArgs a) {
+    constexpr int NSTG = DPV ? 3 : 2;
+    constexpr bool ONES = HD % 32 != 0;
+    constexpr int NCHL = HD / 8;                    // K / V planes with data
+    constexpr int NKS = (HD + 15) / 16;             // QK^T k-steps of 16
+    constexpr int NDB = (HD + (ONES ? 1 : 0) + 31) / 32;  // O^T d-blocks of 32
+    constexpr int NVP = 4 * NDB;                    // V planes read (data, ones, zero padding)
+    constexpr int TILE = (NCHL + NVP) * 1024;
+    constexpr int NINS = 2 * NCHL;
+    constexpr int MAXI = (NINS + NW - 1) / NW;
+    constexpr int QB = NW * 32;
+    static_assert(2 * NKS <= NCHL + NVP, "K reads past the head dim stay inside the tile");
+    __shared__ __attribute__((aligned(16))) char lds[NSTG * TILE];
+
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int r = lane & 31, hh = lane >> 5;
+    const int nqb = (a.T + QB - 1) / QB;
+    int id;
+    {
+        const int bid = blockIdx.x, nwg = gridDim.x;
+        const int xcd = bid & 7, loc = bid >> 3, q8 = nwg >> 3, r8 = nwg & 7;
+        id = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + loc;
+    }
+    const int qb = id % nqb, h = (id / nqb) % a.H, b = id / (nqb * a.H);
+    const int T = a.T, D = a.H * HD;
+    const bf16* base = a.qkv + (long)b * T * a.ld;
+    const int qw0 = qb * QB + wave * 32;
+    const int Tk = a.seq_lens ? a.seq_lens[b] : T;
+    const float c = a.scale_log2;
+
+    // V planes past the data: the ones plane (ONES) and zero padding, in both ring slots
+    constexpr int NPAD = NVP > NCHL ? NVP - NCHL : 1;
+    for (int i = tid; i < NSTG * (NVP - NCHL) * 64; i += NW * 64) {
+        const int slot = i / (NPAD * 64), rem = i % (NPAD * 64);
+        const int pl = NCHL + rem / 64;
+        const unsigned short v = (ONES && pl == NCHL) ? 0x3F80 : 0;
+        *reinterpret_cast<u16x8*>(lds + slot * TILE + (NCHL + pl) * 1024 + (rem & 63) * 16) =
+            u16x8{v, v, v, v, v, v, v, v};
+    }
+
+    bf16x8 qf[NKS];  // B operand: Q^T[d = 16 ks + 8 hh + j][query r]
+    {
+        const bf16* qrow = base + (long)min(qw0 + r, T - 1) * a.ld + h * HD;
+#pragma unroll
+        for (int ks = 0; ks < NKS; ++ks) {
+            const int col = ks * 16 + 8 * hh;
+            if (col < HD)
+                qf[ks] = *reinterpret_cast<const bf16x8*>(qrow + col);
+            else
+                qf[ks] = bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
+        }
+    }
+
+    int nkt = (Tk + 63) / 64;
+    if (a.causal) nkt = min(nkt, (min(T, qb * QB + QB) + 63) / 64);
+
+    auto issue = [&](int t) {
+        char* tb = lds + (t % NSTG) * TILE;
+#pragma unroll
+        for (int i = 0; i < MAXI; ++i) {
+            const int idx = wave + NW * i;
+            if (i < MAXI - 1 || idx < NINS) {
+                const bool isV = idx >= NCHL;
+                const int plane = isV ? idx - NCHL : idx;
+                const int key = isV ? lane ^ (4 * (plane & 3)) : lane;
+                const bf16* src = base + (long)min(t * 64 + key, T - 1) * a.ld + (isV ? 2 : 1) * D + h * HD + plane * 8;
+                glds16(src, tb + idx * 1024);
+            }
+        }
+    };
+
+    const unsigned lds0 = (unsigned)(uintptr_t)(LDS_AS char*)lds;
+    // K fragment (A operand) of k-step ks, key block kb: plane 2 ks + hh, key 32 kb + r
+    const unsigned kb0 = lds0 + hh * 1024 + r * 16;
+    // V^T fragment (A operand) of d-block db, key step (kb, s'): two transposed reads,
+    // keys 32 kb + 16 s' + 8 j + 4 hh + q (j = 0, 1) at d = 32 db + 16 half + 4 p .. + 3
+    unsigned vbj[2];
+    {
+        const int i16 = lane & 15, q = i16 >> 2, p = i16 & 3, half = (lane >> 4) & 1;
+        const int cc = 2 * half + (p >> 1);
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+            vbj[j] = lds0 + (NCHL + cc) * 1024 + (((8 * j + 4 * hh + q) ^ (4 * cc)) * 16) + (p & 1) * 8;
+    }
+
+    f32x16 o[NDB];
+#pragma unroll
+    for (int i = 0; i < NDB; ++i)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) o[i][e] = 0.f;
+    float m = -1e30f, lsum = 0.f;
+
+    auto qk = [&](int t, const unsigned so, f32x16(&sc)[2]) {
+#pragma unroll
+        for (int kb = 0; kb < 2; ++kb) {
+            f32x16 z;
+#pragma unroll
+            for (int e = 0; e < 16; ++e) z[e] = 0.f;
+#pragma unroll
+            for (int ks = 0; ks < NKS; ++ks) {
+                const bf16x8 kf = *reinterpret_cast<const LDS_AS bf16x8*>((uintptr_t)(kb0 + so + kb * 512 + ks * 2048));
+                z = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[ks], z, 0, 0, 0);
+            }
+            sc[kb] = z;
+        }
+        if ((t * 64 + 64 > Tk) || (a.causal && t * 64 + 63 > qw0)) {
+            const int q = qw0 + r;
+            const int lim = a.causal ? min(Tk, q + 1) : Tk;
+#pragma unroll
+            for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+                for (int e = 0; e < 16; ++e)
+                    if (t * 64 + kb * 32 + (e & 3) + 8 * (e >> 2) + 4 * hh >= lim) sc[kb][e] = -INFINITY;
+        }
+    };
+    // online softmax of one tile's scores: running max, lazy O rescale, P packed to bf16
+    // (pk[2 kb + s'] = registers 8 s' .. 8 s' + 7 of key block kb)
+    auto softmax = [&](f32x16(&sc)[2], bf16x8(&pk)[4]) {
+        float mloc = fmaxf(sc[0][0], sc[0][1]);
+#pragma unroll
+        for (int e = 2; e < 16; ++e) mloc = fmaxf(mloc, sc[0][e]);
+#pragma unroll
+        for (int e = 0; e < 16; ++e) mloc = fmaxf(mloc, sc[1][e]);
+        mloc = xmax32(mloc);
+        const float mnew = fmaxf(m, mloc);
+        if (__builtin_amdgcn_ballot_w64(mnew != m)) {
+            const float alpha = __builtin_amdgcn_exp2f((m - mnew) * c);
+            if (!ONES) lsum *= alpha;
+#pragma unroll
+            for (int i = 0; i < NDB; ++i) o[i] *= alpha;
+        }
+        m = mnew;
+        const float mc = mnew * c;
+        float psum = 0.f;
+#pragma unroll
+        for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+            for (int e = 0; e < 16; ++e) {
+                const float pv = __builtin_amdgcn_exp2f(sc[kb][e] * c - mc);
+                sc[kb][e] = pv;
+                if (!ONES) psum += pv;
+            }
+        if (!ONES) lsum += psum;
+#pragma unroll
+        for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+            for (int sp = 0; sp < 2; ++sp)
+#pragma unroll
+                for (int j = 0; j < 8; ++j) pk[2 * kb + sp][j] = f2bf(sc[kb][8 * sp + j]);
+    };
+    auto pv = [&](const unsigned so, const bf16x8(&pk)[4]) {
+#pragma unroll
+        for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+            for (int sp = 0; sp < 2; ++sp)
+#pragma unroll
+                for (int db = 0; db < NDB; ++db) {
+                    const unsigned off = so + db * 4096 + kb * 512 + sp * 256;
+                    const s16x4 v0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS_AS s16x4*)(uintptr_t)(vbj[0] + off));
+                    const s16x4 v1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS_AS s16x4*)(uintptr_t)(vbj[1] + off));
+                    const bf16x8 vv = __builtin_bit_cast(bf16x8, __builtin_shufflevector(v0, v1, 0, 1, 2, 3, 4, 5, 6, 7));
+                    o[db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vv, pk[2 * kb + sp], o[db], 0, 0, 0);
+                }
+    };
+
+    if (PRIO && wave >= NW / 2) __builtin_amdgcn_s_setprio(1);
+    if (nkt > 0) issue(0);
+    f32x16 sc[2];
+    bf16x8 pk[4];
+    if constexpr (!DPV) {
+        for (int t = 0; t < nkt; t += 2) {
+            vm_wait<0>();
+            __builtin_amdgcn_s_barrier();
+            if (t + 1 < nkt) issue(t + 1);
+            qk(t, 0, sc);
+            softmax(sc, pk);
+            pv(0, pk);
+            if (t + 1 < nkt) {
+                vm_wait<0>();
+                __builtin_amdgcn_s_barrier();
+                if (t + 2 < nkt) issue(t + 2);
+                qk(t + 1, TILE, sc);
+                softmax(sc, pk);
+                pv(TILE, pk);
+            }
+        }
+    } else {
+        // delayed PV: iteration t runs QK(t), then PV(t - 1) -- MFMAs independent of tile t's
+        // softmax, which the wave issues beside them -- then softmax(t) (its O rescale after
+        // PV(t - 1) in program order). 3-slot ring: tile t + 1 lands in the slot of t - 2, whose
+        // last reads (PV(t - 2), iteration t - 1) precede this iteration's barrier.
+        for (int t = 0; t < nkt; t += 3) {
+#pragma unroll
+            for (int u = 0; u < 3; ++u) {
+                const int tt = t + u;
+                if (tt < nkt) {
+                    vm_wait<0>();
+                    __builtin_amdgcn_s_barrier();
+                    if (tt + 1 < nkt) issue(tt + 1);
+                    qk(tt, u * TILE, sc);
+                    if (tt > 0) pv(((u + 2) % 3) * TILE, pk);
+                    softmax(sc, pk);
+                }
+            }
+        }
+        if (nkt > 0) pv(((nkt - 1) % 3) * TILE, pk);
+    }
+
+    float ltot;
+    if (ONES) {
+        // register 4 (HD % 32) / 8 of d-block HD / 32 is O^T row HD + 4 hh: both rows lie in
+        // the ones plane (columns HD .. HD + 7), so every lane holds its query's weight sum
+        constexpr int DB1 = HD / 32, REG1 = 4 * ((HD % 32) / 8);
+        ltot = o[DB1][REG1];
+    } else {
+        ltot = xsum32(lsum);
+    }
+    const float inv = 1.0f / ltot;
+    const int q = qw0 + r;
+    bf16* orow = a.out + ((long)b * T + min(q, T - 1)) * a.ldo + h * HD;
+    // registers 4 mm .. 4 mm + 3 of d-block db = columns 32 db + 8 mm + 4 hh .. + 3; a
+    // permlane32 swap of the pair (mm, mm + 1) gives lane half hh the 8 columns 32 db + 8 (mm + hh) ..
+#pragma unroll
+    for (int db = 0; db < NDB; ++db)
+#pragma unroll
+        for (int mm = 0; mm < 4; mm += 2) {
+            if (32 * db + 8 * mm >= HD) continue;
+            bf16x4 v0, v1;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                v0[e] = f2bf(o[db][4 * mm + e] * inv);
+                v1[e] = f2bf(o[db][4 * mm + 4 + e] * inv);
+            }
+            const uint2 x = __builtin_bit_cast(uint2, v0), y = __builtin_bit_cast(uint2, v1);
+            const auto sx = __builtin_amdgcn_permlane32_swap(x.x, y.x, false, false);
+            const auto sy = __builtin_amdgcn_permlane32_swap(x.y, y.y, false, false);
+            const int d0 = 32 * db + 8 * (mm + hh);
+            if (q < T && d0 + 8 <= HD) *reinterpret_cast<uint4*>(orow + d0) = make_uint4(sx[0], sy[0], sx[1], sy[1]);
+        }
+}
+
 // SigLIP MAP head: one probe query per head, keys = the T tokens of image b.
 constexpr int PROBE_MAXT = 1024;
 __global__ __launch_bounds__(256) void probe_attn_kernel(const bf16* __restrict__ qv, const bf16* __restrict__ kv,
@@ -1284,6 +1558,25 @@ void launch_attn(int kind, const AttnArgs& a, int B, int T, int H, hipStream_t s
     else if (kind == 31)  // dev: both
         hipLaunchKernelGGL((attn_pipe_kernel<HD, 8, 2, false, HD == 72, true, false, 4, true, 6>),
                            dim3(cdiv(T, 256) * H * B), dim3(512), 0, st, a);
+    else if (kind == 38)  // attn_m32_kernel: 8 waves (<= 128 VGPRs uncapped: 4 waves / SIMD), static priority;
+                          // production for hd 80 (DFN5B T 730)
+        hipLaunchKernelGGL((attn_m32_kernel<HD, 8, 1, true>), dim3(cdiv(T, 256) * H * B), dim3(512), 0, st, a);
+    else if (kind == 39)  // dev: attn_m32_kernel, 12 waves (384 queries), 3 waves / SIMD
+        hipLaunchKernelGGL((attn_m32_kernel<HD, 12, 3, true>), dim3(cdiv(T, 384) * H * B), dim3(768), 0, st, a);
+    else if (kind == 40)  // dev: attn_m32_kernel, 8 waves, amdgpu_waves_per_eu(4) (spills 8 registers)
+        hipLaunchKernelGGL((attn_m32_kernel<HD, 8, 4, true>), dim3(cdiv(T, 256) * H * B), dim3(512), 0, st, a);
+    else if (kind == 41)  // attn_m32_kernel, 9 waves (288 queries): production for hd 80 where 9-wave blocks pad least
+        hipLaunchKernelGGL((attn_m32_kernel<HD, 9, 1, true>), dim3(cdiv(T, 288) * H * B), dim3(576), 0, st, a);
+    else if (kind == 42)  // dev: attn_m32_kernel, 8 waves, no static priority
+        hipLaunchKernelGGL((attn_m32_kernel<HD, 8, 1, false>), dim3(cdiv(T, 256) * H * B), dim3(512), 0, st, a);
+    else if (kind == 43)  // dev: attn_m32_kernel with delayed PV (3-slot ring), 8 waves
+        hipLaunchKernelGGL((attn_m32_kernel<HD, 8, 1, true, true>), dim3(cdiv(T, 256) * H * B), dim3(512), 0, st, a);
+    else if (kind == 44)  // dev: delayed PV, 8 waves, amdgpu_waves_per_eu(4)
+        hipLaunchKernelGGL((attn_m32_kernel<HD, 8, 4, true, true>), dim3(cdiv(T, 256) * H * B), dim3(512), 0, st, a);
+    else if (kind == 45)  // dev: delayed PV, 12 waves
+        hipLaunchKernelGGL((attn_m32_kernel<HD, 12, 1, true, true>), dim3(cdiv(T, 384) * H * B), dim3(768), 0, st, a);
+    else if (kind == 46)  // dev: delayed PV, 9 waves
+        hipLaunchKernelGGL((attn_m32_kernel<HD, 9, 1, true, true>), dim3(cdiv(T, 288) * H * B), dim3(576), 0, st, a);
     else if (kind == 12)  // dev: pipelined + lazy + ones
         hipLaunchKernelGGL((attn_pipe_kernel<HD, 8, 3, true, HD == 72, true>), dim3(cdiv(T, 256) * H * B), dim3(512), 0, st, a);
     else
@@ -1333,8 +1626,14 @@ extern "C" int mme_attention(const void* qkv, int ld_qkv, void* out, int ld_out,
     // (one block per CU either way): DFN5B (T 730) 0.640 -> 0.558 ms per 128-image layer.
     const long pad8 = (long)cdiv(T, 256) * 256, pad4 = (long)cdiv(T, 128) * 128, pad9 = (long)cdiv(T, 288) * 288;
     const long pad12 = (long)cdiv(T, 384) * 384;
+    // Round 2, head dim 80: attn_m32_kernel (32x32x16 MFMAs, QK^T 80 deep instead of 96, weight
+    // sums from a ones plane): DFN5B (T 730) 632 -> 700-723 TF/s with 8-wave blocks, ViT-H (T 257)
+    // 308-317 -> 349 TF/s with 9-wave blocks (profiles/r02_attn_m32_bench.log). At head dim 72 it
+    // measures level with kind 30 (635-645 vs 604-638) and at 64 slower than kind 0: not dispatched.
     int kind = T <= 64 ? 16
                : (T <= 128 || hd == 64) ? 0
+               : (hd == 80 && pad9 * 10 < min(pad8, pad4) * 9) ? 41
+               : hd == 80 && pad8 * 10 <= pad4 * 11 ? 38
                : pad9 * 10 < min(pad8, pad4) * 9 ? 35
                : (hd == 80 && pad12 <= pad8 && pad12 * 10 <= pad4 * 11) ? 23
                : (pad8 * 10 <= pad4 * 11 ? (hd == 72 ? 30 : 11) : 14);
@@ -1349,7 +1648,7 @@ extern "C" int mme_attention(const void* qkv, int ld_qkv, void* out, int ld_out,
         return mme_check_launch("mme_attention");
     }
     if (g_attn_variant >= 9 && g_attn_variant <= 16) kind = g_attn_variant - 9;  // dev: force a kernel
-    if (g_attn_variant >= 30 && g_attn_variant <= 69) kind = g_attn_variant - 30;  // dev: force a kernel
+    if (g_attn_variant >= 30 && g_attn_variant <= 99) kind = g_attn_variant - 30;  // dev: force a kernel
     if ((kind == 16 || kind == 19) && T > 64) kind = 0;  // the short kernels hold one 64-key tile
     if (g_attn_variant >= 21 && g_attn_variant <= 26 && hd == 72) {  // dev: attn_dma_kernel<72,8,2> diagnostics
         const dim3 grid(cdiv(T, 256) * H * B), blk(512);

@@ -129,6 +129,33 @@ def test_attention(cuda, B, T, H, hd, causal, lens):
     torch.testing.assert_close(out.float(), ref, atol=2e-2, rtol=2e-2)
 
 
+@pytest.mark.parametrize("kind", [38, 39, 40, 41, 42, 43, 44, 45, 46])
+@pytest.mark.parametrize("B,T,H,hd,causal,lens", [
+    (2, 729, 4, 72, False, None),       # SigLIP vision geometry
+    (2, 520, 3, 72, False, [520, 301]),  # key padding, partial last tile
+    (2, 200, 3, 72, True, None),
+    (1, 730, 3, 80, False, None),        # DFN5B
+    (2, 257, 2, 80, True, [257, 100]),
+    (2, 577, 3, 64, False, None),        # CLIP-L (f32 weight sums, no ones plane)
+    (2, 300, 2, 64, True, [300, 133]),
+])
+def test_attention_m32(cuda, kind, B, T, H, hd, causal, lens):
+    """attn_m32_kernel (v_mfma_f32_32x32x16_bf16 flash loop) forced through the dev switch."""
+    from mme import _lib
+    lib = _lib.load()
+    g = torch.Generator(device="cuda").manual_seed(B * T + hd + kind)
+    qkv = rnd(B * T, 3 * H * hd, scale=1.5, gen=g)
+    sl = None if lens is None else torch.tensor(lens, dtype=torch.int32, device="cuda")
+    lib.mme_attention_variant(30 + kind)
+    try:
+        out = ops.attention(qkv, B, T, H, hd, seq_lens=sl, causal=causal)
+        torch.cuda.synchronize()
+    finally:
+        lib.mme_attention_variant(0)
+    ref = attn_ref(qkv, B, T, H, hd, sl, causal, hd ** -0.5)
+    torch.testing.assert_close(out.float(), ref, atol=2e-2, rtol=2e-2)
+
+
 def test_attention_strided_qkv(cuda):
     B, T, H, hd = 2, 100, 16, 72
     g = torch.Generator(device="cuda").manual_seed(9)

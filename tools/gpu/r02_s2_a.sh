@@ -1,0 +1,9 @@
+set -o pipefail
+export PYTHONUNBUFFERED=1
+export TMPDIR=/tmp
+mkdir -p gpurun_out
+timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread -m gpu tests/test_gpu_kernels.py -k "attention" > gpurun_out/r02_attn_m32_pytest.log 2>&1 && \
+timeout -k 10 400 python -u tools/attn_bench.py --cases siglip_vision,dfn5b_vision,vitH_vision,clipL_vision --variants 0,68,69,70,71,72,0,68 > gpurun_out/r02_attn_m32_bench.log 2>&1 && \
+timeout -k 10 900 python -u -m pytest -x -q --timeout 300 --timeout-method thread -m gpu tests/ > gpurun_out/r02_s2_pytest.log 2>&1 && \
+timeout -k 10 200 python -u -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/r02_s2_smoke.log 2>&1 && \
+timeout -k 10 600 python -u bench.py > gpurun_out/r02_s2_bench.log 2>&1
