@@ -262,6 +262,35 @@ def test_gemm_res_stats(cuda, M, N, K, shift):
     assert torch.equal(xi, ref_out)
 
 
+# The LDS-staged statistics combine (production for an even slice count <= 20) runs the per-row
+# kernel's arithmetic in the same order: bit-identical statistics (dev variant 48 = per-row form),
+# including a ragged last block of rows.
+@pytest.mark.parametrize("M,N,K", [(4096, 1152, 1152), (3001, 1280, 512), (2000, 1024, 256)])
+def test_row_part_combine_lds_bit_identical(cuda, M, N, K):
+    import ctypes
+    lib = _lib.load()
+    lib.mme_gemm_variant.argtypes = [ctypes.c_int]
+    g = torch.Generator(device="cuda").manual_seed(M + 3 * N + K)
+    a = rnd(M, K, gen=g)
+    w = rnd(N, K, scale=1 / math.sqrt(K), gen=g)
+    b = rnd(N, scale=0.1, gen=g)
+    x = rnd(M, N, scale=2.0, gen=g)
+    res = []
+    for v in (-1, 48):
+        st = torch.full((M, 2), float("nan"), dtype=torch.float32, device="cuda")
+        part = torch.empty(M, N // 64, 2, dtype=torch.float32, device="cuda")
+        lib.mme_gemm_variant(v)
+        try:
+            out = ops.gemm_res_stats(a, w, b, x.clone(), 1e-6, st, part)
+            torch.cuda.synchronize()
+        finally:
+            lib.mme_gemm_variant(-1)
+        res.append((out, st))
+    assert torch.equal(res[0][0], res[1][0])
+    assert torch.isfinite(res[0][1]).all()
+    assert torch.equal(res[0][1], res[1][1]), "LDS-staged combine differs from the per-row combine"
+
+
 # pipe8 (production where K % 64 == 0 and K >= 192: 64-deep stages of whole-line rows in a
 # 5-unit LDS ring) keeps pipe6's K-step order and per-MFMA k ranges, so its outputs are
 # bit-identical to pipe6 (dev variant 47) on every epilogue: the ring's minimum depth
