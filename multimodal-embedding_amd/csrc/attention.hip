@@ -1400,6 +1400,363 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(MINW)))
         }
 }
 
+// ---------------------------------------------------------------------------
+// attn_m32x2_kernel: attn_m32_kernel with TWO 32-query sub-blocks per wave. The hd-72 loop
+// reads ~22 KiB of K / V fragments from LDS per wave and tile (10 K reads of 1 KiB, 24
+// transposed V reads of 512 B); at 4 waves per SIMD that is ~80 % of the LDS array's
+// 256 B/clk over the measured tile time, i.e. the loop is bound by the LDS reads, which
+// neither the MFMA shape nor the issue order changes. Here every K / V fragment read
+// feeds the MFMAs of both sub-blocks (64 queries), halving the LDS read bytes per FLOP.
+// Registers: Q^T fragments, O^T accumulators, running max / sum per sub-block (~220
+// VGPRs: 2 waves per SIMD); NW = 4 waves = 256 queries per block, two blocks per CU.
+// Sub-block math, LDS layout, DMA and output are attn_m32_kernel's.
+// ---------------------------------------------------------------------------
+template <int V>
+struct IC {
+    static constexpr int value = V;
+};
+
+template <int HD, int NW, bool PRIO, bool ILV = false>
+__global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(2))) void attn_m32x2_kernel(AttnArgs a) {
+    constexpr bool ONES = HD % 32 != 0;
+    constexpr int NCHL = HD / 8;
+    constexpr int NKS = (HD + 15) / 16;
+    constexpr int NDB = (HD + (ONES ? 1 : 0) + 31) / 32;
+    constexpr int NVP = 4 * NDB;
+    constexpr int TILE = (NCHL + NVP) * 1024;
+    constexpr int NINS = 2 * NCHL;
+    constexpr int MAXI = (NINS + NW - 1) / NW;
+    constexpr int QB = NW * 64;
+    static_assert(2 * NKS <= NCHL + NVP, "K reads past the head dim stay inside the tile");
+    __shared__ __attribute__((aligned(16))) char lds[2 * TILE];
+
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int r = lane & 31, hh = lane >> 5;
+    const int nqb = (a.T + QB - 1) / QB;
+    int id;
+    {
+        const int bid = blockIdx.x, nwg = gridDim.x;
+        const int xcd = bid & 7, loc = bid >> 3, q8 = nwg >> 3, r8 = nwg & 7;
+        id = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + loc;
+    }
+    const int qb = id % nqb, h = (id / nqb) % a.H, b = id / (nqb * a.H);
+    const int T = a.T, D = a.H * HD;
+    const bf16* base = a.qkv + (long)b * T * a.ld;
+    const int qw0 = qb * QB + wave * 64;  // sub-block u: queries qw0 + 32 u + r
+    const int Tk = a.seq_lens ? a.seq_lens[b] : T;
+    const float c = a.scale_log2;
+
+    constexpr int NPAD = NVP > NCHL ? NVP - NCHL : 1;
+    for (int i = tid; i < 2 * (NVP - NCHL) * 64; i += NW * 64) {
+        const int slot = i / (NPAD * 64), rem = i % (NPAD * 64);
+        const int pl = NCHL + rem / 64;
+        const unsigned short v = (ONES && pl == NCHL) ? 0x3F80 : 0;
+        *reinterpret_cast<u16x8*>(lds + slot * TILE + (NCHL + pl) * 1024 + (rem & 63) * 16) =
+            u16x8{v, v, v, v, v, v, v, v};
+    }
+
+    bf16x8 qf[2][NKS];
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+        const bf16* qrow = base + (long)min(qw0 + 32 * u + r, T - 1) * a.ld + h * HD;
+#pragma unroll
+        for (int ks = 0; ks < NKS; ++ks) {
+            const int col = ks * 16 + 8 * hh;
+            if (col < HD)
+                qf[u][ks] = *reinterpret_cast<const bf16x8*>(qrow + col);
+            else
+                qf[u][ks] = bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
+        }
+    }
+
+    int nkt = (Tk + 63) / 64;
+    if (a.causal) nkt = min(nkt, (min(T, qb * QB + QB) + 63) / 64);
+
+    auto issue = [&](int t) {
+        char* tb = lds + (t & 1) * TILE;
+#pragma unroll
+        for (int i = 0; i < MAXI; ++i) {
+            const int idx = wave + NW * i;
+            if (i < MAXI - 1 || idx < NINS) {
+                const bool isV = idx >= NCHL;
+                const int plane = isV ? idx - NCHL : idx;
+                const int key = isV ? lane ^ (4 * (plane & 3)) : lane;
+                const bf16* src = base + (long)min(t * 64 + key, T - 1) * a.ld + (isV ? 2 : 1) * D + h * HD + plane * 8;
+                glds16(src, tb + idx * 1024);
+            }
+        }
+    };
+
+    const unsigned lds0 = (unsigned)(uintptr_t)(LDS_AS char*)lds;
+    const unsigned kb0 = lds0 + hh * 1024 + r * 16;
+    unsigned vbj[2];
+    {
+        const int i16 = lane & 15, q = i16 >> 2, p = i16 & 3, half = (lane >> 4) & 1;
+        const int cc = 2 * half + (p >> 1);
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+            vbj[j] = lds0 + (NCHL + cc) * 1024 + (((8 * j + 4 * hh + q) ^ (4 * cc)) * 16) + (p & 1) * 8;
+    }
+
+    f32x16 o[2][NDB];
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+#pragma unroll
+        for (int i = 0; i < NDB; ++i)
+#pragma unroll
+            for (int e = 0; e < 16; ++e) o[u][i][e] = 0.f;
+    float m[2] = {-1e30f, -1e30f}, lsum[2] = {0.f, 0.f};
+
+    // ILV: each wave's own MFMA and VALU streams interleaved in program order (the counters put
+    // MFMA busy + VALU busy ~ the tile time: the two barely overlap). Per tile, four segments:
+    // QK(u0) | QK(u1) + softmax(u0) | PV(u0) + softmax(u1) | PV(u1), the MFMA / VALU / LDS-read
+    // placement inside the two mixed segments fixed by sched_group_barrier; the masking and the
+    // lazy rescale branches sit on the segment boundaries.
+    auto qk_u = [&](auto U, const unsigned so, f32x16(&s2)[2]) {
+        constexpr int u = decltype(U)::value;
+#pragma unroll
+        for (int kb = 0; kb < 2; ++kb) {
+            f32x16 z;
+#pragma unroll
+            for (int e = 0; e < 16; ++e) z[e] = 0.f;
+#pragma unroll
+            for (int ks = 0; ks < NKS; ++ks) {
+                const bf16x8 kf = *reinterpret_cast<const LDS_AS bf16x8*>((uintptr_t)(kb0 + so + kb * 512 + ks * 2048));
+                z = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[u][ks], z, 0, 0, 0);
+            }
+            s2[kb] = z;
+        }
+    };
+    auto mask_u = [&](auto U, int t, f32x16(&s2)[2]) {
+        constexpr int u = decltype(U)::value;
+        if ((t * 64 + 64 > Tk) || (a.causal && t * 64 + 63 > qw0 + 32 * u)) {
+            const int q = qw0 + 32 * u + r;
+            const int lim = a.causal ? min(Tk, q + 1) : Tk;
+#pragma unroll
+            for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+                for (int e = 0; e < 16; ++e)
+                    if (t * 64 + kb * 32 + (e & 3) + 8 * (e >> 2) + 4 * hh >= lim) s2[kb][e] = -INFINITY;
+        }
+    };
+    // max + exp + pack (no branch): returns the new max; the caller rescales O on the boundary
+    auto sm_u = [&](auto U, f32x16(&s2)[2], bf16x8(&p4)[4]) {
+        constexpr int u = decltype(U)::value;
+        float mloc = fmaxf(s2[0][0], s2[0][1]);
+#pragma unroll
+        for (int e = 2; e < 16; ++e) mloc = fmaxf(mloc, s2[0][e]);
+#pragma unroll
+        for (int e = 0; e < 16; ++e) mloc = fmaxf(mloc, s2[1][e]);
+        mloc = xmax32(mloc);
+        const float mnew = fmaxf(m[u], mloc);
+        const float mc = mnew * c;
+        float psum = 0.f;
+#pragma unroll
+        for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+            for (int e = 0; e < 16; ++e) {
+                const float pv = __builtin_amdgcn_exp2f(s2[kb][e] * c - mc);
+                s2[kb][e] = pv;
+                if (!ONES) psum += pv;
+            }
+#pragma unroll
+        for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+            for (int sp = 0; sp < 2; ++sp)
+#pragma unroll
+                for (int j = 0; j < 8; ++j) p4[2 * kb + sp][j] = f2bf(s2[kb][8 * sp + j]);
+        return make_float2(mnew, psum);
+    };
+    auto rescale_u = [&](auto U, float2 mp) __attribute__((always_inline)) {
+        constexpr int u = decltype(U)::value;
+        const float mnew = mp.x;
+        if (__builtin_amdgcn_ballot_w64(mnew != m[u])) {
+            const float alpha = __builtin_amdgcn_exp2f((m[u] - mnew) * c);
+            if (!ONES) lsum[u] *= alpha;
+#pragma unroll
+            for (int i = 0; i < NDB; ++i) o[u][i] *= alpha;
+        }
+        m[u] = mnew;
+        if (!ONES) lsum[u] += mp.y;
+    };
+    auto pv_u = [&](auto U, const unsigned so, const bf16x8(&p4)[4]) {
+        constexpr int u = decltype(U)::value;
+#pragma unroll
+        for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+            for (int sp = 0; sp < 2; ++sp)
+#pragma unroll
+                for (int db = 0; db < NDB; ++db) {
+                    const unsigned off = so + db * 4096 + kb * 512 + sp * 256;
+                    const s16x4 v0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS_AS s16x4*)(uintptr_t)(vbj[0] + off));
+                    const s16x4 v1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS_AS s16x4*)(uintptr_t)(vbj[1] + off));
+                    const bf16x8 vv = __builtin_bit_cast(bf16x8, __builtin_shufflevector(v0, v1, 0, 1, 2, 3, 4, 5, 6, 7));
+                    o[u][db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vv, p4[2 * kb + sp], o[u][db], 0, 0, 0);
+                }
+    };
+    auto tile_ilv = [&](int t, const unsigned so) __attribute__((always_inline)) {
+        f32x16 s0[2], s1[2];
+        bf16x8 p0[4], p1[4];
+        qk_u(IC<0>{}, so, s0);
+        mask_u(IC<0>{}, t, s0);
+        __builtin_amdgcn_sched_barrier(0);
+        qk_u(IC<1>{}, so, s1);
+        const float2 mp0 = sm_u(IC<0>{}, s0, p0);
+#pragma unroll
+        for (int i = 0; i < 2 * NKS; ++i) {
+            __builtin_amdgcn_sched_group_barrier(0x100, 1, 1);  // K fragment read
+            __builtin_amdgcn_sched_group_barrier(0x008, 1, 1);  // QK(u1) MFMA
+            __builtin_amdgcn_sched_group_barrier(0x402, 9, 1);  // softmax(u0) VALU / exp
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        rescale_u(IC<0>{}, mp0);
+        mask_u(IC<1>{}, t, s1);
+        __builtin_amdgcn_sched_barrier(0);
+        pv_u(IC<0>{}, so, p0);
+        const float2 mp1 = sm_u(IC<1>{}, s1, p1);
+#pragma unroll
+        for (int i = 0; i < 4 * NDB; ++i) {
+            __builtin_amdgcn_sched_group_barrier(0x100, 2, 2);  // V^T transposed reads
+            __builtin_amdgcn_sched_group_barrier(0x008, 1, 2);  // PV(u0) MFMA
+            __builtin_amdgcn_sched_group_barrier(0x402, 8, 2);  // softmax(u1) VALU / exp
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        rescale_u(IC<1>{}, mp1);
+        __builtin_amdgcn_sched_barrier(0);
+        pv_u(IC<1>{}, so, p1);
+    };
+
+    auto tile_step = [&](int t, const unsigned so) __attribute__((always_inline)) {
+        if constexpr (ILV) {
+            tile_ilv(t, so);
+            return;
+        }
+        f32x16 sc[2][2];
+#pragma unroll
+        for (int kb = 0; kb < 2; ++kb) {
+            f32x16 z0, z1;
+#pragma unroll
+            for (int e = 0; e < 16; ++e) z0[e] = z1[e] = 0.f;
+#pragma unroll
+            for (int ks = 0; ks < NKS; ++ks) {
+                const bf16x8 kf = *reinterpret_cast<const LDS_AS bf16x8*>((uintptr_t)(kb0 + so + kb * 512 + ks * 2048));
+                z0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[0][ks], z0, 0, 0, 0);
+                z1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[1][ks], z1, 0, 0, 0);
+            }
+            sc[0][kb] = z0;
+            sc[1][kb] = z1;
+        }
+        if ((t * 64 + 64 > Tk) || (a.causal && t * 64 + 63 > qw0)) {
+#pragma unroll
+            for (int u = 0; u < 2; ++u) {
+                const int q = qw0 + 32 * u + r;
+                const int lim = a.causal ? min(Tk, q + 1) : Tk;
+#pragma unroll
+                for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+                    for (int e = 0; e < 16; ++e)
+                        if (t * 64 + kb * 32 + (e & 3) + 8 * (e >> 2) + 4 * hh >= lim) sc[u][kb][e] = -INFINITY;
+            }
+        }
+        bf16x8 pk[2][4];
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+            float mloc = fmaxf(sc[u][0][0], sc[u][0][1]);
+#pragma unroll
+            for (int e = 2; e < 16; ++e) mloc = fmaxf(mloc, sc[u][0][e]);
+#pragma unroll
+            for (int e = 0; e < 16; ++e) mloc = fmaxf(mloc, sc[u][1][e]);
+            mloc = xmax32(mloc);
+            const float mnew = fmaxf(m[u], mloc);
+            if (__builtin_amdgcn_ballot_w64(mnew != m[u])) {
+                const float alpha = __builtin_amdgcn_exp2f((m[u] - mnew) * c);
+                if (!ONES) lsum[u] *= alpha;
+#pragma unroll
+                for (int i = 0; i < NDB; ++i) o[u][i] *= alpha;
+            }
+            m[u] = mnew;
+            const float mc = mnew * c;
+            float psum = 0.f;
+#pragma unroll
+            for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+                for (int e = 0; e < 16; ++e) {
+                    const float pv = __builtin_amdgcn_exp2f(sc[u][kb][e] * c - mc);
+                    sc[u][kb][e] = pv;
+                    if (!ONES) psum += pv;
+                }
+            if (!ONES) lsum[u] += psum;
+#pragma unroll
+            for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+                for (int sp = 0; sp < 2; ++sp)
+#pragma unroll
+                    for (int j = 0; j < 8; ++j) pk[u][2 * kb + sp][j] = f2bf(sc[u][kb][8 * sp + j]);
+        }
+#pragma unroll
+        for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+            for (int sp = 0; sp < 2; ++sp)
+#pragma unroll
+                for (int db = 0; db < NDB; ++db) {
+                    const unsigned off = so + db * 4096 + kb * 512 + sp * 256;
+                    const s16x4 v0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS_AS s16x4*)(uintptr_t)(vbj[0] + off));
+                    const s16x4 v1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS_AS s16x4*)(uintptr_t)(vbj[1] + off));
+                    const bf16x8 vv = __builtin_bit_cast(bf16x8, __builtin_shufflevector(v0, v1, 0, 1, 2, 3, 4, 5, 6, 7));
+                    o[0][db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vv, pk[0][2 * kb + sp], o[0][db], 0, 0, 0);
+                    o[1][db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vv, pk[1][2 * kb + sp], o[1][db], 0, 0, 0);
+                }
+    };
+
+    if (PRIO && wave >= NW / 2) __builtin_amdgcn_s_setprio(1);
+    if (nkt > 0) issue(0);
+    for (int t = 0; t < nkt; t += 2) {
+        vm_wait<0>();
+        __builtin_amdgcn_s_barrier();
+        if (t + 1 < nkt) issue(t + 1);
+        tile_step(t, 0);
+        if (t + 1 < nkt) {
+            vm_wait<0>();
+            __builtin_amdgcn_s_barrier();
+            if (t + 2 < nkt) issue(t + 2);
+            tile_step(t + 1, TILE);
+        }
+    }
+
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+        float ltot;
+        if (ONES) {
+            constexpr int DB1 = HD / 32, REG1 = 4 * ((HD % 32) / 8);
+            ltot = o[u][DB1][REG1];
+        } else {
+            ltot = xsum32(lsum[u]);
+        }
+        const float inv = 1.0f / ltot;
+        const int q = qw0 + 32 * u + r;
+        bf16* orow = a.out + ((long)b * T + min(q, T - 1)) * a.ldo + h * HD;
+#pragma unroll
+        for (int db = 0; db < NDB; ++db)
+#pragma unroll
+            for (int mm = 0; mm < 4; mm += 2) {
+                if (32 * db + 8 * mm >= HD) continue;
+                bf16x4 v0, v1;
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    v0[e] = f2bf(o[u][db][4 * mm + e] * inv);
+                    v1[e] = f2bf(o[u][db][4 * mm + 4 + e] * inv);
+                }
+                const uint2 x = __builtin_bit_cast(uint2, v0), y = __builtin_bit_cast(uint2, v1);
+                const auto sx = __builtin_amdgcn_permlane32_swap(x.x, y.x, false, false);
+                const auto sy = __builtin_amdgcn_permlane32_swap(x.y, y.y, false, false);
+                const int d0 = 32 * db + 8 * (mm + hh);
+                if (q < T && d0 + 8 <= HD)
+                    *reinterpret_cast<uint4*>(orow + d0) = make_uint4(sx[0], sy[0], sx[1], sy[1]);
+            }
+    }
+}
+
 // SigLIP MAP head: one probe query per head, keys = the T tokens of image b.
 constexpr int PROBE_MAXT = 1024;
 __global__ __launch_bounds__(256) void probe_attn_kernel(const bf16* __restrict__ qv, const bf16* __restrict__ kv,
@@ -1577,6 +1934,18 @@ void launch_attn(int kind, const AttnArgs& a, int B, int T, int H, hipStream_t s
         hipLaunchKernelGGL((attn_m32_kernel<HD, 12, 1, true, true>), dim3(cdiv(T, 384) * H * B), dim3(768), 0, st, a);
     else if (kind == 46)  // dev: delayed PV, 9 waves
         hipLaunchKernelGGL((attn_m32_kernel<HD, 9, 1, true, true>), dim3(cdiv(T, 288) * H * B), dim3(576), 0, st, a);
+    else if (kind == 47)  // dev: attn_m32x2_kernel (64 queries per wave), 4 waves = 256 queries per block
+        hipLaunchKernelGGL((attn_m32x2_kernel<HD, 4, true>), dim3(cdiv(T, 256) * H * B), dim3(256), 0, st, a);
+    else if (kind == 48)  // dev: attn_m32x2_kernel, no static priority
+        hipLaunchKernelGGL((attn_m32x2_kernel<HD, 4, false>), dim3(cdiv(T, 256) * H * B), dim3(256), 0, st, a);
+    else if (kind == 49)  // dev: attn_m32x2_kernel, 6 waves = 384 queries per block
+        hipLaunchKernelGGL((attn_m32x2_kernel<HD, 6, true>), dim3(cdiv(T, 384) * H * B), dim3(384), 0, st, a);
+    else if (kind == 50)  // dev: attn_m32x2_kernel, 8 waves = 512 queries per block
+        hipLaunchKernelGGL((attn_m32x2_kernel<HD, 8, true>), dim3(cdiv(T, 512) * H * B), dim3(512), 0, st, a);
+    else if (kind == 51)  // dev: attn_m32x2_kernel, MFMA / VALU interleaved per wave (sched_group_barrier)
+        hipLaunchKernelGGL((attn_m32x2_kernel<HD, 4, true, true>), dim3(cdiv(T, 256) * H * B), dim3(256), 0, st, a);
+    else if (kind == 52)  // dev: kind 51 without static priority
+        hipLaunchKernelGGL((attn_m32x2_kernel<HD, 4, false, true>), dim3(cdiv(T, 256) * H * B), dim3(256), 0, st, a);
     else if (kind == 12)  // dev: pipelined + lazy + ones
         hipLaunchKernelGGL((attn_pipe_kernel<HD, 8, 3, true, HD == 72, true>), dim3(cdiv(T, 256) * H * B), dim3(512), 0, st, a);
     else
