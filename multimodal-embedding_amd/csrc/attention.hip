@@ -1157,7 +1157,7 @@ __global__ __launch_bounds__(256, 3) void attn_short_kernel(AttnArgs a, int unit
 //     ring (every LDS address a lane base + immediate), 16-B O stores after a
 //     v_permlane32_swap of the two lane halves.
 // ---------------------------------------------------------------------------
-template <int HD, int NW, int MINW, bool PRIO, bool DPV = false>
+template <int HD, int NW, int MINW, bool PRIO, bool DPV = false, bool PF = false>
 __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(MINW))) void attn_m32_kernel(AttnArgs a) {
     constexpr int NSTG = DPV ? 3 : 2;
     constexpr bool ONES = HD % 32 != 0;
@@ -1251,7 +1251,32 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(MINW)))
         for (int e = 0; e < 16; ++e) o[i][e] = 0.f;
     float m = -1e30f, lsum = 0.f;
 
-    auto qk = [&](int t, const unsigned so, f32x16(&sc)[2]) {
+    // PF: every LDS fragment a product needs is read ahead of its MFMAs (the 10 K fragments
+    // before QK^T, the 24 transposed V reads before the softmax, whose VALU covers their
+    // latency); without it the register-capped build re-uses one fragment register and waits
+    // lgkmcnt(0) in front of every MFMA.
+    auto qk_pf = [&](int t, const unsigned so, f32x16(&sc)[2]) __attribute__((always_inline)) {
+        bf16x8 kf[2][NKS];
+#pragma unroll
+        for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+            for (int ks = 0; ks < NKS; ++ks)
+                kf[kb][ks] = *reinterpret_cast<const LDS_AS bf16x8*>((uintptr_t)(kb0 + so + kb * 512 + ks * 2048));
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int kb = 0; kb < 2; ++kb) {
+            f32x16 z;
+#pragma unroll
+            for (int e = 0; e < 16; ++e) z[e] = 0.f;
+#pragma unroll
+            for (int ks = 0; ks < NKS; ++ks) z = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf[kb][ks], qf[ks], z, 0, 0, 0);
+            sc[kb] = z;
+        }
+    };
+    auto qk = [&](int t, const unsigned so, f32x16(&sc)[2]) __attribute__((always_inline)) {
+        if constexpr (PF) {
+            qk_pf(t, so, sc);
+        } else {
 #pragma unroll
         for (int kb = 0; kb < 2; ++kb) {
             f32x16 z;
@@ -1263,6 +1288,7 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(MINW)))
                 z = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[ks], z, 0, 0, 0);
             }
             sc[kb] = z;
+        }
         }
         if ((t * 64 + 64 > Tk) || (a.causal && t * 64 + 63 > qw0)) {
             const int q = qw0 + r;
@@ -1323,12 +1349,53 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(MINW)))
                     o[db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vv, pk[2 * kb + sp], o[db], 0, 0, 0);
                 }
     };
+    // PF: V^T fragments read before the softmax, MFMAs after it
+    auto vread = [&](const unsigned so, bf16x8(&vf)[4][NDB]) __attribute__((always_inline)) {
+#pragma unroll
+        for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+            for (int sp = 0; sp < 2; ++sp)
+#pragma unroll
+                for (int db = 0; db < NDB; ++db) {
+                    const unsigned off = so + db * 4096 + kb * 512 + sp * 256;
+                    const s16x4 v0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS_AS s16x4*)(uintptr_t)(vbj[0] + off));
+                    const s16x4 v1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS_AS s16x4*)(uintptr_t)(vbj[1] + off));
+                    vf[2 * kb + sp][db] = __builtin_bit_cast(bf16x8, __builtin_shufflevector(v0, v1, 0, 1, 2, 3, 4, 5, 6, 7));
+                }
+    };
+    auto pv_pf = [&](const bf16x8(&vf)[4][NDB], const bf16x8(&pk)[4]) __attribute__((always_inline)) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int db = 0; db < NDB; ++db) o[db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf[i][db], pk[i], o[db], 0, 0, 0);
+    };
+    auto tile_pf = [&](int t, const unsigned so, f32x16(&sc)[2], bf16x8(&pk)[4]) __attribute__((always_inline)) {
+        bf16x8 vf[4][NDB];
+        qk(t, so, sc);
+        vread(so, vf);
+        __builtin_amdgcn_sched_barrier(0);
+        softmax(sc, pk);
+        pv_pf(vf, pk);
+    };
 
     if (PRIO && wave >= NW / 2) __builtin_amdgcn_s_setprio(1);
     if (nkt > 0) issue(0);
     f32x16 sc[2];
     bf16x8 pk[4];
-    if constexpr (!DPV) {
+    if constexpr (PF) {
+        for (int t = 0; t < nkt; t += 2) {
+            vm_wait<0>();
+            __builtin_amdgcn_s_barrier();
+            if (t + 1 < nkt) issue(t + 1);
+            tile_pf(t, 0, sc, pk);
+            if (t + 1 < nkt) {
+                vm_wait<0>();
+                __builtin_amdgcn_s_barrier();
+                if (t + 2 < nkt) issue(t + 2);
+                tile_pf(t + 1, TILE, sc, pk);
+            }
+        }
+    } else if constexpr (!DPV) {
         for (int t = 0; t < nkt; t += 2) {
             vm_wait<0>();
             __builtin_amdgcn_s_barrier();
@@ -1946,6 +2013,14 @@ void launch_attn(int kind, const AttnArgs& a, int B, int T, int H, hipStream_t s
         hipLaunchKernelGGL((attn_m32x2_kernel<HD, 4, true, true>), dim3(cdiv(T, 256) * H * B), dim3(256), 0, st, a);
     else if (kind == 52)  // dev: kind 51 without static priority
         hipLaunchKernelGGL((attn_m32x2_kernel<HD, 4, false, true>), dim3(cdiv(T, 256) * H * B), dim3(256), 0, st, a);
+    else if (kind == 54)  // dev: attn_m32_kernel with fragment prefetch (PF), 8 waves, <= 256 VGPRs
+        hipLaunchKernelGGL((attn_m32_kernel<HD, 8, 2, true, false, true>), dim3(cdiv(T, 256) * H * B), dim3(512), 0, st, a);
+    else if (kind == 55)  // dev: PF, 12 waves, 3 waves / SIMD
+        hipLaunchKernelGGL((attn_m32_kernel<HD, 12, 3, true, false, true>), dim3(cdiv(T, 384) * H * B), dim3(768), 0, st, a);
+    else if (kind == 56)  // dev: PF, 8 waves, 4 waves / SIMD cap
+        hipLaunchKernelGGL((attn_m32_kernel<HD, 8, 4, true, false, true>), dim3(cdiv(T, 256) * H * B), dim3(512), 0, st, a);
+    else if (kind == 57)  // dev: PF, 9 waves, 3 waves / SIMD
+        hipLaunchKernelGGL((attn_m32_kernel<HD, 9, 3, true, false, true>), dim3(cdiv(T, 288) * H * B), dim3(576), 0, st, a);
     else if (kind == 12)  // dev: pipelined + lazy + ones
         hipLaunchKernelGGL((attn_pipe_kernel<HD, 8, 3, true, HD == 72, true>), dim3(cdiv(T, 256) * H * B), dim3(512), 0, st, a);
     else
