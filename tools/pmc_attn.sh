@@ -5,7 +5,7 @@ cd "${GRAFT_REPO_ROOT:-/root/repo}"
 export TMPDIR=/tmp
 OUT=gpurun_out/pmc_attn
 mkdir -p $OUT
-CMD="python3 tools/attn_bench.py --cases ${CASES:-siglip_vision}"
+CMD="python3 tools/attn_bench.py --cases ${CASES:-siglip_vision} --variants ${VARIANTS:-0}"
 timeout -k 10 60 rocprofv3 -L > $OUT/counters_list.txt 2>&1 || true
 i=0
 for G in "SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE" \
@@ -23,7 +23,7 @@ for f in glob.glob("gpurun_out/pmc_attn/**/*counter_collection.csv", recursive=T
         k = r["Kernel_Name"]
         if "attn" not in k:
             continue
-        k = k[:90]
+        k = k[:110]
         acc[k][r["Counter_Name"]] += float(r["Counter_Value"])
         cnt[k].add(r.get("Dispatch_Id"))
 out = {}
