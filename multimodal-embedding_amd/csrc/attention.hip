@@ -1824,6 +1824,225 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(2))) vo
     }
 }
 
+// ---------------------------------------------------------------------------
+// attn_hyb_kernel (head dim 72): QK^T on v_mfma_f32_32x32x16_bf16 (80 deep, as attn_m32_kernel)
+// and PV on v_mfma_f32_16x16x32_bf16 (80 output rows: 5 d-tiles of 16, the ones row at d = 72),
+// i.e. 160 MFMA rows per 144 useful instead of 176 for either single-shape kernel. The
+// hd-72 kernels run against the power cap (profiles/r02_pmc_attn_kind30_vs_m32.json), so
+// the MFMA work they skip is what can pay.
+//   P layout change: the 32x32 S^T accumulator gives lane (r, h) query r and keys
+//   (e & 3) + 8 (e >> 2) + 4 h of a 32-key block (e = 0..15). One v_permlane16_swap per
+//   packed register pair (x = e 0..7, y = e 8..15) turns them into the two 16x16x32 B
+//   operands: x' (queries 0..15) and y' (queries 16..31), where lane l of 16-lane group
+//   g = l >> 4 holds keys base_g + (j & 3) + 8 (j >> 2), base = {0, 16, 4, 20}.
+//   V^T operand: two ds_read_b64_tr_b16 per (key block, d-tile) at keys base_g + q and
+//   base_g + 8 + q; V plane c stores key k in slot k ^ (4 bit4(k) + 8 (c & 1)), which puts
+//   a 32-lane half's reads (2 planes x 2 key runs) on 64 distinct banks.
+//   O^T (16x16 tiles): lane l holds query 16 u + (l & 15), rows 4 g + reg of each d-tile;
+//   the running max lives with the S^T lanes, so the (lazy) rescale shuffles alpha over.
+// ---------------------------------------------------------------------------
+template <int NW, int MINW, bool PRIO>
+__global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(MINW))) void attn_hyb_kernel(AttnArgs a) {
+    constexpr int HD = 72;
+    constexpr int NCHL = HD / 8;  // 9 K / V planes with data
+    constexpr int NKS = 5;        // QK^T k-steps of 16 (80 deep)
+    constexpr int NDT = 5;        // PV d-tiles of 16 (80 rows; row 72 = weight sums)
+    constexpr int NVP = 2 * NDT;  // V planes read: 9 data + the ones plane
+    constexpr int TILE = (NCHL + NVP) * 1024;
+    constexpr int NINS = 2 * NCHL;
+    constexpr int MAXI = (NINS + NW - 1) / NW;
+    constexpr int QB = NW * 32;
+    static_assert(2 * NKS <= NCHL + NVP, "K reads past the head dim stay inside the tile");
+    typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
+    __shared__ __attribute__((aligned(16))) char lds[2 * TILE];
+
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int r = lane & 31, hh = lane >> 5;
+    const int g = lane >> 4, li = lane & 15;
+    const int nqb = (a.T + QB - 1) / QB;
+    int id;
+    {
+        const int bid = blockIdx.x, nwg = gridDim.x;
+        const int xcd = bid & 7, loc = bid >> 3, q8 = nwg >> 3, r8 = nwg & 7;
+        id = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + loc;
+    }
+    const int qb = id % nqb, h = (id / nqb) % a.H, b = id / (nqb * a.H);
+    const int T = a.T, D = a.H * HD;
+    const bf16* base = a.qkv + (long)b * T * a.ld;
+    const int qw0 = qb * QB + wave * 32;
+    const int Tk = a.seq_lens ? a.seq_lens[b] : T;
+    const float c = a.scale_log2;
+
+    // the ones plane (V plane 9) in both ring slots
+    for (int i = tid; i < 2 * 64; i += NW * 64)
+        *reinterpret_cast<u16x8*>(lds + (i >> 6) * TILE + (2 * NCHL) * 1024 + (i & 63) * 16) =
+            u16x8{0x3F80, 0x3F80, 0x3F80, 0x3F80, 0x3F80, 0x3F80, 0x3F80, 0x3F80};
+
+    bf16x8 qf[NKS];  // B operand of QK^T: Q^T[d = 16 ks + 8 hh + j][query r]
+    {
+        const bf16* qrow = base + (long)min(qw0 + r, T - 1) * a.ld + h * HD;
+#pragma unroll
+        for (int ks = 0; ks < NKS; ++ks) {
+            const int col = ks * 16 + 8 * hh;
+            if (col < HD)
+                qf[ks] = *reinterpret_cast<const bf16x8*>(qrow + col);
+            else
+                qf[ks] = bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
+        }
+    }
+
+    int nkt = (Tk + 63) / 64;
+    if (a.causal) nkt = min(nkt, (min(T, qb * QB + QB) + 63) / 64);
+
+    auto vslot = [](int key, int plane) { return key ^ (4 * ((key >> 4) & 1) + 8 * (plane & 1)); };
+    auto issue = [&](int t) {
+        char* tb = lds + (t & 1) * TILE;
+#pragma unroll
+        for (int i = 0; i < MAXI; ++i) {
+            const int idx = wave + NW * i;
+            if (i < MAXI - 1 || idx < NINS) {
+                const bool isV = idx >= NCHL;
+                const int plane = isV ? idx - NCHL : idx;
+                const int key = isV ? vslot(lane, plane) : lane;  // slot lane holds this key (involution)
+                const bf16* src = base + (long)min(t * 64 + key, T - 1) * a.ld + (isV ? 2 : 1) * D + h * HD + plane * 8;
+                glds16(src, tb + idx * 1024);
+            }
+        }
+    };
+
+    const unsigned lds0 = (unsigned)(uintptr_t)(LDS_AS char*)lds;
+    const unsigned kb0 = lds0 + hh * 1024 + r * 16;  // K fragment: plane 2 ks + hh, key 32 kb + r
+    unsigned vbj[2];
+    {
+        const int q = li >> 2, p = li & 3, pc = p >> 1;
+        const int bg = 16 * (g & 1) + 4 * (g >> 1);
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+            vbj[j] = lds0 + (NCHL + pc) * 1024 + vslot(bg + 8 * j + q, pc) * 16 + (p & 1) * 8;
+    }
+
+    f32x4 o[2][NDT];
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+#pragma unroll
+        for (int i = 0; i < NDT; ++i) o[u][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+    float m = -1e30f;
+
+    auto tile_step = [&](int t, const unsigned so) __attribute__((always_inline)) {
+        f32x16 sc[2];
+#pragma unroll
+        for (int kb = 0; kb < 2; ++kb) {
+            f32x16 z;
+#pragma unroll
+            for (int e = 0; e < 16; ++e) z[e] = 0.f;
+#pragma unroll
+            for (int ks = 0; ks < NKS; ++ks) {
+                const bf16x8 kf = *reinterpret_cast<const LDS_AS bf16x8*>((uintptr_t)(kb0 + so + kb * 512 + ks * 2048));
+                z = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[ks], z, 0, 0, 0);
+            }
+            sc[kb] = z;
+        }
+        if ((t * 64 + 64 > Tk) || (a.causal && t * 64 + 63 > qw0)) {
+            const int q = qw0 + r;
+            const int lim = a.causal ? min(Tk, q + 1) : Tk;
+#pragma unroll
+            for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+                for (int e = 0; e < 16; ++e)
+                    if (t * 64 + kb * 32 + (e & 3) + 8 * (e >> 2) + 4 * hh >= lim) sc[kb][e] = -INFINITY;
+        }
+        float mloc = fmaxf(sc[0][0], sc[0][1]);
+#pragma unroll
+        for (int e = 2; e < 16; ++e) mloc = fmaxf(mloc, sc[0][e]);
+#pragma unroll
+        for (int e = 0; e < 16; ++e) mloc = fmaxf(mloc, sc[1][e]);
+        mloc = xmax32(mloc);
+        const float mnew = fmaxf(m, mloc);
+        if (__builtin_amdgcn_ballot_w64(mnew != m)) {
+            const float alpha = __builtin_amdgcn_exp2f((m - mnew) * c);  // of query r
+#pragma unroll
+            for (int u = 0; u < 2; ++u) {
+                const float au = __shfl(alpha, 16 * u + li, 64);  // O^T lanes hold query 16 u + li
+#pragma unroll
+                for (int i = 0; i < NDT; ++i) o[u][i] *= au;
+            }
+        }
+        m = mnew;
+        const float mc = mnew * c;
+#pragma unroll
+        for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+            for (int e = 0; e < 16; ++e) sc[kb][e] = __builtin_amdgcn_exp2f(sc[kb][e] * c - mc);
+#pragma unroll
+        for (int kb = 0; kb < 2; ++kb) {
+            // packed bf16 pairs: x = registers 0..7, y = 8..15 of key block kb
+            unsigned xw[4], yw[4];
+#pragma unroll
+            for (int w = 0; w < 4; ++w) {
+                bf16x2_t px = {f2bf(sc[kb][2 * w]), f2bf(sc[kb][2 * w + 1])};
+                bf16x2_t py = {f2bf(sc[kb][8 + 2 * w]), f2bf(sc[kb][8 + 2 * w + 1])};
+                xw[w] = __builtin_bit_cast(unsigned, px);
+                yw[w] = __builtin_bit_cast(unsigned, py);
+            }
+            unsigned b0w[4], b1w[4];
+#pragma unroll
+            for (int w = 0; w < 4; ++w) {
+                const auto sw = __builtin_amdgcn_permlane16_swap(xw[w], yw[w], false, false);
+                b0w[w] = sw[0];  // queries 0..15
+                b1w[w] = sw[1];  // queries 16..31
+            }
+            const bf16x8 pb0 = __builtin_bit_cast(bf16x8, make_uint4(b0w[0], b0w[1], b0w[2], b0w[3]));
+            const bf16x8 pb1 = __builtin_bit_cast(bf16x8, make_uint4(b1w[0], b1w[1], b1w[2], b1w[3]));
+#pragma unroll
+            for (int dt = 0; dt < NDT; ++dt) {
+                const unsigned off = so + kb * 512 + dt * 2048;
+                const s16x4 v0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS_AS s16x4*)(uintptr_t)(vbj[0] + off));
+                const s16x4 v1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS_AS s16x4*)(uintptr_t)(vbj[1] + off));
+                const bf16x8 vv = __builtin_bit_cast(bf16x8, __builtin_shufflevector(v0, v1, 0, 1, 2, 3, 4, 5, 6, 7));
+                o[0][dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vv, pb0, o[0][dt], 0, 0, 0);
+                o[1][dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vv, pb1, o[1][dt], 0, 0, 0);
+            }
+        }
+    };
+
+    if (PRIO && wave >= NW / 2) __builtin_amdgcn_s_setprio(1);
+    if (nkt > 0) issue(0);
+    for (int t = 0; t < nkt; t += 2) {
+        vm_wait<0>();
+        __builtin_amdgcn_s_barrier();
+        if (t + 1 < nkt) issue(t + 1);
+        tile_step(t, 0);
+        if (t + 1 < nkt) {
+            vm_wait<0>();
+            __builtin_amdgcn_s_barrier();
+            if (t + 2 < nkt) issue(t + 2);
+            tile_step(t + 1, TILE);
+        }
+    }
+
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+        // O^T row 72 = d-tile 4, rows 4 g + reg with g = 2, reg = 0: lanes 32..47 hold the sums
+        const float ltot = __shfl(o[u][NDT - 1][0], 32 + li, 64);
+        const float inv = 1.0f / ltot;
+        const int q = qw0 + 16 * u + li;
+        if (q < T) {
+            bf16* orow = a.out + ((long)b * T + q) * a.ldo + h * HD;
+#pragma unroll
+            for (int dt = 0; dt < NDT; ++dt) {
+                const int d0 = dt * 16 + 4 * g;
+                if (d0 < HD) {
+                    bf16x4 v;
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) v[e] = f2bf(o[u][dt][e] * inv);
+                    *reinterpret_cast<bf16x4*>(orow + d0) = v;
+                }
+            }
+        }
+    }
+}
+
 // SigLIP MAP head: one probe query per head, keys = the T tokens of image b.
 constexpr int PROBE_MAXT = 1024;
 __global__ __launch_bounds__(256) void probe_attn_kernel(const bf16* __restrict__ qv, const bf16* __restrict__ kv,
@@ -2021,7 +2240,19 @@ void launch_attn(int kind, const AttnArgs& a, int B, int T, int H, hipStream_t s
         hipLaunchKernelGGL((attn_m32_kernel<HD, 8, 4, true, false, true>), dim3(cdiv(T, 256) * H * B), dim3(512), 0, st, a);
     else if (kind == 57)  // dev: PF, 9 waves, 3 waves / SIMD
         hipLaunchKernelGGL((attn_m32_kernel<HD, 9, 3, true, false, true>), dim3(cdiv(T, 288) * H * B), dim3(576), 0, st, a);
-    else if (kind == 12)  // dev: pipelined + lazy + ones
+    else if (kind == 58 || kind == 59 || kind == 60) {  // attn_hyb_kernel (hd 72 only; other head dims: kind 38);
+                                                        // kind 58 is production for hd 72
+        if constexpr (HD == 72) {
+            if (kind == 58)  // 4 waves / SIMD (<= 128 VGPRs)
+                hipLaunchKernelGGL((attn_hyb_kernel<8, 4, true>), dim3(cdiv(T, 256) * H * B), dim3(512), 0, st, a);
+            else if (kind == 59)  // 12 waves, 3 waves / SIMD
+                hipLaunchKernelGGL((attn_hyb_kernel<12, 1, true>), dim3(cdiv(T, 384) * H * B), dim3(768), 0, st, a);
+            else  // 8 waves, no register cap (129 VGPRs: 3 waves / SIMD)
+                hipLaunchKernelGGL((attn_hyb_kernel<8, 1, true>), dim3(cdiv(T, 256) * H * B), dim3(512), 0, st, a);
+        } else {
+            hipLaunchKernelGGL((attn_m32_kernel<HD, 8, 1, true>), dim3(cdiv(T, 256) * H * B), dim3(512), 0, st, a);
+        }
+    } else if (kind == 12)  // dev: pipelined + lazy + ones
         hipLaunchKernelGGL((attn_pipe_kernel<HD, 8, 3, true, HD == 72, true>), dim3(cdiv(T, 256) * H * B), dim3(512), 0, st, a);
     else
         hipLaunchKernelGGL((attn_dma_kernel<HD, 8, 2>), dim3(cdiv(T, 256) * H * B), dim3(512), 0, st, a);
@@ -2074,13 +2305,16 @@ extern "C" int mme_attention(const void* qkv, int ld_qkv, void* out, int ld_out,
     // sums from a ones plane): DFN5B (T 730) 632 -> 700-723 TF/s with 8-wave blocks, ViT-H (T 257)
     // 308-317 -> 349 TF/s with 9-wave blocks (profiles/r02_attn_m32_bench.log). At head dim 72 it
     // measures level with kind 30 (635-645 vs 604-638) and at 64 slower than kind 0: not dispatched.
+    // Head dim 72 since round 2: attn_hyb_kernel (kind 58: QK^T on 32x32x16 80 deep, PV on 16x16x32
+    // 80 rows -- 9 % less MFMA work than either single-shape form under the power cap): SigLIP
+    // vision level to 2 % faster than kind 30 (profiles/r02_attn_hyb_bench.log, r02_hyb_attn.log).
     int kind = T <= 64 ? 16
                : (T <= 128 || hd == 64) ? 0
                : (hd == 80 && pad9 * 10 < min(pad8, pad4) * 9) ? 41
                : hd == 80 && pad8 * 10 <= pad4 * 11 ? 38
                : pad9 * 10 < min(pad8, pad4) * 9 ? 35
                : (hd == 80 && pad12 <= pad8 && pad12 * 10 <= pad4 * 11) ? 23
-               : (pad8 * 10 <= pad4 * 11 ? (hd == 72 ? 30 : 11) : 14);
+               : (pad8 * 10 <= pad4 * 11 ? (hd == 72 ? 58 : 11) : 14);
     if (g_attn_variant >= 1 && g_attn_variant <= 4 && hd == 72) {  // dev-only diagnostic builds
         const dim3 grid(cdiv(T, 128) * H * B);
         switch (g_attn_variant) {
