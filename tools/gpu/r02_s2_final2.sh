@@ -1,0 +1,8 @@
+set -o pipefail
+export PYTHONUNBUFFERED=1
+export TMPDIR=/tmp
+mkdir -p gpurun_out
+rm -rf gpurun_out/prof gpurun_out/pmc
+timeout -k 10 600 python -u bench.py > gpurun_out/r02_s2g_bench.log 2>&1 && \
+PROF_TIMEOUT=500 bash tools/profile_bench.sh > gpurun_out/r02_s2g_prof.log 2>&1 && \
+PMC_TIMEOUT=400 bash tools/pmc_gemm.sh > gpurun_out/r02_s2g_pmc.log 2>&1
