@@ -156,6 +156,36 @@ def test_attention_m32(cuda, kind, B, T, H, hd, causal, lens):
     torch.testing.assert_close(out.float(), ref, atol=2e-2, rtol=2e-2)
 
 
+def test_attention_hd72_production_grid_vs_kind30(cuda):
+    """The production hd-72 kernel (attn_hyb_kernel, kind 58) over the bench's full launch grid
+    (239 images x 16 heads x 3 query blocks of SigLIP vision) against the previous production
+    kernel (kind 30, 16x16x32 throughout): the two differ only in MFMA shape and summation
+    order, so every output agrees within a few bf16 ulps (the fp32 reference comparison of
+    both is test_attention / test_attention_m32 at smaller batches)."""
+    B, T, H, hd = 239, 729, 16, 72
+    g = torch.Generator(device="cuda").manual_seed(729)
+    qkv = rnd(B * T, 3 * H * hd, scale=1.5, gen=g)
+    lib = _lib.load()
+    outs = {}
+    for kind in (0, 30):
+        lib.mme_attention_variant(0 if kind == 0 else 30 + kind)
+        try:
+            outs[kind] = ops.attention(qkv, B, T, H, hd).float()
+            torch.cuda.synchronize()
+        finally:
+            lib.mme_attention_variant(0)
+    diff = (outs[0] - outs[30]).abs()
+    print(f"hd-72 production grid: max |diff| {diff.max().item():.3g}, mean {diff.mean().item():.3g}")
+    assert torch.isfinite(outs[0]).all()
+    # bf16(p) may round differently where the two fp32 score sums straddle a rounding boundary
+    # (an error on the scale of |v|, not of the output, which can be a cancellation): the same
+    # absolute bound as the fp32-reference tests, and almost every output bit-identical
+    frac = (diff > 0).float().mean().item()
+    print(f"hd-72 production grid: outputs differing {frac:.2e}")
+    assert diff.max().item() <= 2e-2, "hd-72 kernels disagree beyond the fp32-reference tolerance"
+    assert diff.mean().item() < 1e-5 and frac < 1e-3
+
+
 def test_attention_strided_qkv(cuda):
     B, T, H, hd = 2, 100, 16, 72
     g = torch.Generator(device="cuda").manual_seed(9)
