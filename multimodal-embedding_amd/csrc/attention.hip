@@ -1841,13 +1841,14 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(2))) vo
 //   O^T (16x16 tiles): lane l holds query 16 u + (l & 15), rows 4 g + reg of each d-tile;
 //   the running max lives with the S^T lanes, so the (lazy) rescale shuffles alpha over.
 // ---------------------------------------------------------------------------
-template <int NW, int MINW, bool PRIO>
+template <int HD, int NW, int MINW, bool PRIO>
 __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(MINW))) void attn_hyb_kernel(AttnArgs a) {
-    constexpr int HD = 72;
-    constexpr int NCHL = HD / 8;  // 9 K / V planes with data
-    constexpr int NKS = 5;        // QK^T k-steps of 16 (80 deep)
-    constexpr int NDT = 5;        // PV d-tiles of 16 (80 rows; row 72 = weight sums)
-    constexpr int NVP = 2 * NDT;  // V planes read: 9 data + the ones plane
+    static_assert(HD == 72 || HD == 80, "80-deep QK^T, 80 PV rows");
+    constexpr bool ONES = HD == 72;  // hd 72: V^T row 72 = ones (weight sums); hd 80: f32 sums
+    constexpr int NCHL = HD / 8;     // K / V planes with data
+    constexpr int NKS = 5;           // QK^T k-steps of 16 (80 deep)
+    constexpr int NDT = 5;           // PV d-tiles of 16 (80 rows)
+    constexpr int NVP = 2 * NDT;     // V planes read: data (+ the ones plane at hd 72)
     constexpr int TILE = (NCHL + NVP) * 1024;
     constexpr int NINS = 2 * NCHL;
     constexpr int MAXI = (NINS + NW - 1) / NW;
@@ -1874,10 +1875,11 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(MINW)))
     const int Tk = a.seq_lens ? a.seq_lens[b] : T;
     const float c = a.scale_log2;
 
-    // the ones plane (V plane 9) in both ring slots
-    for (int i = tid; i < 2 * 64; i += NW * 64)
-        *reinterpret_cast<u16x8*>(lds + (i >> 6) * TILE + (2 * NCHL) * 1024 + (i & 63) * 16) =
-            u16x8{0x3F80, 0x3F80, 0x3F80, 0x3F80, 0x3F80, 0x3F80, 0x3F80, 0x3F80};
+    // the ones plane (V plane 9 at hd 72) in both ring slots
+    if (ONES)
+        for (int i = tid; i < 2 * 64; i += NW * 64)
+            *reinterpret_cast<u16x8*>(lds + (i >> 6) * TILE + (2 * NCHL) * 1024 + (i & 63) * 16) =
+                u16x8{0x3F80, 0x3F80, 0x3F80, 0x3F80, 0x3F80, 0x3F80, 0x3F80, 0x3F80};
 
     bf16x8 qf[NKS];  // B operand of QK^T: Q^T[d = 16 ks + 8 hh + j][query r]
     {
@@ -1927,7 +1929,7 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(MINW)))
     for (int u = 0; u < 2; ++u)
 #pragma unroll
         for (int i = 0; i < NDT; ++i) o[u][i] = f32x4{0.f, 0.f, 0.f, 0.f};
-    float m = -1e30f;
+    float m = -1e30f, lsum = 0.f;  // lsum (hd 80): this lane's share of query r's weight sum
 
     auto tile_step = [&](int t, const unsigned so) __attribute__((always_inline)) {
         f32x16 sc[2];
@@ -1961,6 +1963,7 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(MINW)))
         const float mnew = fmaxf(m, mloc);
         if (__builtin_amdgcn_ballot_w64(mnew != m)) {
             const float alpha = __builtin_amdgcn_exp2f((m - mnew) * c);  // of query r
+            if (!ONES) lsum *= alpha;
 #pragma unroll
             for (int u = 0; u < 2; ++u) {
                 const float au = __shfl(alpha, 16 * u + li, 64);  // O^T lanes hold query 16 u + li
@@ -1970,10 +1973,15 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(MINW)))
         }
         m = mnew;
         const float mc = mnew * c;
+        float psum = 0.f;
 #pragma unroll
         for (int kb = 0; kb < 2; ++kb)
 #pragma unroll
-            for (int e = 0; e < 16; ++e) sc[kb][e] = __builtin_amdgcn_exp2f(sc[kb][e] * c - mc);
+            for (int e = 0; e < 16; ++e) {
+                sc[kb][e] = __builtin_amdgcn_exp2f(sc[kb][e] * c - mc);
+                if (!ONES) psum += sc[kb][e];
+            }
+        if (!ONES) lsum += psum;
 #pragma unroll
         for (int kb = 0; kb < 2; ++kb) {
             // packed bf16 pairs: x = registers 0..7, y = 8..15 of key block kb
@@ -2021,10 +2029,12 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(MINW)))
         }
     }
 
+    const float lq = ONES ? 0.f : xsum32(lsum);  // hd 80: query r's weight sum (S^T lanes)
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
-        // O^T row 72 = d-tile 4, rows 4 g + reg with g = 2, reg = 0: lanes 32..47 hold the sums
-        const float ltot = __shfl(o[u][NDT - 1][0], 32 + li, 64);
+        // hd 72: O^T row 72 = d-tile 4, rows 4 g + reg with g = 2, reg = 0: lanes 32..47 hold the
+        // sums; hd 80: from the S^T lane of query 16 u + li
+        const float ltot = ONES ? __shfl(o[u][NDT - 1][0], 32 + li, 64) : __shfl(lq, 16 * u + li, 64);
         const float inv = 1.0f / ltot;
         const int q = qw0 + 16 * u + li;
         if (q < T) {
@@ -2240,15 +2250,17 @@ void launch_attn(int kind, const AttnArgs& a, int B, int T, int H, hipStream_t s
         hipLaunchKernelGGL((attn_m32_kernel<HD, 8, 4, true, false, true>), dim3(cdiv(T, 256) * H * B), dim3(512), 0, st, a);
     else if (kind == 57)  // dev: PF, 9 waves, 3 waves / SIMD
         hipLaunchKernelGGL((attn_m32_kernel<HD, 9, 3, true, false, true>), dim3(cdiv(T, 288) * H * B), dim3(576), 0, st, a);
-    else if (kind == 58 || kind == 59 || kind == 60) {  // attn_hyb_kernel (hd 72 only; other head dims: kind 38);
-                                                        // kind 58 is production for hd 72
-        if constexpr (HD == 72) {
+    else if (kind == 58 || kind == 59 || kind == 60 || kind == 61) {  // attn_hyb_kernel (hd 72 / 80; hd 64: kind 38);
+                                                                      // kind 58 is production for hd 72
+        if constexpr (HD != 64) {
             if (kind == 58)  // 4 waves / SIMD (<= 128 VGPRs)
-                hipLaunchKernelGGL((attn_hyb_kernel<8, 4, true>), dim3(cdiv(T, 256) * H * B), dim3(512), 0, st, a);
+                hipLaunchKernelGGL((attn_hyb_kernel<HD, 8, 4, true>), dim3(cdiv(T, 256) * H * B), dim3(512), 0, st, a);
             else if (kind == 59)  // 12 waves, 3 waves / SIMD
-                hipLaunchKernelGGL((attn_hyb_kernel<12, 1, true>), dim3(cdiv(T, 384) * H * B), dim3(768), 0, st, a);
-            else  // 8 waves, no register cap (129 VGPRs: 3 waves / SIMD)
-                hipLaunchKernelGGL((attn_hyb_kernel<8, 1, true>), dim3(cdiv(T, 256) * H * B), dim3(512), 0, st, a);
+                hipLaunchKernelGGL((attn_hyb_kernel<HD, 12, 1, true>), dim3(cdiv(T, 384) * H * B), dim3(768), 0, st, a);
+            else if (kind == 60)  // 8 waves, no register cap (129 VGPRs: 3 waves / SIMD)
+                hipLaunchKernelGGL((attn_hyb_kernel<HD, 8, 1, true>), dim3(cdiv(T, 256) * H * B), dim3(512), 0, st, a);
+            else  // 9 waves (288 queries: T = 257 in one block per batch-head)
+                hipLaunchKernelGGL((attn_hyb_kernel<HD, 9, 1, true>), dim3(cdiv(T, 288) * H * B), dim3(576), 0, st, a);
         } else {
             hipLaunchKernelGGL((attn_m32_kernel<HD, 8, 1, true>), dim3(cdiv(T, 256) * H * B), dim3(512), 0, st, a);
         }
