@@ -1841,7 +1841,7 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(2))) vo
 //   O^T (16x16 tiles): lane l holds query 16 u + (l & 15), rows 4 g + reg of each d-tile;
 //   the running max lives with the S^T lanes, so the (lazy) rescale shuffles alpha over.
 // ---------------------------------------------------------------------------
-template <int HD, int NW, int MINW, bool PRIO>
+template <int HD, int NW, int MINW, bool PRIO, bool SKIP = false>
 __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(MINW))) void attn_hyb_kernel(AttnArgs a) {
     static_assert(HD == 72 || HD == 80, "80-deep QK^T, 80 PV rows");
     constexpr bool ONES = HD == 72;  // hd 72: V^T row 72 = ones (weight sums); hd 80: f32 sums
@@ -1932,12 +1932,19 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(MINW)))
     float m = -1e30f, lsum = 0.f;  // lsum (hd 80): this lane's share of query r's weight sum
 
     auto tile_step = [&](int t, const unsigned so) __attribute__((always_inline)) {
+        // SKIP (dev): a tile whose second 32-key block lies wholly past the keys (the last tile
+        // at T = 729) skips that block's QK^T and PV MFMAs; its P is 0 either way (bit-identical)
+        const bool half = SKIP && t * 64 + 32 >= Tk;
         f32x16 sc[2];
 #pragma unroll
         for (int kb = 0; kb < 2; ++kb) {
             f32x16 z;
 #pragma unroll
-            for (int e = 0; e < 16; ++e) z[e] = 0.f;
+            for (int e = 0; e < 16; ++e) z[e] = kb == 1 && half ? -INFINITY : 0.f;
+            if (kb == 1 && half) {
+                sc[kb] = z;
+                continue;
+            }
 #pragma unroll
             for (int ks = 0; ks < NKS; ++ks) {
                 const bf16x8 kf = *reinterpret_cast<const LDS_AS bf16x8*>((uintptr_t)(kb0 + so + kb * 512 + ks * 2048));
@@ -1984,6 +1991,7 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(MINW)))
         if (!ONES) lsum += psum;
 #pragma unroll
         for (int kb = 0; kb < 2; ++kb) {
+            if (kb == 1 && half) break;
             // packed bf16 pairs: x = registers 0..7, y = 8..15 of key block kb
             unsigned xw[4], yw[4];
 #pragma unroll
@@ -2264,6 +2272,12 @@ void launch_attn(int kind, const AttnArgs& a, int B, int T, int H, hipStream_t s
         } else {
             hipLaunchKernelGGL((attn_m32_kernel<HD, 8, 1, true>), dim3(cdiv(T, 256) * H * B), dim3(512), 0, st, a);
         }
+    } else if (kind == 62) {  // kind 58 skipping a tile's second key block when it lies past the keys: production for hd 72
+        if constexpr (HD != 64) {
+            hipLaunchKernelGGL((attn_hyb_kernel<HD, 8, 4, true, true>), dim3(cdiv(T, 256) * H * B), dim3(512), 0, st, a);
+        } else {
+            hipLaunchKernelGGL((attn_m32_kernel<HD, 8, 1, true>), dim3(cdiv(T, 256) * H * B), dim3(512), 0, st, a);
+        }
     } else if (kind == 12)  // dev: pipelined + lazy + ones
         hipLaunchKernelGGL((attn_pipe_kernel<HD, 8, 3, true, HD == 72, true>), dim3(cdiv(T, 256) * H * B), dim3(512), 0, st, a);
     else
@@ -2319,14 +2333,16 @@ extern "C" int mme_attention(const void* qkv, int ld_qkv, void* out, int ld_out,
     // measures level with kind 30 (635-645 vs 604-638) and at 64 slower than kind 0: not dispatched.
     // Head dim 72 since round 2: attn_hyb_kernel (kind 58: QK^T on 32x32x16 80 deep, PV on 16x16x32
     // 80 rows -- 9 % less MFMA work than either single-shape form under the power cap): SigLIP
-    // vision level to 2 % faster than kind 30 (profiles/r02_attn_hyb_bench.log, r02_hyb_attn.log).
+    // vision level to 2 % faster than kind 30 (profiles/r02_attn_hyb_bench.log, r02_hyb_attn.log);
+    // kind 62 = kind 58 skipping the last tile's second 32-key block (wholly past T = 729): +1.2 %
+    // (profiles/r02_hyb_skip_bench.log, 4 of 4 A/B pairs).
     int kind = T <= 64 ? 16
                : (T <= 128 || hd == 64) ? 0
                : (hd == 80 && pad9 * 10 < min(pad8, pad4) * 9) ? 41
                : hd == 80 && pad8 * 10 <= pad4 * 11 ? 38
                : pad9 * 10 < min(pad8, pad4) * 9 ? 35
                : (hd == 80 && pad12 <= pad8 && pad12 * 10 <= pad4 * 11) ? 23
-               : (pad8 * 10 <= pad4 * 11 ? (hd == 72 ? 58 : 11) : 14);
+               : (pad8 * 10 <= pad4 * 11 ? (hd == 72 ? 62 : 11) : 14);
     if (g_attn_variant >= 1 && g_attn_variant <= 4 && hd == 72) {  // dev-only diagnostic builds
         const dim3 grid(cdiv(T, 128) * H * B);
         switch (g_attn_variant) {

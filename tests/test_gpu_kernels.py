@@ -129,7 +129,7 @@ def test_attention(cuda, B, T, H, hd, causal, lens):
     torch.testing.assert_close(out.float(), ref, atol=2e-2, rtol=2e-2)
 
 
-@pytest.mark.parametrize("kind", [38, 39, 40, 41, 42, 43, 44, 45, 46, 47, 48, 49, 50, 51, 52, 54, 55, 56, 57, 58, 59, 60, 61])
+@pytest.mark.parametrize("kind", [38, 39, 40, 41, 42, 43, 44, 45, 46, 47, 48, 49, 50, 51, 52, 54, 55, 56, 57, 58, 59, 60, 61, 62])
 @pytest.mark.parametrize("B,T,H,hd,causal,lens", [
     (2, 729, 4, 72, False, None),       # SigLIP vision geometry
     (2, 520, 3, 72, False, [520, 301]),  # key padding, partial last tile
