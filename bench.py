@@ -42,7 +42,8 @@ HBM_PEAK_GBS = 8000.0
 
 def parse():
     p = argparse.ArgumentParser()
-    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--gpus", type=int, default=None,
+                   help="ranks (default: the launcher's WORLD_SIZE under torchrun, else 1)")
     p.add_argument("--steps", type=int, default=2)
     p.add_argument("--warmup", type=int, default=1)
     p.add_argument("--model", default="SigLIP-400M")
@@ -150,13 +151,14 @@ def retrieval_parity(tables, metrics, caps_per_image: int = 5):
     ref_metrics = {}
     for name, qk, dk, tc in (("T2I", "t2i", "img", 1), ("I2T", "img", "all", caps_per_image),
                              ("I2T_Sym", "img", "t2i", 1)):
-        idx, _ = ops.sim_topk(tables[qk].contiguous(), tables[dk].contiguous(), 10)
-        ridx, rsc = R.topk(R.scores(host[qk], host[dk]), 11)
+        k = min(10, host[dk].shape[0])  # the reference clamps k to the column count (main.py:335)
+        idx, _ = ops.sim_topk(tables[qk].contiguous(), tables[dk].contiguous(), k)
+        ridx, rsc = R.topk(R.scores(host[qk], host[dk]), k + 1)
         same, near = R.compare_topk(idx.cpu().numpy(), ridx, rsc)
         rows[name] = {"rows_identical": f"{int(same.sum())}/{len(same)}", "near_tie_rows": int(near.sum()),
                       "decisive_rows_differing": int((~same & ~near).sum())}
-        for k, h in zip((1, 5, 10), R.recall(ridx[:, :10], tc)):
-            ref_metrics[f"{name}_R@{k}"] = 100.0 * h / n
+        for kr, h in zip((1, 5, 10), R.recall(ridx[:, :k], tc, [min(x, k) for x in (1, 5, 10)])):
+            ref_metrics[f"{name}_R@{kr}"] = 100.0 * h / n
     return {"recall_identical": all(ref_metrics[k] == metrics[k] for k in ref_metrics),
             "oracle_recall": {k: round(v, 2) for k, v in ref_metrics.items()}, "rows": rows,
             "near_tie_rule": "neighbouring oracle scores among the top 11 within 1e-5*|s1|",
@@ -325,7 +327,9 @@ def main_colpali(args, rank, world, dev):
 def main():
     args = parse()
     from mme import launch
-    if args.gpus > 1 and not launch.under_launcher():
+    if args.gpus is None and not launch.under_launcher():
+        args.gpus = 1
+    if args.gpus is not None and args.gpus > 1 and not launch.under_launcher():
         # `python bench.py --gpus N` without torchrun: start N rank processes of this script
         # BEFORE anything touches the GPU (this parent never initialises HIP), and exit with
         # the first failing rank's status
@@ -336,7 +340,7 @@ def main():
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     try:
-        rank, world, _ = launch.init_distributed(args.gpus, args.backend, dev)
+        rank, world, _ = launch.init_distributed(args.gpus, args.backend, dev, same_device=args.same_device)
     except launch.LaunchError as e:
         print(f"bench.py: {e}", file=sys.stderr, flush=True)
         sys.exit(3)

@@ -1836,7 +1836,7 @@ __global__ __launch_bounds__(256) void row_part_combine_lds_kernel(const float* 
     __shared__ float2 sp[256 * COMBINE_MAXP];
     const int r0 = blockIdx.x * 256;
     const int nr = min(256, rows - r0);
-    const int n4 = nr * nparts / 2;  // float4s of this block's rows (nparts is even: N % 128 == 0 or 2 slices)
+    const int n4 = nr * nparts / 2;  // float4s of this block's rows (nparts even: the dispatcher's np % 2 check)
     const float4* src = reinterpret_cast<const float4*>(part + 2 * (size_t)r0 * nparts);
     float4* dst = reinterpret_cast<float4*>(sp);
     for (int i = threadIdx.x; i < n4; i += 256) dst[i] = src[i];

@@ -16,6 +16,7 @@ requested one.
 from __future__ import annotations
 
 import os
+import signal
 import socket
 import subprocess
 import sys
@@ -56,11 +57,29 @@ def spawn_ranks(nprocs: int, argv: Sequence[str], poll_s: float = 0.2, timeout_s
 
     Children inherit stdout / stderr (rank 0 prints the result line). When a
     rank fails, the remaining ranks are terminated (their exact PIDs) and the
-    first non-zero exit code is returned; 0 when every rank succeeded."""
+    first non-zero exit code is returned; 0 when every rank succeeded. A SIGTERM /
+    SIGHUP / SIGINT to this parent (e.g. a job timeout) terminates the ranks before the
+    parent exits (status 128 + signal), so no rank is orphaned holding its GPU and the
+    rendezvous port."""
     if nprocs < 1:
         raise LaunchError(f"nprocs must be >= 1, got {nprocs}")
     port = free_port()
     procs: List[subprocess.Popen] = []
+
+    class _Signalled(Exception):
+        def __init__(self, signum):
+            super().__init__(signum)
+            self.signum = signum
+
+    def _on_signal(signum, _frame):
+        raise _Signalled(signum)
+
+    old = {}
+    for sig in (signal.SIGTERM, signal.SIGHUP, signal.SIGINT):
+        try:
+            old[sig] = signal.signal(sig, _on_signal)
+        except ValueError:  # not the main thread: keep the default handlers
+            break
     try:
         for r in range(nprocs):
             procs.append(subprocess.Popen([sys.executable, *argv], env=rank_env(r, nprocs, port)))
@@ -79,7 +98,11 @@ def spawn_ranks(nprocs: int, argv: Sequence[str], poll_s: float = 0.2, timeout_s
                 break
             time.sleep(poll_s)
         return rc
+    except _Signalled as e:
+        return 128 + int(e.signum)
     finally:
+        for sig, h in old.items():
+            signal.signal(sig, h)
         for p in procs:
             if p.poll() is None:
                 p.terminate()
@@ -97,14 +120,22 @@ def env_rank_world() -> Tuple[int, int, int]:
             int(os.environ.get("LOCAL_RANK", 0)))
 
 
-def init_distributed(expected_world: int, backend: str = "nccl", device=None) -> Tuple[int, int, int]:
+def init_distributed(expected_world: Optional[int], backend: str = "nccl", device=None,
+                     same_device: bool = False) -> Tuple[int, int, int]:
     """Bring up the process group and check its size against the requested rank count.
 
-    Returns (rank, world, local_rank). world == 1 creates no group. Raises
-    LaunchError if the environment's or the group's size differs from
-    ``expected_world`` (e.g. ``--gpus 8`` started as a single process)."""
+    Returns (rank, world, local_rank). world == 1 creates no group. ``expected_world``
+    None (no explicit ``--gpus``) takes the launcher's WORLD_SIZE, so
+    ``torchrun --nproc-per-node 8 bench.py`` works as before. Raises LaunchError if an
+    explicit ``expected_world`` differs from the environment's or the group's size
+    (e.g. ``--gpus 8`` started as a single process), or if ``same_device`` (every rank
+    on one GPU) is asked of a backend other than gloo (RCCL refuses duplicate GPUs)."""
     import torch.distributed as dist
     rank, world, local = env_rank_world()
+    if expected_world is None:
+        expected_world = world
+    if same_device and world > 1 and backend != "gloo":
+        raise LaunchError(f"--same-device puts every rank on one GPU and needs --backend gloo, got {backend!r}")
     if world != expected_world:
         raise LaunchError(f"requested {expected_world} ranks but WORLD_SIZE={world} (rank {rank})")
     if world == 1:

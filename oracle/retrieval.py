@@ -58,10 +58,12 @@ def compare_topk(idx: np.ndarray, ref_idx: np.ndarray, ref_score: np.ndarray, re
     near-tie when two neighbouring scores among those k+1 differ by <= rel_tol·|s_1|:
     a different fp32 summation order may legitimately swap them ("exact-index
     parity"). Returns (identical [rows] bool, near_tie [rows] bool); every row that is
-    not a near-tie must be identical."""
+    not a near-tie must be identical. With no (k+1)-th reference column (fewer columns than
+    k + 1) only the gaps that exist are compared."""
     k = idx.shape[1]
     same = (idx == ref_idx[:, :k]).all(1)
-    gaps = ref_score[:, :k] - ref_score[:, 1:k + 1]
+    kk = min(k + 1, ref_score.shape[1])
+    gaps = ref_score[:, :kk - 1] - ref_score[:, 1:kk]
     near = (gaps <= rel_tol * np.abs(ref_score[:, :1])).any(1)
     return same, near
 

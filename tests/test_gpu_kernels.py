@@ -269,7 +269,9 @@ def test_gemm_lnfold(cuda, M, N, K, act):
 # and a shifted residual stream (mean >> std: the two-pass slices keep the variance exact).
 @pytest.mark.parametrize("M,N,K,shift", [(4096, 1152, 1152, 0.0), (3000, 1280, 512, 0.0), (100, 256, 64, 0.0),
                                          (2048, 1152, 4352, 40.0),
-                                         (2048, 576, 256, 0.0)])  # N % 256 == 64: partial last column tile
+                                         (2048, 576, 256, 0.0),  # N % 256 == 64: partial last column tile
+                                         (2048, 704, 256, 0.0),  # N % 256 == 192: odd slice count (11)
+                                         (1500, 448, 320, 3.0)])
 def test_gemm_res_stats(cuda, M, N, K, shift):
     g = torch.Generator(device="cuda").manual_seed(M + N + K)
     a = rnd(M, K, gen=g)
@@ -329,7 +331,8 @@ def test_row_part_combine_lds_bit_identical(cuda, M, N, K):
 @pytest.mark.parametrize("M,N,K,epi", [(2048, 1024, 192, "bias"), (1500, 1536, 256, "gelu"),
                                        (4096, 1152, 1152, "res"), (1000, 3456, 1152, "lnfold"),
                                        (1024, 1152, 4352, "bias"), (2048, 4352, 320, "geglu"),
-                                       (3000, 1152, 1152, "resstats"), (3000, 576, 320, "resstats")])
+                                       (3000, 1152, 1152, "resstats"), (3000, 576, 320, "resstats"),
+                                       (2048, 704, 256, "resstats"), (1500, 448, 320, "resstats")])
 def test_gemm_pipe8_bit_identical_to_pipe6(cuda, M, N, K, epi):
     import ctypes
     lib = _lib.load()

@@ -56,3 +56,46 @@ def test_bench_parent_spawns_before_touching_the_gpu(tmp_path):
                         "1", "--warmup", "0"], env=env, capture_output=True, text=True, timeout=300)
     assert r.returncode != 0
     assert '"n_gpus"' not in r.stdout
+
+
+def test_launcher_world_is_the_default(monkeypatch):
+    """torchrun --nproc-per-node N bench.py (no --gpus): the expected size is the launcher's."""
+    monkeypatch.setenv("RANK", "0")
+    monkeypatch.setenv("WORLD_SIZE", "1")
+    assert launch.init_distributed(None, "gloo") == (0, 1, 0)
+
+
+def test_same_device_needs_gloo(monkeypatch):
+    monkeypatch.setenv("RANK", "0")
+    monkeypatch.setenv("WORLD_SIZE", "2")
+    with pytest.raises(launch.LaunchError, match="gloo"):
+        launch.init_distributed(2, "nccl", same_device=True)
+
+
+def test_sigterm_to_the_parent_ends_the_ranks(tmp_path):
+    """A job timeout's SIGTERM to the spawning parent must not orphan the ranks."""
+    import signal
+    import time
+    script = tmp_path / "parent.py"
+    script.write_text(
+        "import sys\n"
+        f"sys.path.insert(0, {os.path.join(os.path.dirname(HERE), 'multimodal-embedding_amd')!r})\n"
+        "from mme import launch\n"
+        "sys.exit(launch.spawn_ranks(2, ['-c', 'import os, time; "
+        f"open(r\"{tmp_path}/pid%s\" % os.environ[\"RANK\"], \"w\").write(str(os.getpid())); time.sleep(300)']))\n")
+    env = {k: v for k, v in os.environ.items() if k not in launch.ENV_KEYS}
+    p = subprocess.Popen([sys.executable, str(script)], env=env)
+    t0 = time.time()
+    while not all((tmp_path / f"pid{r}").exists() for r in range(2)) and time.time() - t0 < 60:
+        time.sleep(0.1)
+    pids = [int((tmp_path / f"pid{r}").read_text()) for r in range(2)]
+    p.send_signal(signal.SIGTERM)
+    assert p.wait(timeout=60) == 128 + signal.SIGTERM
+    for pid in pids:
+        try:
+            os.kill(pid, 0)
+            # a zombie is reaped by its parent, which has exited; /proc shows its state
+            with open(f"/proc/{pid}/status") as f:
+                assert "zombie" in f.read()
+        except ProcessLookupError:
+            pass
