@@ -166,6 +166,69 @@ def retrieval_parity(tables, metrics, caps_per_image: int = 5):
             "seconds": round(time.time() - t0, 2)}
 
 
+def colpali_parity(tables, scores, caps_per_image: int = 5, n_t2i: int = 50, n_i2t: int = 10, n_sym: int = 50):
+    """MaxSim parity of the ColPali job (checker; runs after the timed region): sampled query rows
+    of the job's own multi-vector tables re-scored on the host by the oracle's restatement of the
+    reference's colpali chunk loop (oracle/maxsim.py: pad_sequence + bf16 einsum / max / sum per
+    10-doc chunk, main.py:451-470 -> processor.score), against the device's score rows: scores
+    bit-identical, top-10 columns identical in torch.topk's CPU order (oracle/torch_topk.cpp vs the
+    device's mme_topk_rows_torch; MaxSim sums are bf16-quantised, so exact ties are common) and the
+    rows' hit / miss at k = 1, 5, 10 identical, one selection per k (main.py:331-378). Rows:
+    T2I (caption-0 queries vs all images), I2T (image queries vs all caption docs, each with its
+    batch's left padding), I2T-Sym (= T2I columns: every T2I query against one image)."""
+    import numpy as np
+    sys.path.insert(0, ROOT)
+    from oracle import maxsim as om
+    from oracle import torch_topk as TT
+    from mme import ops
+    t0 = time.time()
+    D, dl, Qt, qtl, qtp, Qa, qal, qap = (tables[k] for k in ("D", "dl", "Qt", "qtl", "qtp", "Qa", "qal", "qap"))
+    n = D.shape[0]
+    dlh, qtlh, qtph, qalh, qaph = (x.cpu().tolist() for x in (dl, qtl, qtp, qal, qap))
+    Dh, Qth, Qah = D.cpu(), Qt.cpu(), Qa.cpu()
+
+    def items(Q, ql, qp):  # per-item [L_b, 128] with its leading zero rows, as encode_data returns them
+        out = []
+        for i in range(Q.shape[0]):
+            e = torch.zeros(qp[i], Q.shape[2], dtype=Q.dtype)
+            e[qp[i] - ql[i]:] = Q[i, : ql[i]]
+            out.append(e)
+        return out
+    img_items = [Dh[i, : dlh[i]] for i in range(n)]
+    t2i_items, cap_items = items(Qth, qtlh, qtph), items(Qah, qalh, qaph)
+    rng = np.random.default_rng(7)
+    out, ok = {}, True
+    for name, m, tc in (("T2I", n_t2i, 1), ("I2T", n_i2t, caps_per_image), ("I2T_Sym", n_sym, 1)):
+        rows = np.sort(rng.choice(n, min(m, n), replace=False))
+        if name == "T2I":
+            ref = om.score_reference_chunks([t2i_items[r] for r in rows], img_items)
+            dev = scores["t2i"][torch.from_numpy(rows).to(scores["t2i"].device)]
+        elif name == "I2T":
+            ref = torch.cat([om.score_reference_chunks([img_items[r]], cap_items) for r in rows])
+            dev = scores["i2t"][torch.from_numpy(rows).to(scores["i2t"].device)]
+        else:
+            ref = torch.cat([om.score_reference_chunks(t2i_items, [img_items[r]]) for r in rows], 1).t()
+            dev = scores["t2i"][:, torch.from_numpy(rows).to(scores["t2i"].device)].t()
+        ref = ref.numpy().astype(np.float32)
+        dev = dev.contiguous()
+        ks = [min(kk, ref.shape[1]) for kk in (1, 5, 10)]
+        didx = {kk: ops.topk_rows_torch(dev, kk)[0].cpu().numpy() for kk in ks}
+        ridx = {kk: TT.topk(ref, kk)[0] for kk in ks}
+        hit = lambda ix: np.stack([(ix[kk] // tc == rows[:, None]).any(1) for kk in ks], 1)
+        dev = dev.cpu().numpy()
+        r = {"rows_sampled": int(len(rows)), "scores_identical": int((dev == ref).all(1).sum()),
+             "top10_identical": int((didx[ks[-1]] == ridx[ks[-1]]).all(1).sum()),
+             "hit_rows_identical": int((hit(didx) == hit(ridx)).all(1).sum())}
+        ok &= r["scores_identical"] == r["top10_identical"] == r["hit_rows_identical"] == len(rows)
+        out[name] = r
+    return {"sampled_rows_identical": bool(ok), "rows": out,
+            "rule": "scores bit-identical; top-10 in torch.topk's CPU order; hit/miss at k = 1, 5, 10",
+            "checker": "oracle/maxsim.py chunk loop (reference main.py:451-470) on the job's own multi-vectors, host",
+            "full_geometry_pin": "tests/test_gpu_colpali.py::test_colpali_full_geometry_vs_reference "
+                                 "(1 000 x 5 000 vs the reference's own scores and recall)",
+            "seconds": round(time.time() - t0, 2)}
+
+
 def colpali_captions(n: int, caps: int, seed: int = 1):
     """Synthetic caption token lists for the ColPali job: 8..14 ids each, so a query is
     1 + 3 + len + 10 + 1 = 23..29 tokens (Tq ~ 26)."""
@@ -175,9 +238,11 @@ def colpali_captions(n: int, caps: int, seed: int = 1):
     return [rng.integers(3, 250000, int(L)).tolist() for L in lens]
 
 
-def cpu_baseline_colpali(spec, seconds: float):
+def cpu_baseline_colpali(spec, seconds: float, n: int = 1000, caps: int = 5):
     """oracle/colpali_encoder.py (bf16 PyTorch-CPU) on a bounded sample: images and
-    queries timed separately, extrapolated to n images + 6n queries."""
+    queries timed separately, extrapolated to n images + 6n queries; plus the reference's
+    MaxSim chunk loop (oracle/maxsim.py, 10 x 10 chunks, main.py:451-470) timed on sample
+    chunks of the job's shapes and extrapolated to its (n/10)^2 T2I + (n/10)(5n/10) I2T calls."""
     import numpy as np
     from oracle import colpali_encoder as oc
     from oracle import pil_bicubic
@@ -214,10 +279,24 @@ def cpu_baseline_colpali(spec, seconds: float):
         enc_q(caps[nc:nc + 4])
         nc += 4
     tc = time.time() - t0
-    per_img = ti / ni + 6.0 * tc / nc
+    from oracle import maxsim as om
+    g = torch.Generator().manual_seed(0)
+    docs = [torch.randn(len(spec.image_tokens), 128, generator=g).to(torch.bfloat16) for _ in range(10)]
+    qs = [torch.randn(26, 128, generator=g).to(torch.bfloat16) for _ in range(10)]
+    om.score_chunk(qs, docs)
+    t0, nm = time.time(), 0
+    while nm == 0 or time.time() - t0 < seconds * 0.1:
+        om.score_chunk(qs, docs)      # T2I chunk: 10 caption queries x 10 image docs
+        om.score_chunk(docs, qs)      # I2T chunk: 10 image queries x 10 caption docs
+        nm += 1
+    tm = (time.time() - t0) / nm / 2
+    calls = (n // 10) ** 2 + (n // 10) * (caps * n // 10)
+    per_img = ti / ni + 6.0 * tc / nc + tm * calls / n
     return {"value": round(1.0 / per_img, 5), "unit": "images/sec", "cores": threads, "kind": "port",
             "sample": f"oracle/colpali_encoder.py bf16 CPU: {ni} images in {ti:.1f}s + {nc} queries (bs 4) in "
-                      f"{tc:.1f}s, extrapolated to n images + 6n queries (MaxSim excluded)"}
+                      f"{tc:.1f}s, extrapolated to n images + 6n queries; + the reference's MaxSim chunk loop "
+                      f"(oracle/maxsim.py) {tm * 1e3:.1f} ms per 10 x 10 chunk x {calls} calls",
+            "maxsim_s": round(tm * calls, 2)}
 
 
 def main_colpali(args, rank, world, dev):
@@ -240,6 +319,7 @@ def main_colpali(args, rank, world, dev):
     my_t2i = my_caps[::caps]
     del imgs
     ev = {}
+    last = {}
 
     def mark(name):
         e = torch.cuda.Event(enable_timing=True)
@@ -253,11 +333,12 @@ def main_colpali(args, rank, world, dev):
         Dp = torch.zeros(D.shape[0], -(-D.shape[1] // 16) * 16, D.shape[2], dtype=D.dtype, device=dev)
         Dp[:, : D.shape[1]] = D
         mark("img")
-        Qt, qtl, _ = model.encode_queries(my_t2i, exec_batch=args.txt_batch, width=width)
+        Qt, qtl, qtp = model.encode_queries(my_t2i, exec_batch=args.txt_batch, width=width)
         Qa, qal, qap = model.encode_queries(my_caps, exec_batch=args.txt_batch, width=width)
         mark("txt")
-        m = sharded_colpali_recall(Dp, dl, Qt, qtl, Qa, qal, qap, rank, world, n, caps)
+        m, sc = sharded_colpali_recall(Dp, dl, Qt, qtl, Qa, qal, qap, rank, world, n, caps, return_scores=True)
         mark("score")
+        last.update(tables=dict(D=Dp, dl=dl, Qt=Qt, qtl=qtl, qtp=qtp, Qa=Qa, qal=qal, qap=qap), scores=sc)
         return m
 
     for _ in range(args.warmup):
@@ -311,13 +392,15 @@ def main_colpali(args, rank, world, dev):
                    "global_batch": n, "parallelism": f"image-shard x{world}"},
         "phases_rank0_last_step": {k: round(v, 1) for k, v in phases.items()},
         "recall": {k: round(v, 2) for k, v in metrics.items()},
-        "roofline": roofline, "cpu_baseline": None,
+        "roofline": roofline, "parity": None, "cpu_baseline": None,
     }
     out["process_group"] = ({"backend": dist.get_backend(), "ranks": dist.get_world_size(),
                              "same_device": bool(args.same_device)} if world > 1 else None)
+    if rank == 0 and world == 1 and not args.no_parity:
+        out["parity"] = colpali_parity(last["tables"], last["scores"], caps)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         sys.path.insert(0, ROOT)
-        out["cpu_baseline"] = cpu_baseline_colpali(spec, args.cpu_seconds)
+        out["cpu_baseline"] = cpu_baseline_colpali(spec, args.cpu_seconds, n, caps)
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:

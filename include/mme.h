@@ -35,7 +35,10 @@ extern "C" {
 #define MME_ERR_HIP 2         /* HIP runtime error at launch               */
 #define MME_ERR_UNSUPPORTED 3 /* valid request this build does not handle  */
 
-#define MME_ABI_VERSION 6  /* 6: mme_gemm_res_stats row_part is [M][N / 64][2] */
+#define MME_ABI_VERSION 7  /* 6: mme_gemm_res_stats row_part is [M][N / 64][2]; 7: mme_build_flags, mme_topk_rows_torch */
+
+/* mme_build_flags() bits */
+#define MME_BUILD_DEV 1 /* development / diagnostic kernel forms compiled in (libmme_dev.so) */
 
 /* activation codes for mme_gemm (HF config.hidden_act) */
 #define MME_ACT_NONE 0
@@ -50,6 +53,7 @@ extern "C" {
 
 const char* mme_last_error(void);
 int mme_abi_version(void);
+int mme_build_flags(void); /* MME_BUILD_* bits of this library */
 
 /* ---------------------------------------------------------------- a2 ----
  * PIL-exact bicubic resize of u8 RGB images + rescale(1/255) + normalise.
@@ -188,6 +192,16 @@ int mme_topk_merge(const int32_t* in_idx, const float* in_score, int rows, int p
  * Replaces torch.topk at main.py:335,365,375 on the MaxSim (ColPali) score matrices. */
 int mme_topk_rows(const float* scores, int ld, int rows, int cols, int k, int col_offset, int32_t* out_idx,
                   float* out_score, void* stream);
+
+/* Row top-k in torch.topk's CPU order (main.py:335,365,375: torch.topk(row, k) per row).
+ * torch's CPU kernel (aten SortingKernel.cpp topk_impl_loop) selects with libstdc++'s
+ * std::partial_sort when k * 64 <= cols, else std::nth_element + std::sort of the first
+ * k - 1, comparing values only: exact ties (ColPali's bf16-quantised MaxSim sums) come
+ * out in that algorithm's order, which this replays step for step. Same arguments as
+ * mme_topk_rows; workspace >= mme_topk_rows_torch_workspace_bytes (0 when k * 64 <= cols). */
+size_t mme_topk_rows_torch_workspace_bytes(int rows, int cols, int k);
+int mme_topk_rows_torch(const float* scores, int ld, int rows, int cols, int k, int col_offset, int32_t* out_idx,
+                        float* out_score, void* workspace, size_t ws_bytes, void* stream);
 
 /* Bootstrap resampling (§8f-3; run_bootstrap_benchmark main.py:586-634): the score
  * matrices of B resamples as index gathers of the full matrices,

@@ -2133,12 +2133,47 @@ __global__ __launch_bounds__(256) void probe_attn_kernel(const bf16* __restrict_
 }
 
 template <int HD>
-void launch_attn(int kind, const AttnArgs& a, int B, int T, int H, hipStream_t st) {
+bool launch_attn_dev(int kind, const AttnArgs& a, int B, int T, int H, hipStream_t st);
+
+// Production kinds (chosen by mme_attention's dispatch below); every other kind is a
+// development form, built only into the MME_DEV library (make dev -> libmme_dev.so).
+template <int HD>
+bool launch_attn(int kind, const AttnArgs& a, int B, int T, int H, hipStream_t st) {
     if (kind == 0)
         hipLaunchKernelGGL((attn_fwd_kernel<HD>), dim3(cdiv(T, 128) * H * B), dim3(256), 0, st, a);
     else if (kind == 16)  // T <= 64: one key tile, two (batch, head) units per block
         hipLaunchKernelGGL((attn_short_kernel<HD>), dim3(cdiv(B * H, 2)), dim3(256), 0, st, a, B * H);
-    else if (kind == 19)  // dev: short kernel, compact K pitch (4 blocks per CU): no gain, HBM-bound (0.138 / 0.136 ms)
+    else if (kind == 11)  // lean per-tile VALU, lazy rescale, ones column (HD 72), 8 waves
+        hipLaunchKernelGGL((attn_pipe_kernel<HD, 8, 2, false, HD == 72, true>), dim3(cdiv(T, 256) * H * B), dim3(512), 0, st, a);
+    else if (kind == 14)  // the same, 4 waves = 128 queries per block
+        hipLaunchKernelGGL((attn_pipe_kernel<HD, 4, 2, false, HD == 72, true>), dim3(cdiv(T, 128) * H * B), dim3(256), 0, st, a);
+    else if (kind == 23)  // 12 waves = 384 queries per block (hd 80, T = 730: two blocks per batch-head)
+        hipLaunchKernelGGL((attn_pipe_kernel<HD, 12, 2, false, HD == 72, true>), dim3(cdiv(T, 384) * H * B), dim3(768), 0, st, a);
+    else if (kind == 35)  // 9 waves (288 queries) with static priority for waves 4..8 (T = 257 in one block per
+                          // batch-head; +1-4 %, bit-identical; profiles/r02_attn_prio_hd80_ab.log)
+        hipLaunchKernelGGL((attn_pipe_kernel<HD, 9, 2, false, HD == 72, true, false, 1, false, 4>),
+                           dim3(cdiv(T, 288) * H * B), dim3(576), 0, st, a);
+    else if (kind == 38)  // attn_m32_kernel: 8 waves (<= 128 VGPRs uncapped: 4 waves / SIMD), static priority;
+                          // production for hd 80 (DFN5B T 730)
+        hipLaunchKernelGGL((attn_m32_kernel<HD, 8, 1, true>), dim3(cdiv(T, 256) * H * B), dim3(512), 0, st, a);
+    else if (kind == 41)  // attn_m32_kernel, 9 waves (288 queries): production for hd 80 where 9-wave blocks pad least
+        hipLaunchKernelGGL((attn_m32_kernel<HD, 9, 1, true>), dim3(cdiv(T, 288) * H * B), dim3(576), 0, st, a);
+    else if (kind == 62) {  // attn_hyb_kernel skipping a tile's second key block when it lies past the keys:
+                            // production for hd 72
+        if constexpr (HD != 64)
+            hipLaunchKernelGGL((attn_hyb_kernel<HD, 8, 4, true, true>), dim3(cdiv(T, 256) * H * B), dim3(512), 0, st, a);
+        else
+            hipLaunchKernelGGL((attn_m32_kernel<HD, 8, 1, true>), dim3(cdiv(T, 256) * H * B), dim3(512), 0, st, a);
+    } else
+        return launch_attn_dev<HD>(kind, a, B, T, H, st);
+    return true;
+}
+
+#ifdef MME_DEV
+// Development and diagnostic forms (tools/attn_bench.py, tests marked `dev`).
+template <int HD>
+bool launch_attn_dev(int kind, const AttnArgs& a, int B, int T, int H, hipStream_t st) {
+    if (kind == 19)  // dev: short kernel, compact K pitch (4 blocks per CU): no gain, HBM-bound (0.138 / 0.136 ms)
         hipLaunchKernelGGL((attn_short_kernel<HD, true>), dim3(cdiv(B * H, 2)), dim3(256), 0, st, a, B * H);
     else if (kind == 1)
         hipLaunchKernelGGL((attn_dma_kernel<HD, 4, 2>), dim3(cdiv(T, 128) * H * B), dim3(256), 0, st, a);
@@ -2158,12 +2193,8 @@ void launch_attn(int kind, const AttnArgs& a, int B, int T, int H, hipStream_t s
         hipLaunchKernelGGL((attn_pipe_kernel<HD, 8, 2, false, false, false>), dim3(cdiv(T, 256) * H * B), dim3(512), 0, st, a);
     else if (kind == 10)  // dev: + lazy rescale
         hipLaunchKernelGGL((attn_pipe_kernel<HD, 8, 2, false, false, true>), dim3(cdiv(T, 256) * H * B), dim3(512), 0, st, a);
-    else if (kind == 11)  // dev: + ones column (HD 72 only)
-        hipLaunchKernelGGL((attn_pipe_kernel<HD, 8, 2, false, HD == 72, true>), dim3(cdiv(T, 256) * H * B), dim3(512), 0, st, a);
     else if (kind == 13)  // dev: lean + lazy (+ ones), 2 waves = 64 queries per block (text towers)
         hipLaunchKernelGGL((attn_pipe_kernel<HD, 2, 2, false, HD == 72, true>), dim3(cdiv(T, 64) * H * B), dim3(128), 0, st, a);
-    else if (kind == 14)  // dev: lean + lazy (+ ones), 4 waves = 128 queries per block
-        hipLaunchKernelGGL((attn_pipe_kernel<HD, 4, 2, false, HD == 72, true>), dim3(cdiv(T, 128) * H * B), dim3(256), 0, st, a);
     else if (kind == 15)  // dev: ping-pong halves (8 waves), lean + lazy (+ ones)
         hipLaunchKernelGGL((attn_pipe_kernel<HD, 8, 4, false, HD == 72, true, true>), dim3(cdiv(T, 256) * H * B), dim3(512), 0, st, a);
     else if (kind == 17)  // dev: kind 11 held to 128 VGPRs -> two 8-wave blocks per CU (4 waves / SIMD)
@@ -2174,8 +2205,6 @@ void launch_attn(int kind, const AttnArgs& a, int B, int T, int H, hipStream_t s
         hipLaunchKernelGGL((attn_pipe_kernel<HD, 3, 2, false, HD == 72, true>), dim3(cdiv(T, 96) * H * B), dim3(192), 0, st, a);
     else if (kind == 21)  // 9 waves = 288 queries per block (T = 257 in one block per batch-head)
         hipLaunchKernelGGL((attn_pipe_kernel<HD, 9, 2, false, HD == 72, true>), dim3(cdiv(T, 288) * H * B), dim3(576), 0, st, a);
-    else if (kind == 23)  // 12 waves = 384 queries per block (hd 80, T = 730: two blocks per batch-head)
-        hipLaunchKernelGGL((attn_pipe_kernel<HD, 12, 2, false, HD == 72, true>), dim3(cdiv(T, 384) * H * B), dim3(768), 0, st, a);
     else if (kind == 24)  // dev: 12 waves, 3 waves / SIMD register budget (hd 72 T 729: 1.033 ms vs 1.03-1.07, noise)
         hipLaunchKernelGGL((attn_pipe_kernel<HD, 12, 2, false, HD == 72, true, false, 3>), dim3(cdiv(T, 384) * H * B), dim3(768), 0, st, a);
     else if (kind == 25)  // dev: 12 waves, 3-stage ring (slower: LDS occupancy)
@@ -2206,10 +2235,6 @@ void launch_attn(int kind, const AttnArgs& a, int B, int T, int H, hipStream_t s
     else if (kind == 34)  // dev: kind 27 with 16-B O stores + static priority
         hipLaunchKernelGGL((attn_pipe_kernel<HD, 8, 2, false, HD == 72, true, false, 4, true, 20>),
                            dim3(cdiv(T, 256) * H * B), dim3(512), 0, st, a);
-    else if (kind == 35)  // kind 21 (9 waves) with static priority for waves 4..8: production (ViT-H T 257,
-                          // +1-4 %, bit-identical; profiles/r02_attn_prio_hd80_ab.log)
-        hipLaunchKernelGGL((attn_pipe_kernel<HD, 9, 2, false, HD == 72, true, false, 1, false, 4>),
-                           dim3(cdiv(T, 288) * H * B), dim3(576), 0, st, a);
     else if (kind == 36)  // dev: kind 23 (12 waves) with static priority (DFN5B T 730: within noise)
         hipLaunchKernelGGL((attn_pipe_kernel<HD, 12, 2, false, HD == 72, true, false, 1, false, 4>),
                            dim3(cdiv(T, 384) * H * B), dim3(768), 0, st, a);
@@ -2219,15 +2244,10 @@ void launch_attn(int kind, const AttnArgs& a, int B, int T, int H, hipStream_t s
     else if (kind == 31)  // dev: both
         hipLaunchKernelGGL((attn_pipe_kernel<HD, 8, 2, false, HD == 72, true, false, 4, true, 6>),
                            dim3(cdiv(T, 256) * H * B), dim3(512), 0, st, a);
-    else if (kind == 38)  // attn_m32_kernel: 8 waves (<= 128 VGPRs uncapped: 4 waves / SIMD), static priority;
-                          // production for hd 80 (DFN5B T 730)
-        hipLaunchKernelGGL((attn_m32_kernel<HD, 8, 1, true>), dim3(cdiv(T, 256) * H * B), dim3(512), 0, st, a);
     else if (kind == 39)  // dev: attn_m32_kernel, 12 waves (384 queries), 3 waves / SIMD
         hipLaunchKernelGGL((attn_m32_kernel<HD, 12, 3, true>), dim3(cdiv(T, 384) * H * B), dim3(768), 0, st, a);
     else if (kind == 40)  // dev: attn_m32_kernel, 8 waves, amdgpu_waves_per_eu(4) (spills 8 registers)
         hipLaunchKernelGGL((attn_m32_kernel<HD, 8, 4, true>), dim3(cdiv(T, 256) * H * B), dim3(512), 0, st, a);
-    else if (kind == 41)  // attn_m32_kernel, 9 waves (288 queries): production for hd 80 where 9-wave blocks pad least
-        hipLaunchKernelGGL((attn_m32_kernel<HD, 9, 1, true>), dim3(cdiv(T, 288) * H * B), dim3(576), 0, st, a);
     else if (kind == 42)  // dev: attn_m32_kernel, 8 waves, no static priority
         hipLaunchKernelGGL((attn_m32_kernel<HD, 8, 1, false>), dim3(cdiv(T, 256) * H * B), dim3(512), 0, st, a);
     else if (kind == 43)  // dev: attn_m32_kernel with delayed PV (3-slot ring), 8 waves
@@ -2272,17 +2292,20 @@ void launch_attn(int kind, const AttnArgs& a, int B, int T, int H, hipStream_t s
         } else {
             hipLaunchKernelGGL((attn_m32_kernel<HD, 8, 1, true>), dim3(cdiv(T, 256) * H * B), dim3(512), 0, st, a);
         }
-    } else if (kind == 62) {  // kind 58 skipping a tile's second key block when it lies past the keys: production for hd 72
-        if constexpr (HD != 64) {
-            hipLaunchKernelGGL((attn_hyb_kernel<HD, 8, 4, true, true>), dim3(cdiv(T, 256) * H * B), dim3(512), 0, st, a);
-        } else {
-            hipLaunchKernelGGL((attn_m32_kernel<HD, 8, 1, true>), dim3(cdiv(T, 256) * H * B), dim3(512), 0, st, a);
-        }
     } else if (kind == 12)  // dev: pipelined + lazy + ones
         hipLaunchKernelGGL((attn_pipe_kernel<HD, 8, 3, true, HD == 72, true>), dim3(cdiv(T, 256) * H * B), dim3(512), 0, st, a);
-    else
+    else if (kind == 2)
         hipLaunchKernelGGL((attn_dma_kernel<HD, 8, 2>), dim3(cdiv(T, 256) * H * B), dim3(512), 0, st, a);
+    else
+        return false;
+    return true;
 }
+#else
+template <int HD>
+bool launch_attn_dev(int, const AttnArgs&, int, int, int, hipStream_t) {
+    return false;  // development kinds live in the MME_DEV build only
+}
+#endif
 
 int g_attn_variant = 0;  // dev-only override (tools/attn_bench.py)
 
@@ -2343,6 +2366,7 @@ extern "C" int mme_attention(const void* qkv, int ld_qkv, void* out, int ld_out,
                : pad9 * 10 < min(pad8, pad4) * 9 ? 35
                : (hd == 80 && pad12 <= pad8 && pad12 * 10 <= pad4 * 11) ? 23
                : (pad8 * 10 <= pad4 * 11 ? (hd == 72 ? 62 : 11) : 14);
+#ifdef MME_DEV
     if (g_attn_variant >= 1 && g_attn_variant <= 4 && hd == 72) {  // dev-only diagnostic builds
         const dim3 grid(cdiv(T, 128) * H * B);
         switch (g_attn_variant) {
@@ -2353,9 +2377,11 @@ extern "C" int mme_attention(const void* qkv, int ld_qkv, void* out, int ld_out,
         }
         return mme_check_launch("mme_attention");
     }
+#endif
     if (g_attn_variant >= 9 && g_attn_variant <= 16) kind = g_attn_variant - 9;  // dev: force a kernel
     if (g_attn_variant >= 30 && g_attn_variant <= 99) kind = g_attn_variant - 30;  // dev: force a kernel
     if ((kind == 16 || kind == 19) && T > 64) kind = 0;  // the short kernels hold one 64-key tile
+#ifdef MME_DEV
     if (g_attn_variant >= 21 && g_attn_variant <= 26 && hd == 72) {  // dev: attn_dma_kernel<72,8,2> diagnostics
         const dim3 grid(cdiv(T, 256) * H * B), blk(512);
         hipStream_t st = as_stream(stream);
@@ -2369,12 +2395,11 @@ extern "C" int mme_attention(const void* qkv, int ld_qkv, void* out, int ld_out,
         }
         return mme_check_launch("mme_attention");
     }
-    if (hd == 64)
-        launch_attn<64>(kind, a, B, T, H, as_stream(stream));
-    else if (hd == 72)
-        launch_attn<72>(kind, a, B, T, H, as_stream(stream));
-    else
-        launch_attn<80>(kind, a, B, T, H, as_stream(stream));
+#endif
+    const bool ok = hd == 64 ? launch_attn<64>(kind, a, B, T, H, as_stream(stream))
+                    : hd == 72 ? launch_attn<72>(kind, a, B, T, H, as_stream(stream))
+                               : launch_attn<80>(kind, a, B, T, H, as_stream(stream));
+    MME_REQUIRE(ok, "mme_attention: kernel kind %d is a development form (build libmme_dev.so: make dev)", kind);
     return mme_check_launch("mme_attention");
 }
 

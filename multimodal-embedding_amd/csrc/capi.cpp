@@ -27,3 +27,10 @@ int mme_check_launch(const char* what) {
 
 extern "C" const char* mme_last_error(void) { return g_err; }
 extern "C" int mme_abi_version(void) { return MME_ABI_VERSION; }
+extern "C" int mme_build_flags(void) {
+#ifdef MME_DEV
+    return MME_BUILD_DEV;
+#else
+    return 0;
+#endif
+}

@@ -1782,6 +1782,12 @@ extern "C" int mme_gemm_debug_buffer(void* p) {  // dev: device buffer for varia
 }
 
 extern "C" int mme_gemm_variant(int v) {
+#ifndef MME_DEV
+    // the production library holds the dispatched kernels and pipe6 (variant 47, the
+    // bit-identity reference of pipe8) / the per-row statistics combine (48) only
+    MME_REQUIRE(v == -1 || v == 47 || v == 48, "mme_gemm_variant: variant %d is a development form "
+                "(build libmme_dev.so: make dev)", v);
+#endif
     g_variant = v;
     return MME_OK;
 }
@@ -1920,10 +1926,12 @@ int gemm_dispatch(GemmArgs a, hipStream_t s) {
     const void* residual = a.res;
     (void)K;
     const bool glu = act == MME_ACT_GEGLU_TANH;
+#ifdef MME_DEV
     if (g_variant >= 40 && g_variant <= 43) {  // dev: pipe6 with the first block wave de-phased by
         a.stagger = (g_variant - 39) * (K / 32) / 12;  // (variant-39)/4 of a tile per phase step
         return launch_pipe6<Pipe256, 4, 1>(a, s);
     }
+#endif
     if (glu) {  // gated epilogue: the pipelined kernel only (its LDS-staged 16-B tile rows pair gate/up)
         MME_REQUIRE(N % 8 == 0 && ldc % 4 == 0 && !out_f32 && !residual && ((uintptr_t)Cp & 7) == 0,
                     "mme_gemm: GeGLU needs N %% 8 == 0, ldc %% 4 == 0, 8-B aligned bf16 C, no residual");
@@ -1931,6 +1939,10 @@ int gemm_dispatch(GemmArgs a, hipStream_t s) {
         return launch_pipe6<Pipe256, 4, 1>(a, s);
     }
     switch (g_variant) {
+        case 47:  // pipe6 as dispatched before pipe8: split grid (512 x 128 tiles for the last 128 columns) where N = 256 k + 128
+            if (a.N % 256 == 128) return launch_pipe6<Pipe256, 4, 1, 0, true>(a, s);
+            return launch_pipe6<Pipe256, 4, 1>(a, s);
+#ifdef MME_DEV
         case 0: return launch<BigCfg, 1>(a, s);
         case 1: return launch<BigCfg, 4>(a, s);
         case 2: return launch<BigCfg, 8>(a, s);
@@ -1961,9 +1973,6 @@ int gemm_dispatch(GemmArgs a, hipStream_t s) {
         case 49:  // dev: epilogue stored straight from the accumulators (no LDS staging)
             if (a.N % 256 == 128) return launch_pipe6<Pipe256, 4, 1, 11, true>(a, s);
             return launch_pipe6<Pipe256, 4, 1, 11>(a, s);
-        case 47:  // pipe6 as dispatched before pipe8: split grid (512 x 128 tiles for the last 128 columns) where N = 256 k + 128
-            if (a.N % 256 == 128) return launch_pipe6<Pipe256, 4, 1, 0, true>(a, s);
-            return launch_pipe6<Pipe256, 4, 1>(a, s);
         case 46: return launch_pipe6<PCfg<256, 256, 2, 4, 3>, 4, 1>(a, s);  // dev: 3-deep ring (2 stages ahead)
         case 63:  // diagnostic: production pipe6 with per-tile timestamps (DIAG 12; needs mme_gemm_debug_buffer)
             if (N % 256 == 128) return launch_pipe6<Pipe256, 4, 1, 12, true>(a, s);
@@ -2021,6 +2030,7 @@ int gemm_dispatch(GemmArgs a, hipStream_t s) {
         case 51: return launch_pipe7<Pipe256w, 8>(a, s);
         case 52: return launch_pipe7<Pipe256w, 4, 1>(a, s);  // diagnostic: no DMA
         case 53: return launch_pipe7<Pipe256w, 4, 2>(a, s);  // diagnostic: no epilogue
+#endif
         default: break;
     }
     // production dispatch: the pipelined 256x256 kernel whenever its 16-byte

@@ -221,6 +221,181 @@ __global__ __launch_bounds__(256) void topk_rows_kernel(const float* __restrict_
     }
 }
 
+// ---------------------------------------------------------------------------
+// Row top-k in torch.topk's CPU order (main.py:335,365,375 call torch.topk(row, k)
+// per row on the CPU). torch's CPU kernel (aten SortingKernel.cpp topk_impl_loop)
+// builds (value, column) pairs and, with comp(x, y) = x.value > y.value (NaN first),
+// runs libstdc++'s std::partial_sort when k * 64 <= n (heap select over the first k,
+// then sort_heap) and otherwise std::nth_element(k - 1) + std::sort of the first k - 1
+// (introselect: median-of-3 pivot, unguarded partition, heap-select fallback at
+// depth 2 floor(log2 n), insertion sort of <= 3). Exact ties -- the rule with ColPali's
+// bf16-quantised MaxSim sums -- therefore come out in that algorithm's order, not by
+// column; this kernel replays the same algorithm step for step (oracle:
+// oracle/torch_topk.cpp, which calls the libstdc++ algorithms themselves).
+//
+// k * 64 <= n (every configs[3] row): one wave per row. The heap (k <= 16 pairs)
+// lives in LDS; the row streams through in 64-column chunks, and a ballot of
+// `value > heap top` picks the only columns heap select can act on (the top only
+// grows), which are then replayed in column order. Otherwise (n < 64 k <= 1024):
+// nth_element + sort on a copy of the row in the workspace.
+struct TPair {
+    float v;
+    int i;
+};
+__device__ __forceinline__ bool tcomp(const TPair& x, const TPair& y) {  // torch: largest, NaN first
+    return (__builtin_isnan(x.v) && !__builtin_isnan(y.v)) || (x.v > y.v);
+}
+// libstdc++ std::__adjust_heap + std::__push_heap (bits/stl_heap.h), comp = tcomp
+__device__ void heap_adjust(TPair* h, int hole, int len, TPair value) {
+    const int top = hole;
+    int second = hole;
+    while (second < (len - 1) / 2) {
+        second = 2 * (second + 1);
+        if (tcomp(h[second], h[second - 1])) second--;
+        h[hole] = h[second];
+        hole = second;
+    }
+    if ((len & 1) == 0 && second == (len - 2) / 2) {
+        second = 2 * (second + 1);
+        h[hole] = h[second - 1];
+        hole = second - 1;
+    }
+    int parent = (hole - 1) / 2;
+    while (hole > top && tcomp(h[parent], value)) {
+        h[hole] = h[parent];
+        hole = parent;
+        parent = (hole - 1) / 2;
+    }
+    h[hole] = value;
+}
+__device__ void heap_make(TPair* h, int len) {  // std::__make_heap
+    if (len < 2) return;
+    for (int parent = (len - 2) / 2;; --parent) {
+        heap_adjust(h, parent, len, h[parent]);
+        if (parent == 0) return;
+    }
+}
+__device__ void heap_sort(TPair* h, int len) {  // std::__sort_heap
+    while (len > 1) {
+        --len;
+        const TPair value = h[len];
+        h[len] = h[0];
+        heap_adjust(h, 0, len, value);
+    }
+}
+// std::__heap_select(first, middle, last) on a materialised range
+__device__ void heap_select_range(TPair* q, int middle, int last) {
+    heap_make(q, middle);
+    for (int i = middle; i < last; ++i)
+        if (tcomp(q[i], q[0])) {  // std::__pop_heap(first, middle, i)
+            const TPair value = q[i];
+            q[i] = q[0];
+            heap_adjust(q, 0, middle, value);
+        }
+}
+__device__ __forceinline__ void tswap(TPair* a, TPair* b) {
+    const TPair t = *a;
+    *a = *b;
+    *b = t;
+}
+__device__ void insertion_sort(TPair* q, int first, int last) {  // std::__insertion_sort
+    if (first == last) return;
+    for (int i = first + 1; i < last; ++i) {
+        const TPair val = q[i];
+        if (tcomp(val, q[first])) {
+            for (int j = i; j > first; --j) q[j] = q[j - 1];  // move_backward
+            q[first] = val;
+        } else {  // std::__unguarded_linear_insert
+            int last_ = i, next = i - 1;
+            while (tcomp(val, q[next])) {
+                q[last_] = q[next];
+                last_ = next;
+                --next;
+            }
+            q[last_] = val;
+        }
+    }
+}
+__device__ void move_median_to_first(TPair* q, int result, int a, int b, int c) {
+    if (tcomp(q[a], q[b])) {
+        if (tcomp(q[b], q[c])) tswap(q + result, q + b);
+        else if (tcomp(q[a], q[c])) tswap(q + result, q + c);
+        else tswap(q + result, q + a);
+    } else if (tcomp(q[a], q[c])) tswap(q + result, q + a);
+    else if (tcomp(q[b], q[c])) tswap(q + result, q + c);
+    else tswap(q + result, q + b);
+}
+__device__ int unguarded_partition(TPair* q, int first, int last, int pivot) {
+    while (true) {
+        while (tcomp(q[first], q[pivot])) ++first;
+        --last;
+        while (tcomp(q[pivot], q[last])) --last;
+        if (!(first < last)) return first;
+        tswap(q + first, q + last);
+        ++first;
+    }
+}
+__device__ void nth_element_torch(TPair* q, int nth, int n) {  // std::nth_element -> std::__introselect
+    if (n == 0 || nth == n) return;
+    int first = 0, last = n;
+    int depth = 2 * (31 - __builtin_clz(n));  // std::__lg(n) * 2
+    while (last - first > 3) {
+        if (depth == 0) {
+            heap_select_range(q + first, nth + 1 - first, last - first);
+            tswap(q + first, q + nth);
+            return;
+        }
+        --depth;
+        const int mid = first + (last - first) / 2;
+        move_median_to_first(q, first, first + 1, mid, last - 1);
+        const int cut = unguarded_partition(q, first + 1, last, first);
+        if (cut <= nth) first = cut;
+        else last = cut;
+    }
+    insertion_sort(q, first, last);
+}
+
+// Every lane of the wave runs the (uniform) algorithm itself on the shared LDS heap /
+// workspace row -- the same reads and writes of the same values in every lane -- so no
+// lane ever depends on another lane's memory writes.
+__global__ __launch_bounds__(256) void topk_rows_torch_kernel(const float* __restrict__ S, int ld, int rows, int cols,
+                                                              int k, int col_offset, int32_t* __restrict__ oi,
+                                                              float* __restrict__ os, TPair* __restrict__ ws) {
+    __shared__ TPair heaps[4][KMAX];
+    const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int row = blockIdx.x * 4 + wv;
+    if (row >= rows) return;  // wave-uniform
+    const float* sr = S + (long)row * ld;
+    TPair* q;
+    if ((long)k * 64 <= cols) {  // std::partial_sort(q, q + k, q + n): heap select + sort_heap
+        q = heaps[wv];
+        for (int j = 0; j < k; ++j) q[j] = TPair{sr[j], j};
+        heap_make(q, k);
+        for (int c0 = k; c0 < cols; c0 += 64) {
+            const int c = c0 + lane;
+            const float v = c < cols ? sr[c] : 0.f;
+            const TPair top = q[0];
+            unsigned long long m = __ballot(c < cols && tcomp(TPair{v, c}, top));
+            while (m) {  // candidates in column order (the top only grows: no other column acts)
+                const int b = __builtin_ctzll(m);
+                m &= m - 1;
+                const float vb = __shfl(v, b, 64);
+                if (tcomp(TPair{vb, 0}, q[0])) heap_adjust(q, 0, k, TPair{vb, c0 + b});  // __pop_heap(first, middle, i)
+            }
+        }
+        heap_sort(q, k);
+    } else {  // std::nth_element(q, q + k - 1, q + n) + std::sort(q, q + k - 1)
+        q = ws + (long)row * cols;
+        for (int c = 0; c < cols; ++c) q[c] = TPair{sr[c], c};
+        nth_element_torch(q, k - 1, cols);
+        insertion_sort(q, 0, k - 1);  // std::sort of <= 15 elements = its final insertion sort
+    }
+    if (lane < k) {
+        oi[(long)row * k + lane] = q[lane].i + col_offset;
+        os[(long)row * k + lane] = q[lane].v;
+    }
+}
+
 // Winoground 2x2 scoring (run_winoground, run_benchmark_grand_slam_v28_publication_ready.py:
 // 413-461): per example s[t][i] = bf16( <text_t, image_i> ) — torch.matmul on the bf16
 // (normalised) embeddings, fp32 accumulation, one rounding — then the strict comparisons
@@ -372,6 +547,25 @@ extern "C" int mme_topk_rows(const float* scores, int ld, int rows, int cols, in
     hipLaunchKernelGGL(topk_rows_kernel, dim3(cdiv(rows, 4)), dim3(256), 0, as_stream(stream), scores, ld, rows, cols,
                        k, col_offset, out_idx, out_score);
     return mme_check_launch("mme_topk_rows");
+}
+
+extern "C" size_t mme_topk_rows_torch_workspace_bytes(int rows, int cols, int k) {
+    return ((long)k * 64 <= cols) ? 0 : (size_t)rows * cols * sizeof(TPair);
+}
+
+extern "C" int mme_topk_rows_torch(const float* scores, int ld, int rows, int cols, int k, int col_offset,
+                                   int32_t* out_idx, float* out_score, void* workspace, size_t ws_bytes,
+                                   void* stream) {
+    MME_REQUIRE(scores && out_idx && out_score, "mme_topk_rows_torch: null pointer");
+    MME_REQUIRE(rows >= 0 && cols >= 1 && ld >= cols, "mme_topk_rows_torch: bad shape");
+    MME_REQUIRE(k >= 1 && k <= KMAX && k <= cols, "mme_topk_rows_torch: k=%d out of range (<= %d, <= cols)", k, KMAX);
+    const size_t need = mme_topk_rows_torch_workspace_bytes(rows, cols, k);
+    MME_REQUIRE(ws_bytes >= need && (need == 0 || workspace), "mme_topk_rows_torch: workspace %zu < %zu bytes",
+                ws_bytes, need);
+    if (rows == 0) return MME_OK;
+    hipLaunchKernelGGL(topk_rows_torch_kernel, dim3(cdiv(rows, 4)), dim3(256), 0, as_stream(stream), scores, ld, rows,
+                       cols, k, col_offset, out_idx, out_score, reinterpret_cast<TPair*>(workspace));
+    return mme_check_launch("mme_topk_rows_torch");
 }
 
 extern "C" int mme_gather_scores(const float* S, long ld, const int32_t* rows, const int32_t* cols, int B, int R,

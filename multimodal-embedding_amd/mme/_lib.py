@@ -11,18 +11,22 @@ import os
 from ctypes import c_float, c_int, c_int64, c_size_t, c_void_p
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.environ.get("MME_LIB", os.path.join(_HERE, "libmme.so"))
+# MME_DEV=1 loads the development build (every dev / diagnostic kernel form; `make dev`)
+DEV = os.environ.get("MME_DEV", "0") == "1"
+LIB_PATH = os.environ.get("MME_LIB", os.path.join(_HERE, "libmme_dev.so" if DEV else "libmme.so"))
 
 # MME_ACT_* / MME_PIX_* from include/mme.h
 ACT_NONE, ACT_GELU_TANH, ACT_QUICK_GELU, ACT_GELU_ERF, ACT_GEGLU_TANH = 0, 1, 2, 3, 4
 PIX_F32_NCHW, PIX_PATCHES = 0, 1
-ABI_VERSION = 6
+ABI_VERSION = 7
+BUILD_DEV = 1  # MME_BUILD_DEV
 
 # name -> (restype, argtypes)
 _P = c_void_p
 SIGNATURES = {
     "mme_last_error": (ctypes.c_char_p, []),
     "mme_abi_version": (c_int, []),
+    "mme_build_flags": (c_int, []),
     "mme_preprocess_workspace_bytes": (c_size_t, [c_int] * 5),
     "mme_preprocess_u8": (c_int, [_P, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, _P, _P, c_int, c_int,
                                   c_int, _P, _P, c_size_t, _P]),
@@ -47,6 +51,8 @@ SIGNATURES = {
     "mme_recall_hits_groups": (c_int, [_P, c_int, c_int, c_int, c_int, _P, c_int, _P, _P]),
     "mme_winoground": (c_int, [_P, _P, c_int, c_int, _P, _P, _P]),
     "mme_topk_rows": (c_int, [_P, c_int, c_int, c_int, c_int, c_int, _P, _P, _P]),
+    "mme_topk_rows_torch_workspace_bytes": (c_size_t, [c_int, c_int, c_int]),
+    "mme_topk_rows_torch": (c_int, [_P, c_int, c_int, c_int, c_int, c_int, _P, _P, _P, c_size_t, _P]),
     "mme_recall_hits":(c_int, [_P, c_int, c_int, _P, c_int, c_int, _P, c_int, _P, _P]),
     "mme_maxsim_workspace_bytes": (c_size_t, [c_int, c_int, c_int]),
     "mme_maxsim": (c_int, [_P, _P, c_int, c_int, _P, _P, _P, c_int, c_int, c_int, _P, _P, c_size_t, _P]),
@@ -74,8 +80,8 @@ def _build() -> None:
     import subprocess
     pkg = os.path.dirname(_HERE)
     if os.path.exists(os.path.join(pkg, "Makefile")):
-        subprocess.run(["make", "-C", pkg, "-j", str(min(16, os.cpu_count() or 8))], check=False,
-                       stdout=subprocess.DEVNULL)
+        subprocess.run(["make", "-C", pkg, "-j", str(min(16, os.cpu_count() or 8))] + (["dev"] if DEV else []),
+                       check=False, stdout=subprocess.DEVNULL)
 
 
 def load() -> ctypes.CDLL:
@@ -103,6 +109,11 @@ def load() -> ctypes.CDLL:
         fn.argtypes = args
     _lib = lib
     return lib
+
+
+def is_dev() -> bool:
+    """True when the loaded library is the development build (dev kernel forms compiled in)."""
+    return bool(load().mme_build_flags() & BUILD_DEV)
 
 
 def call(name: str, *args) -> None:

@@ -7,16 +7,16 @@ images WITH replacement (main.py:588), re-scores the sampled embeddings
 (README.md:70-72). A resample's score matrices are index gathers of the full
 matrices, so here the full T2I [n, n] and I2T [n, 5n] matrices are computed once
 (mme_gemm, or MaxSim for ColPali) and each batch of resamples is
-mme_gather_scores -> mme_topk_rows (top-10, score desc / position asc) ->
-mme_recall_hits_groups; only the 9 x iterations hit counts leave the device.
+mme_gather_scores -> mme_topk_rows_torch (one selection per k, in torch.topk's CPU
+order) -> mme_recall_hits_groups; only the 9 x iterations hit counts leave the device.
 
 Sampled positions: resample b's image i is samples[b, i]; its T2I query is that
 image's caption-0 row, its I2T targets the 5 positions of that image's captions
 (img_to_caps_map, main.py:601-609), I2T-Sym is the transposed T2I matrix
-(main.py:624). Ties — a duplicated image scores exactly like its copies — are
-ordered by position; torch.topk's order among equal values is implementation
-defined (observed to vary with k), so rows whose target ties straddle the k-th
-place are the only ones where the reference's own result is not determined.
+(main.py:624). Ties — a duplicated image scores exactly like its copies — decide
+many rows; the reference's torch.topk keeps the copy its libstdc++ partial_sort /
+nth_element leaves (a different selection per k), and mme_topk_rows_torch replays
+exactly that, so every resample's counts equal the reference's.
 
 The confidence interval (bootstrap_confidence_interval, main.py:259-278: 10 000
 resamples of the per-iteration values, 2.5 / 97.5 percentiles) is host statistics
@@ -56,7 +56,6 @@ def bootstrap_hits(s_t2i: torch.Tensor, s_i2t: torch.Tensor, samples: torch.Tens
     if s_t2i.shape != (n, n) or s_i2t.shape != (n, caps_per_image * n):
         raise ValueError("bootstrap_hits: expected T2I [n, n] and I2T [n, caps*n] score matrices")
     s_sym = s_t2i.t().contiguous()
-    kmax = max(ks)
     if batch is None:  # ~2 GiB of gathered scores per batch
         batch = max(1, min(iters, (2 << 30) // max(1, 4 * n * n * (2 + caps_per_image))))
     out = torch.empty(iters, 3 * len(ks), dtype=torch.int64, device=samples.device)
@@ -64,10 +63,11 @@ def bootstrap_hits(s_t2i: torch.Tensor, s_i2t: torch.Tensor, samples: torch.Tens
         smp = samples[b0:b0 + batch].contiguous()
         for j, (S, g) in enumerate(((s_t2i, 1), (s_i2t, caps_per_image), (s_sym, 1))):
             G = ops.gather_scores(S, smp, smp, g)
-            k = min(kmax, G.shape[1])
-            idx, _ = ops.topk_rows(G, k)
-            out[b0:b0 + smp.shape[0], j * len(ks):(j + 1) * len(ks)] = ops.recall_hits_groups(
-                idx, n, g, [min(x, k) for x in ks])
+            for q, k in enumerate(ks):  # one torch.topk per row and k (main.py:331-378)
+                kk = min(k, G.shape[1])
+                idx, _ = ops.topk_rows_torch(G, kk)
+                out[b0:b0 + smp.shape[0], j * len(ks) + q:j * len(ks) + q + 1] = ops.recall_hits_groups(
+                    idx, n, g, [kk])
             del G
     return out
 

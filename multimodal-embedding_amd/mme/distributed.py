@@ -137,11 +137,19 @@ def env_rank_world() -> Tuple[int, int, int]:
 
 
 class MaxSimOps:
-    """Default compute of the ColPali recall: libmme MaxSim, row top-k and recall counters."""
+    """Default compute of the ColPali recall: libmme MaxSim, row top-k and recall counters.
+
+    Recall ranks every row in torch.topk's CPU order (mme_topk_rows_torch), one selection per k
+    as compute_metrics_detailed calls it (main.py:331-378): MaxSim sums are bf16-quantised, so
+    exact ties at the k-th place are common and the reference's tie order decides them."""
 
     def maxsim(self, Q, ql, D, dl, flags):
         from . import ops
         return ops.maxsim(Q, ql, D, dl, flags)
+
+    def recall(self, s: torch.Tensor, tgt_count: int, ks: Sequence[int], row_offset: int) -> torch.Tensor:
+        from . import ops
+        return ops.recall_hits_torch(s.contiguous(), tgt_count, ks, row_offset)
 
     def topk(self, s: torch.Tensor, k: int) -> torch.Tensor:
         from . import ops
@@ -187,7 +195,9 @@ def sharded_colpali_recall(img_D: torch.Tensor, img_len: torch.Tensor, t2i_Q: to
     for s, tc in ((s_t2i, 1), (s_i2t, caps_per_image), (s_sym, 1)):
         k = min(kmax, s.shape[1])
         kk = [min(x, k) for x in ks]
-        if s.shape[0]:
+        if s.shape[0] and hasattr(compute, "recall"):
+            res.append(compute.recall(s, tc, kk, lo).to(torch.int64))
+        elif s.shape[0]:
             res.append(compute.hits(compute.topk(s, k), tc, kk, lo).to(torch.int64))
         else:
             res.append(torch.zeros(len(ks), dtype=torch.int64, device=s.device))

@@ -481,6 +481,34 @@ def topk_rows(scores: torch.Tensor, k: int, col_offset: int = 0):
     return idx, sc
 
 
+def topk_rows_torch(scores: torch.Tensor, k: int, col_offset: int = 0):
+    """Row top-k in torch.topk's CPU order (main.py:335,365,375): (idx int32 [rows,k], score fp32
+    [rows,k]). Exact ties come out as torch's libstdc++ partial_sort / nth_element leaves them."""
+    _dev(scores)
+    if scores.dtype != torch.float32:
+        raise ValueError("topk_rows_torch: scores must be fp32")
+    rows, cols = scores.shape
+    idx = torch.empty(rows, k, dtype=torch.int32, device=scores.device)
+    sc = torch.empty(rows, k, dtype=torch.float32, device=scores.device)
+    ws_bytes = query("mme_topk_rows_torch_workspace_bytes", rows, cols, k)
+    ws = torch.empty(max(ws_bytes, 1), dtype=torch.uint8, device=scores.device)
+    call("mme_topk_rows_torch", scores.data_ptr(), _rowmajor(scores, "scores"), rows, cols, k, col_offset,
+         idx.data_ptr(), sc.data_ptr(), ws.data_ptr(), ws_bytes, _stream())
+    return idx, sc
+
+
+def recall_hits_torch(scores: torch.Tensor, tgt_count: int, ks: Sequence[int], row_offset: int = 0) -> torch.Tensor:
+    """int64 [len(ks)]: rows whose torch.topk(row, min(k, cols)) holds a target column -- one selection
+    per k, as compute_metrics_detailed calls torch.topk (main.py:331-378)."""
+    cols = scores.shape[1]
+    hits = torch.zeros(len(ks), dtype=torch.int64, device=scores.device)
+    for j, k in enumerate(ks):
+        kk = min(k, cols)
+        idx, _ = topk_rows_torch(scores, kk)
+        hits[j:j + 1] = recall_hits(idx, tgt_count, [kk], row_offset=row_offset)
+    return hits
+
+
 def gather_scores(S: torch.Tensor, rows: torch.Tensor, cols: torch.Tensor, g: int = 1,
                   out: Optional[torch.Tensor] = None) -> torch.Tensor:
     """out[b*R + i, p] = S[rows[b, i], g*cols[b, p // g] + p % g]  (fp32 [B*R, C*g])."""

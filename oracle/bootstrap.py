@@ -6,13 +6,14 @@ s_i2t[s][:, caption positions of s] (img_to_caps_map, main.py:601-609), I2T-Sym
 the transposed T2I matrix (main.py:624); compute_metrics_detailed (main.py:305-383)
 counts a hit when a target column is among torch.topk(row, k).
 
-Ties: a duplicated image (sampling with replacement) scores exactly like its copy.
-This restatement orders equal scores by position (the device rule); torch.topk's
-order among equal values is implementation defined, so `ambiguous` counts the
-rows where tied columns straddle the k-th place around the target — the only rows
-on which the reference's own result is not determined by the scores.
-Pinned against tests/golden/bootstrap.npz (the reference's compute_metrics_detailed
-on resampled matrices built by its own compute_similarity_scores).
+Ties: a duplicated image (sampling with replacement) scores exactly like its copy,
+so which copy torch.topk keeps decides many rows. `resample_hits` ranks every row
+in torch.topk's own CPU order (oracle/torch_topk.cpp: the libstdc++ partial_sort /
+nth_element torch runs), one selection per k as compute_metrics_detailed calls it;
+`ambiguous` still counts the rows whose target tie group straddles the k-th place
+(where a column-order rule would be a guess). Pinned against
+tests/golden/bootstrap.npz (the reference's compute_metrics_detailed on resampled
+matrices built by its own compute_similarity_scores): every value identical.
 """
 from __future__ import annotations
 
@@ -46,13 +47,14 @@ def resample_hits(s_t2i: np.ndarray, s_i2t: np.ndarray, sample: np.ndarray, caps
     capcols = (caps * sample[:, None] + np.arange(caps)[None, :]).reshape(-1)
     i2t = s_i2t[np.ix_(sample, capcols)]
     sym = t2i.T
+    from oracle import torch_topk as TT
     hits, amb = [], []
     for S, tc in ((t2i, 1), (i2t, caps), (sym, 1)):
-        rank, gt = _rank_info(S, np.arange(n) * tc, tc)
+        _, gt = _rank_info(S, np.arange(n) * tc, tc)
         greater, ties = gt[:, 0], gt[:, 1]
+        hits.extend(TT.hits(np.ascontiguousarray(S), tc, ks).sum(0).tolist())
         for k in ks:
             k = min(k, S.shape[1])
-            hits.append(int((rank < k).sum()))
-            # undetermined by the scores: the target's tie group spans the k-th place
+            # where a column-order rule would guess: the target's tie group spans the k-th place
             amb.append(int(((greater < k) & (greater + ties >= k) & (ties > 0)).sum()))
     return np.array(hits, np.int64), np.array(amb, np.int64)

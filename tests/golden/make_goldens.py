@@ -423,6 +423,130 @@ def make_colpali_recall(main):
     print("colpali_recall.npz:", dict(zip(keys, vals.round(2))))
 
 
+_CPF = {}  # worker state of make_colpali_full (spawned processes, one torch thread each)
+
+
+def _colpali_full_init(tmp):
+    torch.set_num_threads(1)
+    from planted import left_padded_items
+    from transformers.models.colpali.processing_colpali import ColPaliProcessor
+    img = torch.from_numpy(np.load(os.path.join(tmp, "img.npy"))).view(torch.bfloat16)
+    cap = torch.from_numpy(np.load(os.path.join(tmp, "cap.npy"))).view(torch.bfloat16)
+    lens, pad = (torch.from_numpy(np.load(os.path.join(tmp, f"{k}.npy"))) for k in ("lens", "pad"))
+    t2i_pad = torch.from_numpy(np.load(os.path.join(tmp, "t2i_pad.npy")))
+    caps = int(np.load(os.path.join(tmp, "caps.npy")))
+
+    class Scorer:
+        def score(self, qs, ps):
+            return ColPaliProcessor.score_retrieval(None, qs, ps, output_dtype=torch.float32)
+    _CPF.update(main=import_reference(), scorer=Scorer(), imgs=[img[i] for i in range(img.shape[0])],
+                t2i=left_padded_items(cap[::caps].contiguous(), lens[::caps].clone(), t2i_pad),
+                caps=left_padded_items(cap, lens, pad))
+    _CPF["main"].DEVICE = "cpu"
+
+
+def _colpali_full_rows(task):
+    """Rows [lo, hi) (a multiple of the reference's chunk of 10) of one score matrix, computed
+    by the reference's own compute_similarity_scores colpali branch: every 10 x 10 chunk call
+    of the full loop over these query rows, in the same order."""
+    which, lo, hi = task
+    m = _CPF["main"]
+    if which == "t2i":   # queries = caption-0 items, docs = images
+        s = m.compute_similarity_scores(_CPF["imgs"], _CPF["t2i"][lo:hi], {"type": "colpali"}, _CPF["scorer"])
+    else:                # I2T (v28 orientation): queries = images, docs = all caption items
+        s = m.compute_similarity_scores(_CPF["caps"], _CPF["imgs"][lo:hi], {"type": "colpali"}, _CPF["scorer"])
+    return which, lo, s.numpy()
+
+
+def make_colpali_full(main, workers: int = 7):
+    """BASELINE configs[3] at its full geometry: 1 000 images x 1 030 planted doc tokens and
+    5 000 captions of 23..29 tokens (Tq ~ 26) left-padded per batch of 4
+    (tests/golden/planted.py, noise 7.0: T2I R@1 ~ 34 %). Scored by the reference's own colpali
+    branch of compute_similarity_scores (10 x 10 chunk loop, main.py:451-470; processor.score =
+    transformers' ColPaliProcessor.score_retrieval) and ranked by compute_metrics_detailed
+    (main.py:305-383, v28 I2T orientation). The 60 000 chunk calls run in `workers` spawned
+    processes with one torch thread each (the per-call scores are bit-identical to the
+    multi-threaded ones and 4x faster); each worker takes whole chunk rows of 10 queries, so
+    every call sees exactly the chunks of the full loop. Stored: seed / checksums, per row the
+    reference's own torch.topk(row, 10) indices and its top-11 scores, the per-row hit flags of
+    compute_metrics_detailed's calls, a sample of whole score rows, and the 9 metrics."""
+    import multiprocessing as mp
+    from planted import bf16_sha, planted_multivec
+    n, caps, Ld, qlens, noise, seed = 1000, 5, 1030, (23, 30), 7.0, 0
+    img, cap, lens, pad = planted_multivec(n, caps, Ld, qlens, noise, seed=seed)
+    t2i_lens = lens[::caps].clone()
+    t2i_pad = torch.tensor([int(t2i_lens[s:s + 4].max()) for s in range(0, n, 4) for _ in range(min(4, n - s))],
+                           dtype=torch.int32)
+    tmp = tempfile.mkdtemp(prefix="mme_cpf_")
+    np.save(os.path.join(tmp, "img.npy"), img.view(torch.int16).numpy())
+    np.save(os.path.join(tmp, "cap.npy"), cap.view(torch.int16).numpy())
+    for k, v in (("lens", lens), ("pad", pad), ("t2i_pad", t2i_pad)):
+        np.save(os.path.join(tmp, f"{k}.npy"), v.numpy())
+    np.save(os.path.join(tmp, "caps.npy"), np.int64(caps))
+    tasks = [("i2t", lo, min(lo + 20, n)) for lo in range(0, n, 20)] + \
+            [("t2i", lo, min(lo + 50, n)) for lo in range(0, n, 50)]
+    S = {"t2i": torch.empty(n, n), "i2t": torch.empty(n, caps * n)}
+    with mp.get_context("spawn").Pool(workers, initializer=_colpali_full_init, initargs=(tmp,)) as pool:
+        for done, (which, lo, s) in enumerate(pool.imap_unordered(_colpali_full_rows, tasks)):
+            S[which][lo:lo + s.shape[0]] = torch.from_numpy(s)
+            print(f"colpali_full: {done + 1}/{len(tasks)} row blocks", flush=True)
+    s_t2i, s_i2t = S["t2i"], S["i2t"]
+    s_sym = s_t2i.t().contiguous()
+    metrics = main.compute_metrics_detailed(s_t2i, s_i2t, s_sym, list(range(n)),
+                                            {i: list(range(caps * i, caps * i + caps)) for i in range(n)},
+                                            {i: i for i in range(n)}, [""] * n)
+    hits = np.zeros((3, n, 3), bool)  # the reference's own per-row outcome (the same torch.topk calls)
+    out = {"params": np.array([n, caps, Ld, qlens[0], qlens[1], seed], np.int64), "noise": np.float64(noise),
+           "img_sha": np.array(bf16_sha(img)), "cap_sha": np.array(bf16_sha(cap))}
+    lowest = np.zeros((3, n), bool)  # torch.topk(row, 10) == the (score desc, column asc) order
+    for p, (tag, s, tgt) in enumerate((("t2i", s_t2i, lambda i: [i]),
+                                       ("i2t", s_i2t, lambda i: range(caps * i, caps * i + caps)),
+                                       ("sym", s_sym, lambda i: [i]))):
+        for i in range(n):
+            for j, k in enumerate((1, 5, 10)):
+                top = torch.topk(s[i], k=min(k, s.shape[1])).indices.tolist()
+                hits[p, i, j] = any(c in top for c in tgt(i))
+        v11, _ = torch.topk(s, 11, dim=1)
+        ix10 = torch.stack([torch.topk(s[i], 10).indices for i in range(n)])
+        cols = np.broadcast_to(np.arange(s.shape[1]), s.shape)
+        lex = np.lexsort((cols, -s.numpy()), axis=1)[:, :10]
+        lowest[p] = (lex == ix10.numpy()).all(1)
+        out[f"{tag}_idx"] = ix10.numpy().astype(np.int32)
+        out[f"{tag}_score"] = v11.numpy().astype(np.float32)
+        print(f"colpali_full {tag}: torch.topk order == (score desc, column asc) on {int(lowest[p].sum())}/{n} rows")
+    keys = [k for k in metrics if not k.startswith("_")]
+    vals = np.array([metrics[k] for k in keys], np.float64)
+    assert np.allclose(vals.reshape(3, 3), 100.0 * hits.sum(1) / n)
+    sample = np.array([0, 1, 2, 3, 250, 499, 500, 777, 996, 997, 998, 999], np.int64)
+    out.update(hits=hits, lowest_index_rows=lowest, metric_names=np.array(keys), metric_values=vals,
+               sample_rows=sample, t2i_rows=s_t2i[sample].numpy(), i2t_rows=s_i2t[sample].numpy())
+    np.savez_compressed(os.path.join(HERE, "colpali_full.npz"), **out)
+    print("colpali_full.npz:", dict(zip(keys, vals.round(2))))
+
+
+def make_torch_topk():
+    """torch.topk's own CPU outputs on tie-heavy rows (the selection main.py:335,365,375 runs per row):
+    integer-level scores (2, 5 or 50 levels) so exact ties decide most rows, at widths on both sides of
+    torch's partial_sort / nth_element switch (k * 64 <= n) and k = 1, 5, 10. Pins oracle/torch_topk.cpp
+    and the device's mme_topk_rows_torch."""
+    rng = np.random.default_rng(11)
+    out, cases = {}, []
+    for n in (7, 10, 64, 100, 320, 639, 640, 1000, 5000):
+        for k in (1, 5, 10):
+            if k > n:
+                continue
+            for levels in (2, 5, 50):
+                s = rng.integers(0, levels, (6, n)).astype(np.float32) * np.float32(0.25)
+                v, i = torch.topk(torch.from_numpy(s), k, dim=1)
+                tag = f"n{n}_k{k}_l{levels}"
+                out[f"{tag}_s"] = (s * 4).astype(np.uint8)
+                out[f"{tag}_idx"] = i.numpy().astype(np.int32)
+                cases.append(tag)
+    out["cases"] = np.array(cases)
+    np.savez_compressed(os.path.join(HERE, "torch_topk.npz"), **out)
+    print("torch_topk.npz:", len(cases), "cases")
+
+
 def make_l2norm(main):
     """main.py:414 `out / out.norm(dim=-1, keepdim=True)` on bf16 model outputs."""
     g = torch.Generator().manual_seed(5)
@@ -647,7 +771,8 @@ if __name__ == "__main__":
              "maxsim": lambda: make_maxsim(main), "colpali_recall": lambda: make_colpali_recall(main),
              "encoders": lambda: make_encoders(main), "colpali": lambda: make_colpali(main),
              "config0": lambda: make_config0(main), "edge": lambda: make_edge(main),
-             "winoground": make_winoground, "bootstrap": lambda: make_bootstrap(main)}
+             "winoground": make_winoground, "bootstrap": lambda: make_bootstrap(main),
+             "colpali_full": lambda: make_colpali_full(main), "torch_topk": make_torch_topk}
     for name, fn in steps.items():
         if not only or name in only:
             fn()

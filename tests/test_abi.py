@@ -62,3 +62,14 @@ def test_workspace_queries():
     assert _lib.query("mme_sim_topk_workspace_bytes", 5000, 25000, 10) > 5000 * 10 * 8
     assert _lib.query("mme_maxsim_workspace_bytes", 10, 32, 100) >= 10 * 32 * 100 * 2
     assert _lib.query("mme_preprocess_workspace_bytes", 4, 224, 224, 384, 384) >= 4 * 224 * 384 * 3
+
+
+def test_production_library_holds_no_dev_forms():
+    """The default libmme.so is the production build: dev / diagnostic kernel forms are
+    refused loudly (they live in libmme_dev.so, `make dev`, MME_DEV=1)."""
+    lib = _lib.load()
+    if _lib.is_dev():
+        pytest.skip("the development library is loaded (MME_DEV=1)")
+    lib.mme_gemm_variant.argtypes = [ctypes.c_int]
+    assert lib.mme_gemm_variant(64) != 0 and b"development form" in lib.mme_last_error()
+    assert lib.mme_gemm_variant(47) == 0 and lib.mme_gemm_variant(-1) == 0

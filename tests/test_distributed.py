@@ -98,13 +98,9 @@ class MaxSimCPU:
         m = m.masked_fill(~imask[:, None, :], 0.0)
         return m.sum(-1).to(torch.bfloat16).float()
 
-    def topk(self, s, k):
-        from oracle import retrieval as R
-        return torch.from_numpy(R.topk(s.numpy(), k)[0])
-
-    def hits(self, idx, tgt_count, ks, row_offset):
-        from oracle import retrieval as R
-        return torch.from_numpy(R.recall(idx.numpy(), tgt_count, ks, row_offset))
+    def recall(self, s, tgt_count, ks, row_offset):
+        from oracle import torch_topk as TT
+        return torch.from_numpy(TT.hits(s.numpy(), tgt_count, ks, row_offset).sum(0).astype(np.int64))
 
 
 def _colpali_tables(n=13, caps=5, Ld=20, seed=0):
@@ -147,7 +143,6 @@ def _reference_colpali_metrics():
     """The reference's colpali scoring (oracle/maxsim.py chunk loop over per-item lists whose
     caption tensors carry their left zero padding) + compute_metrics_detailed's recall."""
     from oracle import maxsim as om
-    from oracle import retrieval as R
     D, dl, Qt, qtl, Qa, qal, qap = _colpali_tables()
     n, caps = D.shape[0], 5
 
@@ -164,9 +159,11 @@ def _reference_colpali_metrics():
     s_i2t = om.score_reference_chunks(imgs, cap_items(Qa, qal, qap)).numpy()
     out = {}
     for name, s, tc in (("T2I", s_t2i, 1), ("I2T", s_i2t, caps), ("I2T_Sym", s_t2i.T.copy(), 1)):
-        idx, _ = R.topk(s, 10)
-        for k, c in zip((1, 5, 10), R.recall(idx, tc, (1, 5, 10))):
-            out[f"{name}_R@{k}"] = 100.0 * c / n
+        st = torch.from_numpy(s)
+        for k in (1, 5, 10):  # compute_metrics_detailed: one torch.topk per row and k (main.py:331-378)
+            hit = sum(any(c // tc == i for c in torch.topk(st[i], min(k, st.shape[1])).indices.tolist())
+                      for i in range(n))
+            out[f"{name}_R@{k}"] = 100.0 * hit / n
     return out
 
 

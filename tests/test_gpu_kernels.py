@@ -129,7 +129,12 @@ def test_attention(cuda, B, T, H, hd, causal, lens):
     torch.testing.assert_close(out.float(), ref, atol=2e-2, rtol=2e-2)
 
 
-@pytest.mark.parametrize("kind", [38, 39, 40, 41, 42, 43, 44, 45, 46, 47, 48, 49, 50, 51, 52, 54, 55, 56, 57, 58, 59, 60, 61, 62])
+PROD_ATTN_KINDS = (38, 41, 62)  # dispatched by mme_attention; the rest are development forms (libmme_dev.so)
+
+
+@pytest.mark.parametrize("kind", [k if k in PROD_ATTN_KINDS else pytest.param(k, marks=pytest.mark.dev)
+                                  for k in (38, 39, 40, 41, 42, 43, 44, 45, 46, 47, 48, 49, 50, 51, 52, 54, 55, 56,
+                                            57, 58, 59, 60, 61, 62)])
 @pytest.mark.parametrize("B,T,H,hd,causal,lens", [
     (2, 729, 4, 72, False, None),       # SigLIP vision geometry
     (2, 520, 3, 72, False, [520, 301]),  # key padding, partial last tile
@@ -156,6 +161,21 @@ def test_attention_m32(cuda, kind, B, T, H, hd, causal, lens):
     torch.testing.assert_close(out.float(), ref, atol=2e-2, rtol=2e-2)
 
 
+def test_attention_production_full_grid(cuda):
+    """The production hd-72 kernel over the bench's full launch grid (239 images x 16 heads x
+    3 query blocks of SigLIP vision) against the fp32 reference on the first and last images
+    (grid-to-(batch, head, query block) mapping at production size)."""
+    B, T, H, hd = 239, 729, 16, 72
+    g = torch.Generator(device="cuda").manual_seed(729)
+    qkv = rnd(B * T, 3 * H * hd, scale=1.5, gen=g)
+    out = ops.attention(qkv, B, T, H, hd).float().view(B, T, H * hd)
+    assert torch.isfinite(out).all()
+    for b in (0, 1, B - 2, B - 1):
+        ref = attn_ref(qkv[b * T:(b + 1) * T], 1, T, H, hd, None, False, hd ** -0.5)
+        torch.testing.assert_close(out[b], ref.view(T, H * hd), atol=2e-2, rtol=2e-2)
+
+
+@pytest.mark.dev
 def test_attention_hd72_production_grid_vs_kind30(cuda):
     """The production hd-72 kernel (attn_hyb_kernel, kind 58) over the bench's full launch grid
     (239 images x 16 heads x 3 query blocks of SigLIP vision) against the previous production
