@@ -2132,6 +2132,96 @@ __global__ __launch_bounds__(256) void probe_attn_kernel(const bf16* __restrict_
     }
 }
 
+// SigLIP MAP head, one workgroup per image (all H heads; production where H * hd <= 1152,
+// H <= 16, T <= PROBE_MAXT). probe_attn_kernel's (image, head) blocks each read their head's
+// 144-B slice of every K / V row: the 128-B lines at head boundaries were fetched by two
+// blocks, often on two XCDs (2.6x the K / V bytes fetched). Here the image's K rows stream
+// through LDS in 16-row tiles by LDS-DMA (a tile = 16 whole 2304-B rows, read once,
+// double-buffered), thread (row, head) takes its dot product from LDS (144-B head stride:
+// the 16 lanes of a ds_read_b128 group hit 64 distinct banks), and the V rows are read once,
+// coalesced (thread = 16-B column chunk). Same math as probe_attn_kernel (fp32 dots, the
+// same exp and normalisation); the summation order of the V pass differs (fp32).
+constexpr int PROBE2_D = 1152, PROBE2_H = 16;
+__global__ __launch_bounds__(256) void probe_attn_img_kernel(const bf16* __restrict__ qv, const bf16* __restrict__ kv,
+                                                             int ld, bf16* __restrict__ out, int ldo, int T, int H,
+                                                             int hd, float scale) {
+    __shared__ __attribute__((aligned(16))) char kt[2][16 * PROBE2_D * 2];
+    __shared__ float sc[PROBE2_H * PROBE_MAXT];
+    __shared__ float qs[PROBE2_D];
+    __shared__ float hinv[PROBE2_H];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int b = blockIdx.x, D = H * hd, TR = 256 / H, CPR = D / 8;  // rows per tile, 16-B chunks per row
+    for (int i = tid; i < D; i += 256) qs[i] = bf2f(qv[i]);
+    const bf16* kb = kv + (long)b * T * ld;
+    const int npiece = TR * CPR / 64, ntile = (T + TR - 1) / TR;
+    auto issue = [&](int tile) {
+        char* dst = kt[tile & 1];
+        for (int pc = wave; pc < npiece; pc += 4) {
+            const int g = pc * 64 + lane, row = g / CPR, ch = g % CPR;
+            glds16(kb + (long)min(tile * TR + row, T - 1) * ld + ch * 8, dst + pc * 1024);
+        }
+    };
+    issue(0);
+    const int r = tid / H, h = tid % H;
+    for (int tile = 0; tile < ntile; ++tile) {
+        wait_vmcnt0();
+        __syncthreads();  // tile landed for every wave; every wave is done with the other slot
+        if (tile + 1 < ntile) issue(tile + 1);
+        const int t = tile * TR + r;
+        if (r < TR && t < T) {
+            const char* kr = kt[tile & 1] + (r * D + h * hd) * 2;
+            float dot = 0.f;
+            for (int d = 0; d < hd; d += 8) {
+                const u16x8 u = *reinterpret_cast<const u16x8*>(kr + d * 2);
+#pragma unroll
+                for (int e = 0; e < 8; ++e) dot += qs[h * hd + d + e] * bits2f(u[e]);
+            }
+            sc[h * T + t] = dot * scale;
+        }
+    }
+    __syncthreads();
+    for (int hh = wave; hh < H; hh += 4) {  // softmax of head hh
+        float mx = -INFINITY;
+        for (int t = lane; t < T; t += 64) mx = fmaxf(mx, sc[hh * T + t]);
+        mx = wave_max(mx);
+        float sum = 0.f;
+        for (int t = lane; t < T; t += 64) {
+            const float p = __expf(sc[hh * T + t] - mx);
+            sc[hh * T + t] = p;
+            sum += p;
+        }
+        sum = wave_sum(sum);
+        if (lane == 0) hinv[hh] = 1.f / sum;
+    }
+    __syncthreads();
+    if (tid < CPR) {  // V: thread = one 16-B column chunk, every row read once (coalesced rows)
+        const bf16* vb = kb + D + tid * 8;
+        const int hv = tid * 8 / hd;
+        const float* ph = sc + hv * T;
+        float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+        int t = 0;
+        for (; t + 4 <= T; t += 4) {
+            u16x8 u[4];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) u[j] = *reinterpret_cast<const u16x8*>(vb + (long)(t + j) * ld);
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+#pragma unroll
+                for (int e = 0; e < 8; ++e) acc[e] += ph[t + j] * bits2f(u[j][e]);
+        }
+        for (; t < T; ++t) {
+            const u16x8 u = *reinterpret_cast<const u16x8*>(vb + (long)t * ld);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) acc[e] += ph[t] * bits2f(u[e]);
+        }
+        const float inv = hinv[hv];
+        u16x8 o;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) o[e] = __builtin_bit_cast(unsigned short, f2bf(acc[e] * inv));
+        *reinterpret_cast<u16x8*>(out + (long)b * ldo + tid * 8) = o;
+    }
+}
+
 template <int HD>
 bool launch_attn_dev(int kind, const AttnArgs& a, int B, int T, int H, hipStream_t st);
 
@@ -2410,7 +2500,13 @@ extern "C" int mme_probe_attention(const void* q, const void* kv, int ld_kv, voi
     MME_REQUIRE(hd % 8 == 0 && hd <= 128, "mme_probe_attention: head_dim %d unsupported", hd);
     MME_REQUIRE(ld_kv % 8 == 0 && ld_kv >= 2 * H * hd, "mme_probe_attention: bad ld_kv");
     if (B == 0) return MME_OK;
-    hipLaunchKernelGGL(probe_attn_kernel, dim3(H * B), dim3(256), 0, as_stream(stream), (const bf16*)q,
-                       (const bf16*)kv, ld_kv, (bf16*)out, ld_out, T, H, hd, scale);
+    const int D = H * hd, TR = H <= 16 && 256 % H == 0 ? 256 / H : 0;
+    if (TR && D <= PROBE2_D && D % 8 == 0 && (TR * D / 8) % 64 == 0 && hd % 8 == 0 && ld_kv % 8 == 0 &&
+        ld_out % 8 == 0 && ((uintptr_t)out & 15) == 0 && ((uintptr_t)kv & 15) == 0 && g_attn_variant != 90)
+        hipLaunchKernelGGL(probe_attn_img_kernel, dim3(B), dim3(256), 0, as_stream(stream), (const bf16*)q,
+                           (const bf16*)kv, ld_kv, (bf16*)out, ld_out, T, H, hd, scale);
+    else  // other geometries (and dev variant 90: the per-(image, head) form for A/B)
+        hipLaunchKernelGGL(probe_attn_kernel, dim3(H * B), dim3(256), 0, as_stream(stream), (const bf16*)q,
+                           (const bf16*)kv, ld_kv, (bf16*)out, ld_out, T, H, hd, scale);
     return mme_check_launch("mme_probe_attention");
 }

@@ -159,6 +159,78 @@ __global__ void resample_v_patch_kernel(const uint8_t* __restrict__ tmp, int n, 
     out[t] = f2bf(normalize(u, na.mean[c], na.stdv[c]));
 }
 
+// Fused patch path (production for MME_PIX_PATCHES): one workgroup per (image, patch row).
+// The input rows that patch row's p output rows need (vertical support included) are
+// staged in LDS once, the horizontal pass fills an LDS u8 raster of those rows x the S
+// cropped columns, and the vertical pass + rescale / normalise (a 256-entry per-channel
+// table of the exact float32 values) writes the patch row's G patches x kpad bf16 -- one
+// contiguous range of the im2col image -- as 16-B stores. The two-kernel path above it
+// stored the h-pass raster to HBM and re-read it byte by byte (7.9x its bytes fetched,
+// ~1 TB/s); same integer arithmetic in the same order, so the output is bit-identical.
+constexpr int FUSED_LDS = 64 * 1024;  // staged input rows + h-pass raster (bytes)
+__global__ __launch_bounds__(256) void resample_patch_fused_kernel(
+    const uint8_t* __restrict__ img, int n, int H, int W, int S, int top, int left, int kx, int ky,
+    const int* __restrict__ xb, const int* __restrict__ xk, const int* __restrict__ yb, const int* __restrict__ yk,
+    NormArgs na, int p, int kpad, bf16* __restrict__ out) {
+    __shared__ __attribute__((aligned(16))) uint8_t buf[FUSED_LDS];
+    __shared__ unsigned short lut[3][256];
+    const int G = S / p;
+    const int b = blockIdx.x / G, py = blockIdx.x % G, tid = threadIdx.x;
+    const int oy0 = py * p + top, oy1 = oy0 + p - 1;
+    const int r0 = yb[2 * oy0], r1 = yb[2 * oy1] + yb[2 * oy1 + 1];  // input rows [r0, r1) (ymin is monotone)
+    const int R = r1 - r0, rowb = W * 3;
+    uint8_t* in_l = buf;                                             // [R][W][3]
+    uint8_t* hr = buf + ((R * rowb + 15) & ~15);                     // [R][S][3]
+    for (int i = tid; i < 3 * 256; i += 256) {
+        const int c = i >> 8, u = i & 255;
+        lut[c][u] = __builtin_bit_cast(unsigned short, f2bf(normalize(u, na.mean[c], na.stdv[c])));
+    }
+    const uint8_t* src = img + ((long)b * H + r0) * rowb;
+    const int nbytes = R * rowb;
+    if ((((uintptr_t)src | (unsigned)nbytes) & 15) == 0) {
+        for (int i = tid; i < nbytes / 16; i += 256)
+            reinterpret_cast<uint4*>(in_l)[i] = reinterpret_cast<const uint4*>(src)[i];
+    } else {
+        for (int i = tid; i < nbytes; i += 256) in_l[i] = src[i];
+    }
+    __syncthreads();
+    for (int i = tid; i < R * S * 3; i += 256) {  // horizontal pass (resample_h_kernel's sums)
+        const int c = i % 3, xc = (i / 3) % S, r = i / (3 * S);
+        const int xx = xc + left;
+        const int xmin = xb[2 * xx], cnt = xb[2 * xx + 1];
+        const int* k = xk + xx * kx;
+        const uint8_t* sp = in_l + r * rowb + xmin * 3 + c;
+        int sum = 1 << (PREC - 1);
+        for (int x = 0; x < cnt; ++x) sum += sp[3 * x] * k[x];
+        hr[i] = (uint8_t)clip8(sum);
+    }
+    __syncthreads();
+    const int P2 = p * p, C3 = 3 * P2;
+    bf16* dst = out + ((long)b * G * G + (long)py * G) * kpad;
+    const int n8 = G * kpad / 8;  // 16-B chunks of the patch row (kpad % 8 == 0)
+    for (int i = tid; i < n8; i += 256) {
+        const int px = (i * 8) / kpad, col0 = (i * 8) % kpad;
+        u16x8 v;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+            const int col = col0 + e;
+            unsigned short o = 0;  // bf16 +0 for the K padding
+            if (col < C3) {
+                const int c = col / P2, kyy = (col / p) % p, kxx = col % p;
+                const int oy = oy0 + kyy, xc = px * p + kxx;
+                const int ymin = yb[2 * oy] - r0, cnt = yb[2 * oy + 1];
+                const int* kk = yk + oy * ky;
+                const uint8_t* hp = hr + ((long)ymin * S + xc) * 3 + c;
+                int sum = 1 << (PREC - 1);
+                for (int y = 0; y < cnt; ++y) sum += hp[(long)y * S * 3] * kk[y];
+                o = lut[c][clip8(sum)];
+            }
+            v[e] = o;
+        }
+        *reinterpret_cast<u16x8*>(dst + (long)i * 8) = v;
+    }
+}
+
 // Plain im2col of pixel_values (the HF-API path: get_image_features(pixel_values)).
 template <typename T>
 __global__ void im2col_kernel(const T* __restrict__ pix, int n, int S, int p, int kpad, bf16* __restrict__ out) {
@@ -180,6 +252,30 @@ __global__ void im2col_kernel(const T* __restrict__ pix, int n, int S, int p, in
 }
 
 size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
+
+// Host restatement of coeffs_kernel's bounds (same IEEE double operations, no contraction):
+// the largest number of input rows one patch row of the fused kernel stages.
+#pragma clang fp contract(off)
+int fused_max_rows(int in, int out, int S, int top, int p) {
+    const double scale = (double)in / out;
+    const double fs = scale < 1.0 ? 1.0 : scale;
+    const double support = 2.0 * fs;
+    auto bounds = [&](int yy, int& lo, int& hi) {
+        const double center = (yy + 0.5) * scale;
+        lo = (int)(center - support + 0.5);
+        if (lo < 0) lo = 0;
+        hi = (int)(center + support + 0.5);
+        if (hi > in) hi = in;
+    };
+    int best = 0;
+    for (int py = 0; py < S / p; ++py) {
+        int lo0, hi0, lo1, hi1;
+        bounds(py * p + top, lo0, hi0);
+        bounds(py * p + top + p - 1, lo1, hi1);
+        best = best > hi1 - lo0 ? best : hi1 - lo0;
+    }
+    return best;
+}
 
 }  // namespace
 
@@ -219,14 +315,23 @@ extern "C" int mme_preprocess_u8(const uint8_t* imgs, int n, int H, int W, int r
 
     hipLaunchKernelGGL(coeffs_kernel, dim3(cdiv(rw, 64)), dim3(64), 0, s, W, rw, kx, xb, xk);
     hipLaunchKernelGGL(coeffs_kernel, dim3(cdiv(rh, 64)), dim3(64), 0, s, H, rh, ky, yb, yk);
-    const long th = (long)n * H * S;
-    hipLaunchKernelGGL(resample_h_kernel, dim3(cdiv(th, 256)), dim3(256), 0, s, imgs, n, H, W, S, left, kx, xb, xk,
-                       tmp);
     NormArgs na;
     for (int c = 0; c < 3; ++c) {
         na.mean[c] = mean3[c];
         na.stdv[c] = std3[c];
     }
+    if (out_kind == MME_PIX_PATCHES) {
+        const int R = fused_max_rows(H, rh, S, top, patch);
+        if ((((long)R * W * 3 + 15) & ~15L) + (long)R * S * 3 <= FUSED_LDS) {
+            const int G = S / patch;
+            hipLaunchKernelGGL(resample_patch_fused_kernel, dim3(n * G), dim3(256), 0, s, imgs, n, H, W, S, top, left,
+                               kx, ky, xb, xk, yb, yk, na, patch, kpad, (bf16*)out);
+            return mme_check_launch("mme_preprocess_u8");
+        }
+    }
+    const long th = (long)n * H * S;
+    hipLaunchKernelGGL(resample_h_kernel, dim3(cdiv(th, 256)), dim3(256), 0, s, imgs, n, H, W, S, left, kx, xb, xk,
+                       tmp);
     if (out_kind == MME_PIX_F32_NCHW) {
         const long tv = (long)n * 3 * S * S;
         hipLaunchKernelGGL(resample_v_nchw_kernel, dim3(cdiv(tv, 256)), dim3(256), 0, s, tmp, n, H, S, top, ky, yb,

@@ -216,7 +216,9 @@ def test_attention_strided_qkv(cuda):
                                atol=2e-2, rtol=2e-2)
 
 
-@pytest.mark.parametrize("B,T,H,hd", [(3, 729, 16, 72), (2, 49, 8, 72)])
+# (image, all heads) blocks for H * hd <= 1152 (SigLIP MAP head: 16 x 72); per-(image, head)
+# blocks otherwise (H = 5: 256 % H != 0)
+@pytest.mark.parametrize("B,T,H,hd", [(3, 729, 16, 72), (2, 49, 8, 72), (239, 729, 16, 72), (2, 100, 5, 64)])
 def test_probe_attention(cuda, B, T, H, hd):
     g = torch.Generator(device="cuda").manual_seed(T)
     d = H * hd

@@ -32,7 +32,9 @@ def test_preprocess_pixel_values_bit_exact(cuda, golden, case):
         f"{case}: {np.sum(got != ref)} pixel values differ from PIL+HF"
 
 
-@pytest.mark.parametrize("case", ["siglip384", "clip336"])
+# patches: the fused kernel (one workgroup per patch row, LDS-staged rows) at every golden
+# geometry (S % 14 != 0 for SigLIP 384 and DFN5B 378: the last pixels feed no patch)
+@pytest.mark.parametrize("case", CASES)
 def test_preprocess_patches_match_im2col(cuda, golden, case):
     g = golden("preprocess")
     H, W, S, kind = (int(v) for v in g[case + "_meta"])
@@ -55,3 +57,30 @@ def test_preprocess_batch_of_synthetic(cuda):
     for i in range(6):
         ref = pil_bicubic.normalize(pil_bicubic.preprocess_u8(imgs[i], 384, "square"), ip.mean, ip.std)
         assert np.array_equal(pv[i], ref)
+
+
+def test_preprocess_patches_large_downscale_fallback(cuda):
+    """A 1500 x 1300 image to 224 (CLIP shortest edge + crop): a patch row needs more input rows
+    than the fused kernel stages in LDS, so the two-kernel path runs; both equal im2col of the
+    bit-exact pixel values."""
+    rng = np.random.default_rng(3)
+    imgs = rng.integers(0, 256, (2, 1500, 1300, 3), dtype=np.uint8)
+    ip = _cfg(1, 224)
+    rh, rw, top, left = image_geometry(1500, 1300, ip)
+    x = torch.from_numpy(imgs).cuda()
+    patches = ops.preprocess_u8(x, resize=(rh, rw), crop=(top, left), size=224, mean=ip.mean, std=ip.std,
+                                patch=14, kpad=640)
+    pv = ops.preprocess_u8(x, resize=(rh, rw), crop=(top, left), size=224, mean=ip.mean, std=ip.std)
+    assert torch.equal(patches, ops.im2col(pv, 14, 640))
+    ref = pil_bicubic.normalize(pil_bicubic.preprocess_u8(imgs[1], 224, "shortest_edge"), ip.mean, ip.std)
+    assert np.array_equal(pv[1].cpu().numpy(), ref)
+
+
+def test_preprocess_patches_batch_vs_pixel_values(cuda):
+    """The production batch shape (SigLIP 384, 40 images): fused patches == im2col(pixel_values)."""
+    rng = np.random.default_rng(12)
+    x = torch.from_numpy(rng.integers(0, 256, (40, 224, 224, 3), dtype=np.uint8)).cuda()
+    ip = _cfg(0, 384)
+    kw = dict(resize=(384, 384), crop=(0, 0), size=384, mean=ip.mean, std=ip.std)
+    patches = ops.preprocess_u8(x, patch=14, kpad=640, **kw)
+    assert torch.equal(patches, ops.im2col(ops.preprocess_u8(x, **kw), 14, 640))
