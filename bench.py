@@ -145,7 +145,7 @@ def retrieval_parity(tables, metrics, caps_per_image: int = 5):
     from oracle import retrieval as R
     from mme import ops
     t0 = time.time()
-    host = {k: v.float().cpu().numpy() for k, v in tables.items()}
+    host = {k: tables[k].float().cpu().numpy() for k in ("img", "t2i", "all")}
     n = host["img"].shape[0]
     rows = {}
     ref_metrics = {}
@@ -216,13 +216,23 @@ def colpali_parity(tables, scores, caps_per_image: int = 5, n_t2i: int = 50, n_i
         ridx = {kk: TT.topk(ref, kk)[0] for kk in ks}
         hit = lambda ix: np.stack([(ix[kk] // tc == rows[:, None]).any(1) for kk in ks], 1)
         dev = dev.cpu().numpy()
-        r = {"rows_sampled": int(len(rows)), "scores_identical": int((dev == ref).all(1).sum()),
-             "top10_identical": int((didx[ks[-1]] == ridx[ks[-1]]).all(1).sum()),
-             "hit_rows_identical": int((hit(didx) == hit(ridx)).all(1).sum())}
-        ok &= r["scores_identical"] == r["top10_identical"] == r["hit_rows_identical"] == len(rows)
+        ulp = np.abs(torch.from_numpy(dev).to(torch.bfloat16).view(torch.int16).int().numpy()
+                     - torch.from_numpy(ref).to(torch.bfloat16).view(torch.int16).int().numpy())
+        top11 = lambda x: -np.sort(-x, 1)[:, :11]
+        same_top = (top11(dev) == top11(ref)).all(1)
+        same_idx = (didx[ks[-1]] == ridx[ks[-1]]).all(1)
+        same_hit = (hit(didx) == hit(ridx)).all(1)
+        r = {"rows_sampled": int(len(rows)), "scores_max_ulp": int(ulp.max()),
+             "scores_identical_frac": round(float((ulp == 0).mean()), 6),
+             "rows_top11_identical": int(same_top.sum()), "top10_identical": int(same_idx.sum()),
+             "hit_rows_identical": int(same_hit.sum())}
+        # a CPU bf16 GEMM and the MFMA sum a dot product's 128 fp32 products in different orders, so a
+        # score may round 1 bf16 ulp apart; every row whose top-11 values agree must rank identically
+        ok &= r["scores_max_ulp"] <= 1 and bool((same_idx | ~same_top).all()) and bool((same_hit | ~same_top).all())
         out[name] = r
-    return {"sampled_rows_identical": bool(ok), "rows": out,
-            "rule": "scores bit-identical; top-10 in torch.topk's CPU order; hit/miss at k = 1, 5, 10",
+    return {"parity_ok": bool(ok), "rows": out,
+            "rule": "scores <= 1 bf16 ulp apart; rows whose top-11 agree: top-10 in torch.topk's CPU order and "
+                    "hit/miss at k = 1, 5, 10 identical",
             "checker": "oracle/maxsim.py chunk loop (reference main.py:451-470) on the job's own multi-vectors, host",
             "full_geometry_pin": "tests/test_gpu_colpali.py::test_colpali_full_geometry_vs_reference "
                                  "(1 000 x 5 000 vs the reference's own scores and recall)",
@@ -489,11 +499,18 @@ def main():
     # phases of the last timed step (device events on the launch stream), max over ranks
     phases = torch.tensor([ev["t0"].elapsed_time(ev["img"]), ev["img"].elapsed_time(ev["txt"]),
                            ev["txt"].elapsed_time(ev["ret"])], dtype=torch.float64, device=dev)
+    gev = last["tables"].get("gather_events")
+    gather_ms = gev[0].elapsed_time(gev[1]) if gev is not None else 0.0
+    allgather_per_rank = [round(gather_ms / 1e3, 5)]
     if world > 1:
         t = torch.tensor([dt], device=dev)
         all_reduce_(t, dist.ReduceOp.MAX)
         dt = float(t.item())
         all_reduce_(phases, dist.ReduceOp.MAX)
+        g_all = torch.zeros(world, dtype=torch.float64, device=dev)
+        g_all[rank] = gather_ms / 1e3
+        all_reduce_(g_all, dist.ReduceOp.SUM)
+        allgather_per_rank = [round(x, 5) for x in g_all.tolist()]
     phases = phases.tolist()
     kt = ops.KernelTimer.summary() if not args.no_kernel_timer else {}
 
@@ -555,6 +572,9 @@ def main():
         # I2T-Sym similarity + fused top-10 + recall counters + counter all-reduce
         "encode_images_s": round(phases[0] / 1e3, 4), "encode_texts_s": round(phases[1] / 1e3, 4),
         "retrieval_s": round(phases[2] / 1e3, 4),
+        # per rank, last timed step: the RCCL all-gathers of the image / T2I / caption tables
+        # (device events around them; 0 at N = 1 where nothing is gathered)
+        "allgather_s_per_rank": allgather_per_rank,
         "roofline": roofline,
         "parity": None,
         "cpu_baseline": None,

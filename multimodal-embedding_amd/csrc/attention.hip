@@ -1841,7 +1841,9 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(2))) vo
 //   O^T (16x16 tiles): lane l holds query 16 u + (l & 15), rows 4 g + reg of each d-tile;
 //   the running max lives with the S^T lanes, so the (lazy) rescale shuffles alpha over.
 // ---------------------------------------------------------------------------
-template <int HD, int NW, int MINW, bool PRIO, bool SKIP = false>
+// SKIP: 0 none; 1 = a tile whose second 32-key block lies wholly past the keys skips that
+// block's MFMAs (kind 62); 2 = the same with literal-zero accumulator starts (kind 63).
+template <int HD, int NW, int MINW, bool PRIO, int SKIP = 0>
 __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(MINW))) void attn_hyb_kernel(AttnArgs a) {
     static_assert(HD == 72 || HD == 80, "80-deep QK^T, 80 PV rows");
     constexpr bool ONES = HD == 72;  // hd 72: V^T row 72 = ones (weight sums); hd 80: f32 sums
@@ -1936,6 +1938,32 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(MINW)))
         // at T = 729) skips that block's QK^T and PV MFMAs; its P is 0 either way (bit-identical)
         const bool half = SKIP && t * 64 + 32 >= Tk;
         f32x16 sc[2];
+        if (SKIP == 2) {
+            // SKIP 2: both QK^T chains start from a literal-zero accumulator (no register init);
+            // only the skipped half of the last tile fills its scores with -inf
+#pragma unroll
+            for (int kb = 0; kb < 2; ++kb) {
+                if (kb == 1 && half) {
+                    // volatile: hipcc would otherwise hoist these fills into every tile (and let
+                    // the MFMAs overwrite them), which is the register init SKIP 2 removes
+#pragma unroll
+                    for (int e = 0; e < 16; ++e) {
+                        float f;
+                        asm volatile("v_mov_b32 %0, 0xff800000" : "=v"(f));
+                        sc[1][e] = f;
+                    }
+                } else {
+                    f32x16 z = {};
+#pragma unroll
+                    for (int ks = 0; ks < NKS; ++ks) {
+                        const bf16x8 kf =
+                            *reinterpret_cast<const LDS_AS bf16x8*>((uintptr_t)(kb0 + so + kb * 512 + ks * 2048));
+                        z = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[ks], z, 0, 0, 0);
+                    }
+                    sc[kb] = z;
+                }
+            }
+        } else {
 #pragma unroll
         for (int kb = 0; kb < 2; ++kb) {
             f32x16 z;
@@ -1951,6 +1979,7 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(MINW)))
                 z = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[ks], z, 0, 0, 0);
             }
             sc[kb] = z;
+        }
         }
         if ((t * 64 + 64 > Tk) || (a.causal && t * 64 + 63 > qw0)) {
             const int q = qw0 + r;
@@ -2251,7 +2280,7 @@ bool launch_attn(int kind, const AttnArgs& a, int B, int T, int H, hipStream_t s
     else if (kind == 62) {  // attn_hyb_kernel skipping a tile's second key block when it lies past the keys:
                             // production for hd 72
         if constexpr (HD != 64)
-            hipLaunchKernelGGL((attn_hyb_kernel<HD, 8, 4, true, true>), dim3(cdiv(T, 256) * H * B), dim3(512), 0, st, a);
+            hipLaunchKernelGGL((attn_hyb_kernel<HD, 8, 4, true, 1>), dim3(cdiv(T, 256) * H * B), dim3(512), 0, st, a);
         else
             hipLaunchKernelGGL((attn_m32_kernel<HD, 8, 1, true>), dim3(cdiv(T, 256) * H * B), dim3(512), 0, st, a);
     } else
@@ -2382,6 +2411,11 @@ bool launch_attn_dev(int kind, const AttnArgs& a, int B, int T, int H, hipStream
         } else {
             hipLaunchKernelGGL((attn_m32_kernel<HD, 8, 1, true>), dim3(cdiv(T, 256) * H * B), dim3(512), 0, st, a);
         }
+    } else if (kind == 63) {  // kind 62 with literal-zero QK^T accumulator starts (no per-tile register init)
+        if constexpr (HD != 64)
+            hipLaunchKernelGGL((attn_hyb_kernel<HD, 8, 4, true, 2>), dim3(cdiv(T, 256) * H * B), dim3(512), 0, st, a);
+        else
+            hipLaunchKernelGGL((attn_m32_kernel<HD, 8, 1, true>), dim3(cdiv(T, 256) * H * B), dim3(512), 0, st, a);
     } else if (kind == 12)  // dev: pipelined + lazy + ones
         hipLaunchKernelGGL((attn_pipe_kernel<HD, 8, 3, true, HD == 72, true>), dim3(cdiv(T, 256) * H * B), dim3(512), 0, st, a);
     else if (kind == 2)
@@ -2502,10 +2536,10 @@ extern "C" int mme_probe_attention(const void* q, const void* kv, int ld_kv, voi
     if (B == 0) return MME_OK;
     const int D = H * hd, TR = H <= 16 && 256 % H == 0 ? 256 / H : 0;
     if (TR && D <= PROBE2_D && D % 8 == 0 && (TR * D / 8) % 64 == 0 && hd % 8 == 0 && ld_kv % 8 == 0 &&
-        ld_out % 8 == 0 && ((uintptr_t)out & 15) == 0 && ((uintptr_t)kv & 15) == 0 && g_attn_variant != 90)
+        ld_out % 8 == 0 && ((uintptr_t)out & 15) == 0 && ((uintptr_t)kv & 15) == 0 && g_attn_variant != 200)
         hipLaunchKernelGGL(probe_attn_img_kernel, dim3(B), dim3(256), 0, as_stream(stream), (const bf16*)q,
                            (const bf16*)kv, ld_kv, (bf16*)out, ld_out, T, H, hd, scale);
-    else  // other geometries (and dev variant 90: the per-(image, head) form for A/B)
+    else  // other geometries (and dev variant 200: the per-(image, head) form for A/B)
         hipLaunchKernelGGL(probe_attn_kernel, dim3(H * B), dim3(256), 0, as_stream(stream), (const bf16*)q,
                            (const bf16*)kv, ld_kv, (bf16*)out, ld_out, T, H, hd, scale);
     return mme_check_launch("mme_probe_attention");

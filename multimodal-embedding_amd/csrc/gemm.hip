@@ -1161,6 +1161,190 @@ __device__ __forceinline__ void pipe8_tile(const GemmArgs& p, char* lds, const i
     }
 }
 
+// ---------------------------------------------------------------------------
+// pipe9: pipe8's LDS ring, ping-pong schedule, K order and per-wave epilogue (so the outputs
+// are bit-identical), with the scalar / vector bookkeeping of a stage taken out of the loop.
+// pipe8's loop spent ~75 SALU and ~10 VALU per 64 MFMAs on it (h % 5 slot arithmetic by
+// multiply-high, an A / B operand select per DMA piece, a VALU add of the K offset to every
+// piece's address, runtime wait-count branches for the two wave rows): rocprofv3 counted more
+// SALU than MFMA instructions (profiles/r02_pmc_gemm_util_fc1.json). Here
+//   * the two wave rows run separate instantiations (LATE), so every wait count and barrier
+//     is static;
+//   * stages are unrolled by the ring period (5): each stage's ring slots are immediates;
+//     stage 0 and the last two stages (which issue fewer units) are peeled, so the steady
+//     state issues both units unconditionally;
+//   * the DMA pieces are buffer_load_dwordx4 ... lds with the per-lane row offsets in
+//     VGPRs fixed for the tile and the K offset in soffset (one SGPR add per stage), M0
+//     stepped by s_add.
+// ---------------------------------------------------------------------------
+typedef int i32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ i32x4 raw_rsrc(const void* base, unsigned bytes) {
+    const unsigned long long b = (unsigned long long)(uintptr_t)base;
+    i32x4 r;
+    r[0] = __builtin_amdgcn_readfirstlane((int)(unsigned)b);
+    r[1] = __builtin_amdgcn_readfirstlane((int)(unsigned)(b >> 32));
+    r[2] = __builtin_amdgcn_readfirstlane((int)bytes);
+    r[3] = 0x00020000;  // raw buffer, dword data format (gfx9)
+    return r;
+}
+// four 1 KiB LDS-DMA pieces: LDS m0base + q KiB <- rsrc base + voff[q] + soff
+__device__ __forceinline__ void dma4(unsigned m0base, const unsigned (&voff)[4], i32x4 rsrc, unsigned soff) {
+    asm volatile(
+        "s_mov_b32 m0, %0\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %5, %6 offen lds\n\t"
+        "s_add_u32 m0, m0, 0x400\n\ts_nop 0\n\tbuffer_load_dwordx4 %2, %5, %6 offen lds\n\t"
+        "s_add_u32 m0, m0, 0x400\n\ts_nop 0\n\tbuffer_load_dwordx4 %3, %5, %6 offen lds\n\t"
+        "s_add_u32 m0, m0, 0x400\n\ts_nop 0\n\tbuffer_load_dwordx4 %4, %5, %6 offen lds"
+        ::"s"(m0base), "v"(voff[0]), "v"(voff[1]), "v"(voff[2]), "v"(voff[3]), "s"(rsrc), "s"(soff)
+        : "memory", "m0");
+}
+
+template <class C, int ACT, bool LATE>
+__device__ __forceinline__ void pipe9_tile(const GemmArgs& p, char* lds, const int m0, const int n0, const int wave) {
+    static_assert(C::BM == 256 && C::BN == 256 && C::FN == 4 && C::FM == 8 && C::NW == 8, "pipe9: 256 x 256, 8 waves");
+    constexpr int UNIT = 32768;
+    const int lane = threadIdx.x & 63;
+    const int wm = wave / C::WN, wn = wave % C::WN;
+    const int g = lane >> 4, li = lane & 15;
+
+    unsigned offA[4], offB[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const int prow = (wave * 4 + q) * 8 + (lane >> 3);
+        const int logical = swz(prow, lane & 7);
+        offA[q] = ((unsigned)min(m0 + prow, p.M - 1) * (unsigned)p.lda + logical * 8) * 2u;
+        offB[q] = ((unsigned)min(n0 + prow, p.N - 1) * (unsigned)p.ldb + logical * 8) * 2u;
+    }
+    const i32x4 rA = raw_rsrc(p.A, (unsigned)((size_t)p.M * p.lda * 2));
+    const i32x4 rB = raw_rsrc(p.B, (unsigned)((size_t)p.N * p.ldb * 2));
+    const unsigned lds0 = (unsigned)(uintptr_t)(LDS_AS char*)lds;
+    const unsigned lw = __builtin_amdgcn_readfirstlane(lds0 + wave * 4096);  // this wave's pieces in a unit
+    const int sw = (li >> 1) & 7;
+    const unsigned a_row = lds0 + (wm * C::TM + li) * 128, b_row = lds0 + (wn * C::TN + li) * 128;
+    const unsigned c0 = ((0 + g) ^ sw) << 4, c1 = ((4 + g) ^ sw) << 4;
+    const unsigned a0 = a_row + c0, a1 = a_row + c1, b0 = b_row + c0, b1 = b_row + c1;
+
+    f32x4 acc[C::FM][C::FN];
+#pragma unroll
+    for (int i = 0; i < C::FM; ++i)
+#pragma unroll
+        for (int j = 0; j < C::FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    bf16x8 b[C::FN], a[8];
+    const int nk = p.K / 64;
+
+    // one 32-deep step: memory phase (12 fragment reads, optionally 4 DMA pieces), barrier,
+    // compute phase (32 MFMAs), barrier. wm_ / wc_: vmcnt kept after the memory / compute phase
+    // (-1: no wait).
+    auto step = [&](unsigned aa, unsigned bb, bool dma, unsigned m0base, const unsigned (&voff)[4], i32x4 rs,
+                    unsigned soff, int wm_, int wc_, bool end_barrier) __attribute__((always_inline)) {
+        ds_read16<0>(b[0], bb);
+        ds_read16<2048>(b[1], bb);
+        ds_read16<4096>(b[2], bb);
+        ds_read16<6144>(b[3], bb);
+        ds_read16<0>(a[0], aa);
+        ds_read16<2048>(a[1], aa);
+        ds_read16<4096>(a[2], aa);
+        ds_read16<6144>(a[3], aa);
+        ds_read16<8192>(a[4], aa);
+        ds_read16<10240>(a[5], aa);
+        ds_read16<12288>(a[6], aa);
+        ds_read16<14336>(a[7], aa);
+        if (dma) dma4(m0base, voff, rs, soff);
+        if (wm_ == 0) vm_wait<0>();
+        else if (wm_ == 4) vm_wait<4>();
+        lgkm_wait<0>();
+        __builtin_amdgcn_s_barrier();
+        __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+#pragma unroll
+            for (int j = 0; j < C::FN; ++j)
+                acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b[j], a[i], acc[i][j], 0, 0, 0);
+        __builtin_amdgcn_s_setprio(0);
+        __builtin_amdgcn_sched_barrier(0);
+        if (wc_ == 0) vm_wait<0>();
+        else if (wc_ == 4) vm_wait<4>();
+        if (end_barrier) __builtin_amdgcn_s_barrier();
+    };
+    // soffset of the next B unit (stage s + 1) and A unit (stage s + 2), bytes along K
+    unsigned kB = 128, kA = 256;
+    // stage with its A in ring slot sa (B in sa + 1); dB / dA: issue B(s + 1) into slot sa + 3,
+    // A(s + 2) into slot sa + 4 (mod 5); need: pieces this wave may keep in flight at the
+    // barrier before stage s + 1's first reads (-1: no wait, last stage)
+    auto stage = [&](int sa, bool dB, bool dA, int need, bool last) __attribute__((always_inline)) {
+        const int sb = sa == 4 ? 0 : sa + 1;
+        const int iB = sa + 3 >= 5 ? sa - 2 : sa + 3, iA = sa + 4 >= 5 ? sa - 1 : sa + 4;
+        step(a0 + sa * UNIT, b0 + sb * UNIT, dB, lw + iB * UNIT, offB, rB, kB, -1, -1, true);
+        step(a1 + sa * UNIT, b1 + sb * UNIT, dA, lw + iA * UNIT, offA, rA, kA, LATE ? need : -1, LATE ? -1 : need,
+             !(LATE && last));
+        kB += 128;
+        kA += 128;
+    };
+
+    // prologue: units 0..4 (A0 B0 A1 B1 A2) into slots 0..4
+    dma4(lw + 0 * UNIT, offA, rA, 0);
+    dma4(lw + 1 * UNIT, offB, rB, 0);
+    dma4(lw + 2 * UNIT, offA, rA, 128);
+    dma4(lw + 3 * UNIT, offB, rB, 128);
+    dma4(lw + 4 * UNIT, offA, rA, 256);
+    vm_wait<12>();  // units 0 and 1 (stage 0) landed
+    __builtin_amdgcn_s_barrier();
+    if (LATE) __builtin_amdgcn_s_barrier();
+
+    stage(0, false, false, 4, false);  // nk >= 3: stage 1's units (2, 3) retired, unit 4 may fly
+    int s = 1;
+    for (; s + 5 <= nk - 2; s += 5) {  // steady state: s = 1 (mod 5) -> A slots 2, 4, 1, 3, 0
+        stage(2, true, true, 4, false);
+        stage(4, true, true, 4, false);
+        stage(1, true, true, 4, false);
+        stage(3, true, true, 4, false);
+        stage(0, true, true, 4, false);
+    }
+    if (s < nk - 2) {
+        stage(2, true, true, 4, false);
+        if (++s < nk - 2) {
+            stage(4, true, true, 4, false);
+            if (++s < nk - 2) {
+                stage(1, true, true, 4, false);
+                if (++s < nk - 2) {
+                    stage(3, true, true, 4, false);
+                    ++s;
+                }
+            }
+        }
+    }
+    // s = nk - 2: B of the last stage only; s = nk - 1: nothing (ring slots at run time)
+    const int sa2 = (2 * s) % 5, sa1 = sa2 >= 3 ? sa2 - 3 : sa2 + 2;
+    stage(sa2, true, false, 0, false);
+    stage(sa1, false, false, -1, true);
+    vm_wait<0>();
+    gemm_epilogue_wave<C, ACT>(p, lds, acc, m0, n0, wave, wm, wn, g, li, lane);
+}
+
+template <class C, int GROUP_M, int ACT, bool SPLIT>
+__global__ __launch_bounds__(C::NT, 2) void gemm_pipe9_kernel(GemmArgs p) {
+    __shared__ __attribute__((aligned(16))) char lds[5 * 32768];
+    const int nbm = (p.M + C::BM - 1) / C::BM;
+    const int tile = xcd_remap(blockIdx.x, gridDim.x);
+    int m0, n0;
+    if constexpr (SPLIT) {
+        if (split_coords(tile, nbm, p.N / C::BN, m0, n0)) {
+            pipe6_tile<Pipe512x128, ACT, 1, 0>(p, lds, m0, n0);
+            return;
+        }
+    } else {
+        const int nbn = (p.N + C::BN - 1) / C::BN;
+        int bm, bn;
+        tile_coords<GROUP_M>(tile, nbm, nbn, bm, bn);
+        m0 = bm * C::BM;
+        n0 = bn * C::BN;
+    }
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    if (wave >= C::NW / 2)
+        pipe9_tile<C, ACT, true>(p, lds, m0, n0, wave);
+    else
+        pipe9_tile<C, ACT, false>(p, lds, m0, n0, wave);
+}
+
 template <class C, int GROUP_M, int ACT, int DIAG = 0, bool SPLIT = false, bool WEPI = false>
 __global__ __launch_bounds__(C::NT, 2) void gemm_pipe8_kernel(GemmArgs p) {
     __shared__ __attribute__((aligned(16))) char lds[5 * 32768];
@@ -1241,6 +1425,30 @@ int launch_pipe8(const GemmArgs& a, hipStream_t s) {
             break;
         default:
             hipLaunchKernelGGL((gemm_pipe8_kernel<C, GROUP_M, MME_ACT_NONE, DIAG, SPLIT, WEPI>), grid, block, 0, s, a);
+            break;
+    }
+    return mme_check_launch("mme_gemm");
+}
+
+template <class C, int GROUP_M, bool SPLIT>
+int launch_pipe9(const GemmArgs& a, hipStream_t s) {
+    const int nbm = (a.M + C::BM - 1) / C::BM, nbn = (a.N + C::BN - 1) / C::BN;
+    const dim3 grid(SPLIT ? split_tiles(nbm, a.N / C::BN) : nbm * nbn), block(C::NT);
+    switch (a.act) {
+        case MME_ACT_GELU_TANH:
+            hipLaunchKernelGGL((gemm_pipe9_kernel<C, GROUP_M, MME_ACT_GELU_TANH, SPLIT>), grid, block, 0, s, a);
+            break;
+        case MME_ACT_QUICK_GELU:
+            hipLaunchKernelGGL((gemm_pipe9_kernel<C, GROUP_M, MME_ACT_QUICK_GELU, SPLIT>), grid, block, 0, s, a);
+            break;
+        case MME_ACT_GELU_ERF:
+            hipLaunchKernelGGL((gemm_pipe9_kernel<C, GROUP_M, MME_ACT_GELU_ERF, SPLIT>), grid, block, 0, s, a);
+            break;
+        case MME_ACT_GEGLU_TANH:
+            hipLaunchKernelGGL((gemm_pipe9_kernel<C, GROUP_M, MME_ACT_GEGLU_TANH, SPLIT>), grid, block, 0, s, a);
+            break;
+        default:
+            hipLaunchKernelGGL((gemm_pipe9_kernel<C, GROUP_M, MME_ACT_NONE, SPLIT>), grid, block, 0, s, a);
             break;
     }
     return mme_check_launch("mme_gemm");
@@ -2024,6 +2232,10 @@ int gemm_dispatch(GemmArgs a, hipStream_t s) {
         case 67:  // diagnostic: pipe8 without MFMAs
             if (!pipe8_ok(a)) break;
             return launch_pipe8<Pipe256, 4, 2>(a, s);
+        case 80:  // dev: pipe9 (pipe8 without the per-stage scalar bookkeeping; split grid where N = 256 k + 128)
+            if (!pipe8_ok(a)) break;
+            if (N % 256 == 128) return launch_pipe9<Pipe256, 4, true>(a, s);
+            return launch_pipe9<Pipe256, 4, false>(a, s);
         case 54: return launch_pipe6<Pipe256, 2, 1>(a, s);   // dev: 2-row tile bands
         case 55: return launch_pipe6<Pipe256, 16, 1>(a, s);  // dev: 16-row tile bands
         case 50: return launch_pipe7<Pipe256w, 4>(a, s);

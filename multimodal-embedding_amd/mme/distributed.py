@@ -116,17 +116,24 @@ def counts_to_metrics(counts: Sequence[int], n_img: int, ks: Sequence[int] = KS)
 def sharded_recall(img_l: torch.Tensor, t2i_l: torch.Tensor, all_l: torch.Tensor, rank: int, world: int,
                    n_img: int, caps_per_image: int = 5, ks: Sequence[int] = KS, group=None,
                    compute: Optional[object] = None, return_tables: bool = False):
-    """Global R@k from per-rank shards (see module docstring)."""
+    """Global R@k from per-rank shards (see module docstring). With return_tables the tables dict
+    also carries "gather_events": device events around the three all-gathers (None on the CPU)."""
     lo, _ = shard_range(n_img, rank, world)
+    evs = None
+    if img_l.is_cuda:
+        evs = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+        evs[0].record()
     img_all = all_gather_rows(img_l, world, group)
     t2i_all = all_gather_rows(t2i_l, world, group)
     all_all = all_gather_rows(all_l, world, group)
+    if evs is not None:
+        evs[1].record()
     counts = rank_hit_counts(img_l, t2i_l, img_all, t2i_all, all_all, lo, caps_per_image, ks, compute)
     if world > 1:
         all_reduce_(counts, dist.ReduceOp.SUM, group)
     out = counts_to_metrics(counts.tolist(), n_img, ks)
     if return_tables:
-        return out, {"img": img_all, "t2i": t2i_all, "all": all_all}
+        return out, {"img": img_all, "t2i": t2i_all, "all": all_all, "gather_events": evs}
     return out
 
 

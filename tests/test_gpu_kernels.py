@@ -134,7 +134,7 @@ PROD_ATTN_KINDS = (38, 41, 62)  # dispatched by mme_attention; the rest are deve
 
 @pytest.mark.parametrize("kind", [k if k in PROD_ATTN_KINDS else pytest.param(k, marks=pytest.mark.dev)
                                   for k in (38, 39, 40, 41, 42, 43, 44, 45, 46, 47, 48, 49, 50, 51, 52, 54, 55, 56,
-                                            57, 58, 59, 60, 61, 62)])
+                                            57, 58, 59, 60, 61, 62, 63)])
 @pytest.mark.parametrize("B,T,H,hd,causal,lens", [
     (2, 729, 4, 72, False, None),       # SigLIP vision geometry
     (2, 520, 3, 72, False, [520, 301]),  # key padding, partial last tile
@@ -441,3 +441,45 @@ def test_im2col(cuda):
     ref = torch.nn.functional.unfold(pv, 14, stride=14).transpose(1, 2).reshape(2 * 16, 588)
     assert torch.equal(out[:, :588], ref.to(torch.bfloat16))
     assert not out[:, 588:].any()
+
+
+# pipe9 (dev variant 80: pipe8 without the per-stage scalar bookkeeping) is bit-identical to the
+# production pipe8 on every epilogue it takes, at every peeling case of its stage loop
+# (nk = K / 64 = 3 .. 8, 18, 68: empty / partial / full unrolled main loops) and the split grid.
+@pytest.mark.dev
+@pytest.mark.parametrize("M,N,K,epi", [(2048, 1024, 192, "bias"), (1500, 1536, 256, "gelu"), (1000, 1280, 320, "res"),
+                                       (777, 1024, 384, "lnfold"), (2048, 1152, 448, "bias"), (1024, 1024, 512, "res"),
+                                       (4096, 1152, 1152, "res"), (1000, 3456, 1152, "lnfold"),
+                                       (1024, 1152, 4352, "bias"), (3000, 4352, 1152, "gelu")])
+def test_gemm_pipe9_bit_identical_to_pipe8(cuda, M, N, K, epi):
+    import ctypes
+    lib = _lib.load()
+    lib.mme_gemm_variant.argtypes = [ctypes.c_int]
+    g = torch.Generator(device="cuda").manual_seed(M + 2 * N + K)
+    a = rnd(M, K, scale=2.0, gen=g) + 0.5
+    w = rnd(N, K, scale=1 / math.sqrt(K), gen=g)
+    b = rnd(N, scale=0.1, gen=g)
+    x = rnd(M, N, gen=g)
+    if epi == "lnfold":
+        fold = ops.LNFolded(w, b, (1.0 + 0.2 * torch.randn(K, generator=g, device="cuda")).to(torch.bfloat16),
+                            rnd(K, scale=0.1, gen=g))
+        stats = ops.rowstats(a, 1e-6)
+
+    def run():
+        if epi == "bias":
+            return ops.gemm(a, w, b)
+        if epi == "gelu":
+            return ops.gemm(a, w, b, act=_lib.ACT_GELU_TANH)
+        if epi == "res":
+            return ops.gemm(a, w, b, residual=x)
+        return ops.gemm_lnfold(a, fold, stats, act=_lib.ACT_GELU_TANH)
+
+    try:
+        lib.mme_gemm_variant(-1)
+        ref = run()
+        lib.mme_gemm_variant(80)
+        new = run()
+    finally:
+        lib.mme_gemm_variant(-1)
+    torch.cuda.synchronize()
+    assert torch.equal(new, ref), f"pipe9 differs from pipe8 ({epi}, {M}x{N}x{K})"
