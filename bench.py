@@ -57,8 +57,9 @@ def parse():
     p.add_argument("--no-kernel-timer", action="store_true")
     p.add_argument("--no-parity", action="store_true",
                    help="skip the post-run R@1 parity check of the job's embeddings against the oracle")
-    p.add_argument("--host-inputs", action="store_true",
-                   help="also time one job whose u8 images start in host memory (streamed H2D, SURVEY 8f-2); "
+    p.add_argument("--no-host-inputs", dest="host_inputs", action="store_false",
+                   help="skip the extra job whose u8 images start in host memory (streamed H2D, SURVEY 8f-2; "
+                        "the reference's timed region includes its host processor + H2D, main.py:407,534-559); "
                         "reported as host_inputs_img_s, never as value")
     p.add_argument("--bootstrap", type=int, default=0,
                    help="also time N bootstrap resamples of the recall on the device (main.py:586-634; untimed "
@@ -166,6 +167,27 @@ def retrieval_parity(tables, metrics, caps_per_image: int = 5):
             "seconds": round(time.time() - t0, 2)}
 
 
+def encoder_parity(spec, imgs_u8, cap_ids, dev_img, dev_txt, bar: float = 0.999):
+    """Encoder parity of the headline job (checker; after the timed region): the job's own first images
+    and T2I captions encoded by the fp32 oracle (oracle/encoders.py: the PIL-exact processor and the
+    transformers towers restated, validated against main.encode_data) with the job's own weights,
+    against the device embeddings the job produced (cosine per item; the SURVEY §8d bar is 0.999, 0.99 for
+    the mx-fp8 encoder GEMMs)."""
+    sys.path.insert(0, ROOT)
+    from oracle import encoders as oe
+    from mme.weights import random_state_dict
+    t0 = time.time()
+    sd = {k: v.float().cpu() for k, v in random_state_dict(spec, seed=0, device="cuda").items()}
+    oi, ot = oe.encode_data(spec, sd, list(imgs_u8.cpu().numpy()), cap_ids.cpu().tolist(), bs=len(imgs_u8),
+                            out_dtype=torch.float32)
+    cos = lambda a, b: torch.nn.functional.cosine_similarity(a.float().cpu(), b.float(), dim=-1)
+    ci, ct = cos(dev_img, oi), cos(dev_txt, ot)
+    return {"items": int(len(imgs_u8)), "img_cos_min": round(float(ci.min()), 6), "txt_cos_min": round(float(ct.min()), 6),
+            "bar": bar, "ok": bool(ci.min() >= bar and ct.min() >= bar),
+            "checker": "oracle/encoders.py fp32 on the job's own first images / T2I captions and weights",
+            "seconds": round(time.time() - t0, 2)}
+
+
 def colpali_parity(tables, scores, caps_per_image: int = 5, n_t2i: int = 50, n_i2t: int = 10, n_sym: int = 50):
     """MaxSim parity of the ColPali job (checker; runs after the timed region): sampled query rows
     of the job's own multi-vector tables re-scored on the host by the oracle's restatement of the
@@ -262,7 +284,7 @@ def cpu_baseline_colpali(spec, seconds: float, n: int = 1000, caps: int = 5):
     threads = torch.get_num_threads()
     ip = spec.image_proc
     imgs = synthetic_images(4)
-    caps = colpali_captions(64, 1)
+    qcaps = colpali_captions(64, 1)
 
     def enc_img(a):
         pv = torch.from_numpy(pil_bicubic.normalize(pil_bicubic.preprocess_u8(a, ip.size, ip.mode), ip.mean,
@@ -285,8 +307,8 @@ def cpu_baseline_colpali(spec, seconds: float, n: int = 1000, caps: int = 5):
         ni += 1
     ti = time.time() - t0
     t0, nc = time.time(), 0
-    while nc < len(caps) and (nc == 0 or time.time() - t0 < seconds * 0.3):
-        enc_q(caps[nc:nc + 4])
+    while nc < len(qcaps) and (nc == 0 or time.time() - t0 < seconds * 0.3):
+        enc_q(qcaps[nc:nc + 4])
         nc += 4
     tc = time.time() - t0
     from oracle import maxsim as om
@@ -458,6 +480,7 @@ def main():
     my_t2i = my_caps[::caps].contiguous()
     del imgs, ids
     torch.cuda.synchronize()
+    n_enc = min(2, my_imgs.shape[0])
 
     last = {}
     ev = {}
@@ -583,6 +606,9 @@ def main():
                              "same_device": bool(args.same_device)} if world > 1 else None)
     if rank == 0 and not args.no_parity:
         out["parity"] = retrieval_parity(last["tables"], metrics, caps)
+        if n_enc:
+            out["parity"]["encoders"] = encoder_parity(spec, my_imgs[:n_enc], my_t2i[:n_enc], last["img"][:n_enc],
+                                                       last["t2i"][:n_enc], bar=0.99 if args.fp8 else 0.999)
     if args.host_inputs:
         host_imgs = my_imgs.cpu().pin_memory()
         barrier()

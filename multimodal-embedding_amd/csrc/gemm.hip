@@ -2095,8 +2095,8 @@ extern "C" int mme_gemm_res_stats(const void* A, int lda, const void* B, int ldb
         if (rc != MME_OK) return rc;
         return mme_rowstats(Cp, ldc, M, N, eps, row_stats, stream);
     }
-    if (pipe8_ok(a) && g_variant != 47)  // variant 47: pipe6 (tests: pipe8 is bit-identical to it)
-        N % 256 == 128 ? launch_pipe8<Pipe256, 4, 0, true, true>(a, s) : launch_pipe8<Pipe256, 4, 0, false, true>(a, s);
+    if (pipe8_ok(a) && g_variant != 47)  // variant 47: pipe6 (tests: pipe9 / pipe8 are bit-identical to it)
+        N % 256 == 128 ? launch_pipe9<Pipe256, 4, true>(a, s) : launch_pipe9<Pipe256, 4, false>(a, s);
     else
         N % 256 == 128 ? launch_pipe6<Pipe256, 4, 1, 0, true>(a, s) : launch_pipe6<Pipe256, 4, 1>(a, s);
     const int rc = mme_check_launch("mme_gemm_res_stats");
@@ -2143,7 +2143,7 @@ int gemm_dispatch(GemmArgs a, hipStream_t s) {
     if (glu) {  // gated epilogue: the pipelined kernel only (its LDS-staged 16-B tile rows pair gate/up)
         MME_REQUIRE(N % 8 == 0 && ldc % 4 == 0 && !out_f32 && !residual && ((uintptr_t)Cp & 7) == 0,
                     "mme_gemm: GeGLU needs N %% 8 == 0, ldc %% 4 == 0, 8-B aligned bf16 C, no residual");
-        if (pipe8_ok(a) && g_variant != 47) return launch_pipe8<Pipe256, 4, 0, false, true>(a, s);
+        if (pipe8_ok(a) && g_variant != 47) return launch_pipe9<Pipe256, 4, false>(a, s);
         return launch_pipe6<Pipe256, 4, 1>(a, s);
     }
     switch (g_variant) {
@@ -2256,9 +2256,11 @@ int gemm_dispatch(GemmArgs a, hipStream_t s) {
         // N = 256 k + 128: split grid (fc2 1144 -> 1200 TF/s, o_proj +5 %, QKV +1.6 %)
         // with the per-wave epilogue (no workgroup barrier; +1-2 %, bit-identical,
         // profiles/r02_pipe8_wave_epilogue_ab.log); mme_gemm_res_stats uses it too
+        // round 3: pipe9 = pipe8 without the per-stage scalar bookkeeping (bit-identical; +1-7 % per
+        // shape and epilogue, profiles/r03_v4_gemm_*.log)
         if (pipe8_ok(a)) {
-            if (N % 256 == 128) return launch_pipe8<Pipe256, 4, 0, true, true>(a, s);
-            return launch_pipe8<Pipe256, 4, 0, false, true>(a, s);
+            if (N % 256 == 128) return launch_pipe9<Pipe256, 4, true>(a, s);
+            return launch_pipe9<Pipe256, 4, false>(a, s);
         }
         if (N % 256 == 128) return launch_pipe6<Pipe256, 4, 1, 0, true>(a, s);
         return launch_pipe6<Pipe256, 4, 1>(a, s);

@@ -1,0 +1,29 @@
+#!/usr/bin/env python3
+"""Attribute kernel dispatches of a rocprofv3 kernel trace (bench.py --steps K --warmup W) to the
+bench phases: every mme_sim_topk launch is listed in dispatch order with its duration, start time
+and phase (warmup / timed step / post-timed parity checker: bench.py runs sim_topk 3 times per job
+step and 3 more times in retrieval_parity after the timed region).
+
+usage: trace_phases.py <kernel_trace.csv> <warmup> <steps>"""
+import csv
+import json
+import sys
+
+
+def main(path, warmup, steps):
+    rows = list(csv.DictReader(open(path)))
+    t0 = min(int(r["Start_Timestamp"]) for r in rows)
+    sim = [r for r in rows if "sim_topk_kernel" in r["Kernel_Name"]]
+    sim.sort(key=lambda r: int(r["Dispatch_Id"]))
+    out = []
+    for i, r in enumerate(sim):
+        job = i // 3
+        phase = "warmup" if job < warmup else ("timed" if job < warmup + steps else "parity (post-timed)")
+        out.append({"dispatch": int(r["Dispatch_Id"]), "phase": phase,
+                    "ms": round((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6, 3),
+                    "start_s": round((int(r["Start_Timestamp"]) - t0) / 1e9, 3)})
+    print(json.dumps({"sim_topk_dispatches": out}, indent=1))
+
+
+if __name__ == "__main__":
+    main(sys.argv[1], int(sys.argv[2]), int(sys.argv[3]))
