@@ -401,7 +401,7 @@ def main_colpali(args, rank, world, dev):
     if "gemm" in kt:
         gk = kt["gemm"]
         achieved = gk["flops"] / (gk["ms"] / 1e3) / 1e12
-        roofline = {"bound": "mfma", "kernel": "mme_gemm (gemm_pipe8_kernel)", "achieved": round(achieved, 1),
+        roofline = {"bound": "mfma", "kernel": "mme_gemm (gemm_pipe9_kernel)", "achieved": round(achieved, 1),
                     "peak": MFMA_BF16_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": round(achieved / MFMA_BF16_PEAK_TFLOPS, 4),
                     "traffic": None, "launches": gk["launches"], "avg_launch_ms": round(gk["ms"] / gk["launches"], 4),
                     "algorithmic_bytes_per_launch": round(gk["bytes"] / gk["launches"]),
@@ -540,7 +540,7 @@ def main():
     roofline = None
     fam = "gemm_mx" if args.fp8 else "gemm"
     if fam in kt:
-        # dominant kernel family: mme_gemm (gemm_pipe8_kernel; gemm_pipe6_kernel where K % 64 != 0;
+        # dominant kernel family: mme_gemm (gemm_pipe9_kernel; gemm_pipe6_kernel where K % 64 != 0;
         # gemm_tn_kernel for the few small shapes),
         # or with --fp8 mme_gemm_mx (gemm_mx_kernel, block-scaled fp8 MFMA; dense fp8 peak).
         # achieved = algorithmic FLOPs per launch (2*M*N*K, zero-padding excluded) / average launch time
@@ -550,7 +550,7 @@ def main():
         achieved = g["flops"] / (g["ms"] / 1e3) / 1e12
         peak = MFMA_FP8_PEAK_TFLOPS if args.fp8 else MFMA_BF16_PEAK_TFLOPS
         roofline = {"bound": "mfma",
-                    "kernel": "mme_gemm_mx (gemm_mx_kernel)" if args.fp8 else "mme_gemm (gemm_pipe8_kernel)",
+                    "kernel": "mme_gemm_mx (gemm_mx_kernel)" if args.fp8 else "mme_gemm (gemm_pipe9_kernel)",
                     "achieved": round(achieved, 1), "peak": peak, "unit": "TFLOP/s", "frac": round(achieved / peak, 4),
                     "traffic": None, "launches": g["launches"], "avg_launch_ms": round(avg_ms, 4),
                     "algorithmic_bytes_per_launch": round(g["bytes"] / g["launches"]),

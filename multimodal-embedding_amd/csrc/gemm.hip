@@ -1195,7 +1195,7 @@ __device__ __forceinline__ void dma4(unsigned m0base, const unsigned (&voff)[4],
         "s_add_u32 m0, m0, 0x400\n\ts_nop 0\n\tbuffer_load_dwordx4 %3, %5, %6 offen lds\n\t"
         "s_add_u32 m0, m0, 0x400\n\ts_nop 0\n\tbuffer_load_dwordx4 %4, %5, %6 offen lds"
         ::"s"(m0base), "v"(voff[0]), "v"(voff[1]), "v"(voff[2]), "v"(voff[3]), "s"(rsrc), "s"(soff)
-        : "memory", "m0");
+        : "memory", "m0", "scc");  // s_add_u32 writes SCC
 }
 
 template <class C, int ACT, bool LATE>

@@ -399,6 +399,275 @@ __global__ __launch_bounds__(512, 2) void gemm_mx_kernel(MxArgs p) {
     }
 }
 
+// ---------------------------------------------------------------------------
+// mx9 (production for K % 128 == 0, N % 256 == 0; round 3): the block-scaled fp8 GEMM on
+// whole-line LDS-DMA rows. gemm_mx_kernel stages 64-deep fp8 stages as 64-B half-line
+// rows (16 rows x 64 B per 1 KiB piece), the piece shape the LDS-DMA path moves at about
+// half the rate of whole 128-B lines (tools/probes/dma_bw.hip); at the fp8 MFMA rate that
+// path was the bound (1.65 PF/s). Here a stage is 128 fp8 deep, so every A / B row of a
+// stage is one 128-B line (pieces of 8 rows x 128 B, XOR-swizzled as pipe8:
+// chunk ^ ((row >> 1) & 7)), and runs as two 64-deep steps of pipe6 / pipe9's ping-pong
+// (memory phase | barrier | compute phase | barrier, the second wave row one phase behind).
+// LDS: two stage slots of A and B (4 x 32 KiB) + two 2 KiB scale slots ([A kb0..3][B kb0..3],
+// 256 rows each). During stage s every wave issues stage s + 1 (its 8 data pieces; waves 0 / 1
+// also the A / B scale piece) in its first memory phase, into the slot stage s - 1 released;
+// the early row retires them after its last compute phase of stage s, the late row before
+// the barrier closing its last memory phase (2.5 - 3.5 phases after issue). Static slots
+// (stage loop unrolled by 2), DMA by buffer_load ... lds with the K offset in soffset.
+// Per-wave epilogue (no workgroup barrier), bf16 + residual or mx8 re-quantisation.
+// ---------------------------------------------------------------------------
+typedef int i32x4v __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ i32x4v mx_rsrc(const void* base, unsigned bytes) {
+    const unsigned long long b = (unsigned long long)(uintptr_t)base;
+    i32x4v r;
+    r[0] = __builtin_amdgcn_readfirstlane((int)(unsigned)b);
+    r[1] = __builtin_amdgcn_readfirstlane((int)(unsigned)(b >> 32));
+    r[2] = __builtin_amdgcn_readfirstlane((int)bytes);
+    r[3] = 0x00020000;
+    return r;
+}
+__device__ __forceinline__ void mx_dma4(unsigned m0base, const unsigned (&voff)[4], i32x4v rsrc, unsigned soff) {
+    asm volatile(
+        "s_mov_b32 m0, %0\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %5, %6 offen lds\n\t"
+        "s_add_u32 m0, m0, 0x400\n\ts_nop 0\n\tbuffer_load_dwordx4 %2, %5, %6 offen lds\n\t"
+        "s_add_u32 m0, m0, 0x400\n\ts_nop 0\n\tbuffer_load_dwordx4 %3, %5, %6 offen lds\n\t"
+        "s_add_u32 m0, m0, 0x400\n\ts_nop 0\n\tbuffer_load_dwordx4 %4, %5, %6 offen lds"
+        ::"s"(m0base), "v"(voff[0]), "v"(voff[1]), "v"(voff[2]), "v"(voff[3]), "s"(rsrc), "s"(soff)
+        : "memory", "m0", "scc");  // s_add_u32 writes SCC
+}
+__device__ __forceinline__ void mx_dma1(unsigned m0base, unsigned voff, i32x4v rsrc, unsigned soff) {
+    asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, %3 offen lds"
+                 ::"s"(m0base), "v"(voff), "s"(rsrc), "s"(soff) : "memory", "m0", "scc");
+}
+
+constexpr int MX9_UNIT = 32768, MX9_SC = 4 * MX9_UNIT, MX9_PITCH = 144;
+constexpr int MX9_LDS = 8 * 128 * MX9_PITCH;  // per-wave epilogue tiles; the main loop uses less
+static_assert(MX9_SC + 4096 + 5 * 1024 + 2048 + 1024 <= MX9_LDS, "mx9: scale slots + scratch pieces fit");
+
+template <int ACT, bool LATE>
+__device__ __forceinline__ void mx9_tile(const MxArgs& p, char* lds, const int m0, const int n0, const int wave) {
+    constexpr int TM = 128, TN = 64;
+    const int lane = threadIdx.x & 63;
+    const int wm = wave / 4, wn = wave % 4;
+    const int h = lane >> 5, r32 = lane & 31;
+
+    unsigned offA[4], offB[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const int prow = (wave * 4 + q) * 8 + (lane >> 3);
+        const int logical = (lane & 7) ^ ((prow >> 1) & 7);
+        offA[q] = (unsigned)min(m0 + prow, p.M - 1) * (unsigned)p.lda + logical * 16;
+        offB[q] = (unsigned)min(n0 + prow, p.N - 1) * (unsigned)p.ldb + logical * 16;
+    }
+    const int K = p.K, nk = K / 128;
+    const i32x4v rA = mx_rsrc(p.A, (unsigned)((size_t)p.M * p.lda));
+    const i32x4v rB = mx_rsrc(p.B, (unsigned)((size_t)p.N * p.ldb));
+    // scale piece (waves 0 / 1: A / B): lane l -> block kb = l / 16 of the stage, 16 rows (l % 16) * 16..
+    // waves 2..7: a zero-length range (no memory traffic) into LDS past the scale slots
+    const bool sc_wave = wave < 2;
+    const int sc_rows = wave == 0 ? p.sa_rows : p.sb_rows;
+    const i32x4v rS = mx_rsrc(wave == 0 ? (const void*)p.sa : (const void*)p.sb,
+                              sc_wave ? (unsigned)((size_t)(K / 32) * sc_rows) : 0u);
+    const unsigned voS = (unsigned)((lane >> 4) * sc_rows + (wave == 0 ? m0 : n0) + (lane & 15) * 16);
+    const unsigned lds0 = (unsigned)(uintptr_t)(LDS_AS char*)lds;
+    const unsigned lw = __builtin_amdgcn_readfirstlane(lds0 + wave * 4096);
+    const unsigned lsc = __builtin_amdgcn_readfirstlane(lds0 + MX9_SC + (sc_wave ? wave * 1024 : 4096 + (wave - 2) * 1024));
+
+    const int sw = (r32 >> 1) & 7;
+    const unsigned a_row = lds0 + (wm * TM + r32) * 128, b_row = lds0 + MX9_UNIT + (wn * TN + r32) * 128;
+    // fragment addresses of step ks = 0 / 1 (logical chunks 4 ks + h, 4 ks + 2 + h); the
+    // fragment rows (i, j) * 32 ride in the ds_read offset field, the stage slot is added per stage
+    const unsigned a00 = a_row + (((0 + h) ^ sw) << 4), a01 = a_row + (((2 + h) ^ sw) << 4);
+    const unsigned a10 = a_row + (((4 + h) ^ sw) << 4), a11 = a_row + (((6 + h) ^ sw) << 4);
+    const unsigned b00 = b_row + (((0 + h) ^ sw) << 4), b01 = b_row + (((2 + h) ^ sw) << 4);
+    const unsigned b10 = b_row + (((4 + h) ^ sw) << 4), b11 = b_row + (((6 + h) ^ sw) << 4);
+    const unsigned sa_l = lds0 + MX9_SC + h * 256 + wm * TM + r32;
+    const unsigned sb_l = lds0 + MX9_SC + 1024 + h * 256 + wn * TN + r32;
+
+    f32x16 acc[4][2];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
+    bf16x8 a[4][2], b[2][2];
+    unsigned sa[4], sbv[2];
+
+    // one 64-deep step: fragments at aa0 / aa1 / bb0 / bb1 (chunks c0, c1 of the slot's rows),
+    // scale bytes at sca / scb (blocks 2 ks + h), optionally the DMA of the next stage into slot
+    // `nslot`, waits, barrier, 8 MFMAs, barrier. wm_ / wc_ = 0: drain vmcnt after the memory /
+    // compute phase (-1: no wait)
+    auto step = [&](unsigned aa0, unsigned aa1, unsigned bb0, unsigned bb1, unsigned sca, unsigned scb, bool dma,
+                    unsigned nslot, unsigned soff, unsigned soffS, bool wm_, bool wc_, bool end_barrier)
+        __attribute__((always_inline)) {
+        ds_read16<0>(b[0][0], bb0);
+        ds_read16<0>(b[0][1], bb1);
+        ds_read16<4096>(b[1][0], bb0);
+        ds_read16<4096>(b[1][1], bb1);
+        ds_read16<0>(a[0][0], aa0);
+        ds_read16<0>(a[0][1], aa1);
+        ds_read16<4096>(a[1][0], aa0);
+        ds_read16<4096>(a[1][1], aa1);
+        ds_read16<8192>(a[2][0], aa0);
+        ds_read16<8192>(a[2][1], aa1);
+        ds_read16<12288>(a[3][0], aa0);
+        ds_read16<12288>(a[3][1], aa1);
+        asm volatile("ds_read_u8 %0, %1 offset:0" : "=v"(sbv[0]) : "v"(scb) : "memory");
+        asm volatile("ds_read_u8 %0, %1 offset:32" : "=v"(sbv[1]) : "v"(scb) : "memory");
+        asm volatile("ds_read_u8 %0, %1 offset:0" : "=v"(sa[0]) : "v"(sca) : "memory");
+        asm volatile("ds_read_u8 %0, %1 offset:32" : "=v"(sa[1]) : "v"(sca) : "memory");
+        asm volatile("ds_read_u8 %0, %1 offset:64" : "=v"(sa[2]) : "v"(sca) : "memory");
+        asm volatile("ds_read_u8 %0, %1 offset:96" : "=v"(sa[3]) : "v"(sca) : "memory");
+        if (dma) {
+            mx_dma4(lw + nslot * 2 * MX9_UNIT, offA, rA, soff);
+            mx_dma4(lw + nslot * 2 * MX9_UNIT + MX9_UNIT, offB, rB, soff);
+            mx_dma1(lsc + nslot * 2048, voS, rS, soffS);
+        }
+        if (wm_) vm_wait<0>();
+        lgkm_wait<0>();
+        __builtin_amdgcn_s_barrier();
+        __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+                const i32x8 bo = __builtin_bit_cast(
+                    i32x8, __builtin_shufflevector(b[j][0], b[j][1], 0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15));
+                const i32x8 ao = __builtin_bit_cast(
+                    i32x8, __builtin_shufflevector(a[i][0], a[i][1], 0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15));
+                acc[i][j] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(bo, ao, acc[i][j], 0, 0, 0, (int)sbv[j], 0,
+                                                                             (int)sa[i]);
+            }
+        __builtin_amdgcn_s_setprio(0);
+        __builtin_amdgcn_sched_barrier(0);
+        if (wc_) vm_wait<0>();
+        if (end_barrier) __builtin_amdgcn_s_barrier();
+    };
+    // prologue: stage 0 into slot 0 (waves 2..7 DMA their scale piece from an empty range into
+    // an LDS scratch area, so every wave's DMA count is the same)
+    mx_dma4(lw, offA, rA, 0);
+    mx_dma4(lw + MX9_UNIT, offB, rB, 0);
+    mx_dma1(lsc, voS, rS, 0);
+    vm_wait<0>();
+    __builtin_amdgcn_s_barrier();
+    if (LATE) __builtin_amdgcn_s_barrier();
+    // stage s in slot s & 1; it issues stage s + 1 into the other slot (data soffset 128 (s + 1),
+    // scale soffset 4 sc_rows (s + 1)). The early row drains its DMA after its last compute
+    // phase of the stage, the late row before the barrier closing its last memory phase.
+    unsigned kN = 128, kS = 4u * (unsigned)sc_rows;
+    for (int s = 0; s < nk; ++s) {
+        const unsigned slot = s & 1, so = slot * 2 * MX9_UNIT, ss = slot * 2048;
+        const bool issue = s + 1 < nk, last = !issue;
+        step(a00 + so, a01 + so, b00 + so, b01 + so, sa_l + ss, sb_l + ss, issue, 1 - slot, kN, kS, false, false,
+             true);
+        step(a10 + so, a11 + so, b10 + so, b11 + so, sa_l + ss + 512, sb_l + ss + 512, false, 0, 0, 0,
+             LATE && issue, !LATE && issue, !(LATE && last));
+        kN += 128;
+        kS += 4u * (unsigned)sc_rows;
+    }
+
+    // ---- per-wave epilogue: the wave's 128 x 64 tile in its own LDS region (pitch 144 B); lane
+    // (r32, h) holds row i*32 + r32, columns j*32 + 8q + 4h + (0..3)
+    char* reg = lds + wave * (128 * MX9_PITCH);
+    const int rm0 = m0 + wm * TM, cn0 = n0 + wn * TN;
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int qd = 0; qd < 4; ++qd) {
+            const int nl = j * 32 + 8 * qd + 4 * h;
+            float bv[4] = {0.f, 0.f, 0.f, 0.f};
+            if (p.bias) {
+#pragma unroll
+                for (int r = 0; r < 4; ++r) bv[r] = bf2f(p.bias[min(cn0 + nl + r, p.N - 1)]);
+            }
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                bf16x4 o;
+#pragma unroll
+                for (int r = 0; r < 4; ++r) o[r] = f2bf(apply_act(acc[i][j][4 * qd + r] + bv[r], ACT));
+                *reinterpret_cast<bf16x4*>(reg + (i * 32 + r32) * MX9_PITCH + nl * 2) = o;
+            }
+        }
+    // the wave's own LDS writes precede its reads
+    const int rr = lane >> 3, cc = lane & 7;
+    if (!p.out_mx) {
+        bf16* Cout = reinterpret_cast<bf16*>(p.C);
+#pragma unroll 4
+        for (int q = 0; q < 16; ++q) {
+            const int row = q * 8 + rr, gr = rm0 + row, gc = cn0 + cc * 8;
+            const u16x8 v = *reinterpret_cast<const u16x8*>(reg + row * MX9_PITCH + cc * 16);
+            if (gr >= p.M || gc >= p.N) continue;
+            if (p.res) {
+                const int r2 = p.res_period ? gr % p.res_period : gr;
+                const u16x8 rv = *reinterpret_cast<const u16x8*>(p.res + (size_t)r2 * p.ldr + gc);
+                u16x8 o;
+#pragma unroll
+                for (int e = 0; e < 8; ++e) o[e] = __builtin_bit_cast(unsigned short, f2bf(bits2f(v[e]) + bits2f(rv[e])));
+                __builtin_nontemporal_store(o, reinterpret_cast<u16x8*>(Cout + (size_t)gr * p.ldc + gc));
+            } else {
+                __builtin_nontemporal_store(v, reinterpret_cast<u16x8*>(Cout + (size_t)gr * p.ldc + gc));
+            }
+        }
+    } else {
+        // mx8 output: lanes cc = 0..3 / 4..7 of a row hold its two 32-column blocks
+        uint8_t* Cq = reinterpret_cast<uint8_t*>(p.C);
+#pragma unroll 4
+        for (int q = 0; q < 16; ++q) {  // same trip count for every lane (shuffles)
+            const int row = q * 8 + rr, gr = rm0 + row, gc = cn0 + cc * 8;
+            const u16x8 v = *reinterpret_cast<const u16x8*>(reg + row * MX9_PITCH + cc * 16);
+            float f[8];
+            float a = 0.f;
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+                f[e] = bits2f(v[e]);
+                a = fmaxf(a, fabsf(f[e]));
+            }
+            const int sbyte = mx_scale_byte(block_amax(a));
+            if (gr < p.M && gc < p.N) {
+                *reinterpret_cast<uint2*>(Cq + (size_t)gr * p.ldc + gc) = mx_pack8(f, sbyte);
+                if ((cc & 3) == 0) p.sc[(size_t)(gc >> 5) * p.sc_rows + gr] = (uint8_t)sbyte;
+            }
+        }
+    }
+}
+
+template <int GROUP_M, int ACT>
+__global__ __launch_bounds__(512, 2) void gemm_mx9_kernel(MxArgs p) {
+    __shared__ __attribute__((aligned(16))) char lds[MX9_LDS];
+    const int nbm = (p.M + 255) / 256, nbn = p.N / 256;
+    const int tile = xcd_remap(blockIdx.x, gridDim.x);
+    int bm, bn;
+    tile_coords<GROUP_M>(tile, nbm, nbn, bm, bn);
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    if (wave >= 4)
+        mx9_tile<ACT, true>(p, lds, bm * 256, bn * 256, wave);
+    else
+        mx9_tile<ACT, false>(p, lds, bm * 256, bn * 256, wave);
+}
+
+int g_mx_variant = -1;  // dev: 0 = gemm_mx_kernel (64-deep half-line stages) where mx9 would run
+
+template <int GROUP_M>
+int launch_mx9(const MxArgs& a, hipStream_t s) {
+    const dim3 grid(((a.M + 255) / 256) * (a.N / 256)), block(512);
+    switch (a.act) {
+        case MME_ACT_GELU_TANH:
+            hipLaunchKernelGGL((gemm_mx9_kernel<GROUP_M, MME_ACT_GELU_TANH>), grid, block, 0, s, a);
+            break;
+        case MME_ACT_QUICK_GELU:
+            hipLaunchKernelGGL((gemm_mx9_kernel<GROUP_M, MME_ACT_QUICK_GELU>), grid, block, 0, s, a);
+            break;
+        case MME_ACT_GELU_ERF:
+            hipLaunchKernelGGL((gemm_mx9_kernel<GROUP_M, MME_ACT_GELU_ERF>), grid, block, 0, s, a);
+            break;
+        default:
+            hipLaunchKernelGGL((gemm_mx9_kernel<GROUP_M, MME_ACT_NONE>), grid, block, 0, s, a);
+            break;
+    }
+    return mme_check_launch("mme_gemm_mx");
+}
+
 template <int GROUP_M>
 int launch_mx(const MxArgs& a, hipStream_t s) {
     const int nbm = (a.M + 255) / 256, nbn = (a.N + 255) / 256;
@@ -449,6 +718,11 @@ extern "C" int mme_layernorm_mx(const void* x, int ldx, const void* gamma, const
     return mme_check_launch("mme_layernorm_mx");
 }
 
+extern "C" int mme_gemm_mx_variant(int v) {  // dev / tests: 0 = the 64-deep half-line kernel
+    g_mx_variant = v;
+    return MME_OK;
+}
+
 extern "C" int mme_gemm_mx(const void* A, int lda, const void* sa, int sa_rows, const void* B, int ldb,
                            const void* sb, int sb_rows, void* Cp, int ldc, void* c_scales, int c_rows_pad, int M,
                            int N, int K, const void* bias, const void* residual, int ldr, int res_period, int act,
@@ -474,5 +748,9 @@ extern "C" int mme_gemm_mx(const void* A, int lda, const void* sa, int sa_rows, 
     MxArgs a{(const uint8_t*)A, (const uint8_t*)B, (const uint8_t*)sa, (const uint8_t*)sb, Cp, (uint8_t*)c_scales,
              (const bf16*)bias, (const bf16*)residual, lda, ldb, ldc, ldr, sa_rows, sb_rows, c_rows_pad, M, N, K,
              res_period, act, out_mx};
+    // mx9 where its geometry holds (every DFN5B-H encoder shape); 32-bit DMA offsets
+    if (K % 128 == 0 && K >= 256 && N % 256 == 0 && (size_t)M * lda < (1ull << 32) && (size_t)N * ldb < (1ull << 32) &&
+        (size_t)(K / 32) * (sa_rows > sb_rows ? sa_rows : sb_rows) < (1ull << 32) && g_mx_variant != 0)
+        return launch_mx9<4>(a, as_stream(stream));
     return launch_mx<4>(a, as_stream(stream));
 }
