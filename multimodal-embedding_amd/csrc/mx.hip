@@ -399,8 +399,9 @@ __global__ __launch_bounds__(512, 2) void gemm_mx_kernel(MxArgs p) {
     }
 }
 
+#ifdef MME_DEV
 // ---------------------------------------------------------------------------
-// mx9 (production for K % 128 == 0, N % 256 == 0; round 3): the block-scaled fp8 GEMM on
+// mx9 (dev variant 9, round 3; MME_DEV builds only): the block-scaled fp8 GEMM on
 // whole-line LDS-DMA rows. gemm_mx_kernel stages 64-deep fp8 stages as 64-B half-line
 // rows (16 rows x 64 B per 1 KiB piece), the piece shape the LDS-DMA path moves at about
 // half the rate of whole 128-B lines (tools/probes/dma_bw.hip); at the fp8 MFMA rate that
@@ -646,8 +647,6 @@ __global__ __launch_bounds__(512, 2) void gemm_mx9_kernel(MxArgs p) {
         mx9_tile<ACT, false>(p, lds, bm * 256, bn * 256, wave);
 }
 
-int g_mx_variant = -1;  // dev: 0 = gemm_mx_kernel (64-deep half-line stages) where mx9 would run
-
 template <int GROUP_M>
 int launch_mx9(const MxArgs& a, hipStream_t s) {
     const dim3 grid(((a.M + 255) / 256) * (a.N / 256)), block(512);
@@ -667,6 +666,10 @@ int launch_mx9(const MxArgs& a, hipStream_t s) {
     }
     return mme_check_launch("mme_gemm_mx");
 }
+
+#endif  // MME_DEV
+
+int g_mx_variant = -1;  // dev: 9 = mx9 where its geometry holds
 
 template <int GROUP_M>
 int launch_mx(const MxArgs& a, hipStream_t s) {
@@ -718,7 +721,11 @@ extern "C" int mme_layernorm_mx(const void* x, int ldx, const void* gamma, const
     return mme_check_launch("mme_layernorm_mx");
 }
 
-extern "C" int mme_gemm_mx_variant(int v) {  // dev / tests: 0 = the 64-deep half-line kernel
+extern "C" int mme_gemm_mx_variant(int v) {  // dev / tests: 9 = mx9 (MME_DEV builds), -1 / 0 = production
+    MME_REQUIRE(v == -1 || v == 0 || v == 9, "mme_gemm_mx_variant: unknown variant %d", v);
+#ifndef MME_DEV
+    MME_REQUIRE(v != 9, "mme_gemm_mx_variant: variant 9 (mx9) is a development form (build libmme_dev.so: make dev)");
+#endif
     g_mx_variant = v;
     return MME_OK;
 }
@@ -748,9 +755,11 @@ extern "C" int mme_gemm_mx(const void* A, int lda, const void* sa, int sa_rows, 
     MxArgs a{(const uint8_t*)A, (const uint8_t*)B, (const uint8_t*)sa, (const uint8_t*)sb, Cp, (uint8_t*)c_scales,
              (const bf16*)bias, (const bf16*)residual, lda, ldb, ldc, ldr, sa_rows, sb_rows, c_rows_pad, M, N, K,
              res_period, act, out_mx};
-    // mx9 where its geometry holds (every DFN5B-H encoder shape); 32-bit DMA offsets
-    if (K % 128 == 0 && K >= 256 && N % 256 == 0 && (size_t)M * lda < (1ull << 32) && (size_t)N * ldb < (1ull << 32) &&
-        (size_t)(K / 32) * (sa_rows > sb_rows ? sa_rows : sb_rows) < (1ull << 32) && g_mx_variant != 0)
+#ifdef MME_DEV
+    // dev variant 9: mx9 where its geometry holds (every DFN5B-H encoder shape); 32-bit DMA offsets
+    if (g_mx_variant == 9 && K % 128 == 0 && K >= 256 && N % 256 == 0 && (size_t)M * lda < (1ull << 32) &&
+        (size_t)N * ldb < (1ull << 32) && (size_t)(K / 32) * (sa_rows > sb_rows ? sa_rows : sb_rows) < (1ull << 32))
         return launch_mx9<4>(a, as_stream(stream));
+#endif
     return launch_mx<4>(a, as_stream(stream));
 }

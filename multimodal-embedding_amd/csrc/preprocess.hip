@@ -231,6 +231,99 @@ __global__ __launch_bounds__(256) void resample_patch_fused_kernel(
     }
 }
 
+// Fused patch path at a compile-time patch size (production for p = 14, every registry
+// vision tower; round 3). resample_patch_fused_kernel above spends its time in index
+// arithmetic, not bytes: every output element re-derives (channel, ky, kx) by runtime
+// division, and every tap of both passes re-reads its bounds and weights (0.97 ms per 239
+// SigLIP images = 0.27 TB/s). Here each loop runs over the axis along which nothing but the
+// data changes:
+//   * horizontal pass: thread = one (column, channel) of the patch row's used columns
+//     (G * P of the S cropped ones -- the conv never reads the rest); its bounds and <= 8
+//     weights are loaded once, then it walks the staged input rows;
+//   * vertical pass: same thread mapping, walking the P output rows; a row's bounds and
+//     weights are the same for every thread (scalar loads);
+//   * im2col write: thread = one 16-B chunk of a patch's kpad columns; its 8 LDS source
+//     offsets and LUT bases are computed once, then it walks every G / 3-rd patch.
+// The u8 raster of the P output rows stays in LDS ([P][G * P * 3]) and the LUT turns it into
+// the exact float32 -> bf16 values. Same integer sums, so the output is bit-identical.
+template <int P>
+__global__ __launch_bounds__(256) void resample_patch_p_kernel(
+    const uint8_t* __restrict__ img, int n, int H, int W, int S, int top, int left, int kx, int ky,
+    const int* __restrict__ xb, const int* __restrict__ xk, const int* __restrict__ yb, const int* __restrict__ yk,
+    NormArgs na, int kpad, bf16* __restrict__ out) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t dyn[];
+    __shared__ unsigned short lut[3 * 256];
+    const int G = S / P, E = G * P * 3;  // used columns x channels
+    const int b = blockIdx.x / G, py = blockIdx.x % G, tid = threadIdx.x;
+    const int oy0 = py * P + top, oy1 = oy0 + P - 1;
+    const int r0 = yb[2 * oy0], r1 = yb[2 * oy1] + yb[2 * oy1 + 1];
+    const int R = r1 - r0, rowb = W * 3;
+    uint8_t* in_l = dyn;                                  // [R][W * 3]
+    uint8_t* hr = dyn + ((R * rowb + 15) & ~15);          // [R][E]
+    uint8_t* vr = hr + ((R * E + 15) & ~15);              // [P][E]
+    for (int i = tid; i < 3 * 256; i += 256) {
+        const int c = i >> 8, u = i & 255;
+        lut[i] = __builtin_bit_cast(unsigned short, f2bf(normalize(u, na.mean[c], na.stdv[c])));
+    }
+    const uint8_t* src = img + ((long)b * H + r0) * rowb;
+    const int nbytes = R * rowb;
+    if ((((uintptr_t)src | (unsigned)nbytes) & 15) == 0) {
+        for (int i = tid; i < nbytes / 16; i += 256)
+            reinterpret_cast<uint4*>(in_l)[i] = reinterpret_cast<const uint4*>(src)[i];
+    } else {
+        for (int i = tid; i < nbytes; i += 256) in_l[i] = src[i];
+    }
+    __syncthreads();
+    for (int e = tid; e < E; e += 256) {  // horizontal pass
+        const int xc = e / 3, c = e - 3 * xc;
+        const int xx = xc + left;
+        const int xmin = xb[2 * xx], cnt = xb[2 * xx + 1];
+        int w[8];
+#pragma unroll
+        for (int x = 0; x < 8; ++x) w[x] = x < cnt ? xk[xx * kx + x] : 0;
+        const uint8_t* sp = in_l + xmin * 3 + c;
+        for (int r = 0; r < R; ++r) {
+            int sum = 1 << (PREC - 1);
+#pragma unroll
+            for (int x = 0; x < 8; ++x)
+                if (x < cnt) sum += sp[r * rowb + 3 * x] * w[x];
+            hr[r * E + e] = (uint8_t)clip8(sum);
+        }
+    }
+    __syncthreads();
+    for (int e = tid; e < E; e += 256) {  // vertical pass
+#pragma unroll 2
+        for (int kyy = 0; kyy < P; ++kyy) {
+            const int oy = oy0 + kyy;
+            const int ymin = yb[2 * oy] - r0, cnt = yb[2 * oy + 1];
+            const int* kk = yk + oy * ky;
+            int sum = 1 << (PREC - 1);
+            for (int y = 0; y < cnt; ++y) sum += hr[(ymin + y) * E + e] * kk[y];
+            vr[kyy * E + e] = (uint8_t)clip8(sum);
+        }
+    }
+    __syncthreads();
+    constexpr int P2 = P * P, C3 = 3 * P2;
+    const int NC = kpad / 8, PG = 256 / NC;  // 16-B chunks per patch, patch groups
+    const int q = tid % NC, g = tid / NC;
+    if (g >= PG) return;
+    int off[8], lb[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+        const int col = q * 8 + e;
+        const int c = col / P2, rem = col - c * P2, kyy = rem / P, kxx = rem - kyy * P;
+        off[e] = col < C3 ? kyy * E + kxx * 3 + c : -1;
+        lb[e] = c * 256;
+    }
+    bf16* dst = out + ((long)b * G * G + (long)py * G) * kpad + q * 8;
+    for (int px = g; px < G; px += PG) {
+        u16x8 v;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] = off[e] >= 0 ? lut[lb[e] + vr[off[e] + px * P * 3]] : (unsigned short)0;
+        *reinterpret_cast<u16x8*>(dst + (long)px * kpad) = v;
+    }
+}
+
 // Plain im2col of pixel_values (the HF-API path: get_image_features(pixel_values)).
 template <typename T>
 __global__ void im2col_kernel(const T* __restrict__ pix, int n, int S, int p, int kpad, bf16* __restrict__ out) {
@@ -322,6 +415,15 @@ extern "C" int mme_preprocess_u8(const uint8_t* imgs, int n, int H, int W, int r
     }
     if (out_kind == MME_PIX_PATCHES) {
         const int R = fused_max_rows(H, rh, S, top, patch);
+        if (patch == 14 && kx <= 8 && ky <= 8 && kpad <= 8 * 256) {
+            const long E = (long)(S / 14) * 14 * 3;
+            const long lds = (((long)R * W * 3 + 15) & ~15L) + ((R * E + 15) & ~15L) + 14 * E;
+            if (lds <= FUSED_LDS) {
+                hipLaunchKernelGGL(resample_patch_p_kernel<14>, dim3(n * (S / 14)), dim3(256), (unsigned)lds, s, imgs,
+                                   n, H, W, S, top, left, kx, ky, xb, xk, yb, yk, na, kpad, (bf16*)out);
+                return mme_check_launch("mme_preprocess_u8");
+            }
+        }
         if ((((long)R * W * 3 + 15) & ~15L) + (long)R * S * 3 <= FUSED_LDS) {
             const int G = S / patch;
             hipLaunchKernelGGL(resample_patch_fused_kernel, dim3(n * G), dim3(256), 0, s, imgs, n, H, W, S, top, left,

@@ -73,3 +73,6 @@ def test_production_library_holds_no_dev_forms():
     lib.mme_gemm_variant.argtypes = [ctypes.c_int]
     assert lib.mme_gemm_variant(64) != 0 and b"development form" in lib.mme_last_error()
     assert lib.mme_gemm_variant(47) == 0 and lib.mme_gemm_variant(-1) == 0
+    lib.mme_gemm_mx_variant.argtypes = [ctypes.c_int]
+    assert lib.mme_gemm_mx_variant(9) != 0 and b"development form" in lib.mme_last_error()
+    assert lib.mme_gemm_mx_variant(-1) == 0

@@ -84,3 +84,18 @@ def test_preprocess_patches_batch_vs_pixel_values(cuda):
     kw = dict(resize=(384, 384), crop=(0, 0), size=384, mean=ip.mean, std=ip.std)
     patches = ops.preprocess_u8(x, patch=14, kpad=640, **kw)
     assert torch.equal(patches, ops.im2col(ops.preprocess_u8(x, **kw), 14, 640))
+
+
+# round 3: p = 14 runs resample_patch_p_kernel<14> (compile-time patch, <= 8 taps per pass);
+# other patch sizes and wider filters the generic fused kernel. Both == im2col of the bit-exact
+# pixel values, upscales and mild downscales (448 -> 384: 7 taps), ragged S % p.
+@pytest.mark.parametrize("H,W,S,patch,kpad", [(224, 224, 384, 14, 640), (448, 448, 384, 14, 640),
+                                              (300, 500, 378, 14, 640), (224, 224, 384, 16, 768),
+                                              (256, 256, 224, 16, 768), (224, 224, 448, 14, 592)])
+def test_preprocess_patch_kernels_vs_pixel_values(cuda, H, W, S, patch, kpad):
+    rng = np.random.default_rng(H + W + S + patch)
+    x = torch.from_numpy(rng.integers(0, 256, (5, H, W, 3), dtype=np.uint8)).cuda()
+    ip = _cfg(0, S)
+    kw = dict(resize=(S, S), crop=(0, 0), size=S, mean=ip.mean, std=ip.std)
+    patches = ops.preprocess_u8(x, patch=patch, kpad=kpad, **kw)
+    assert torch.equal(patches, ops.im2col(ops.preprocess_u8(x, **kw), patch, kpad))

@@ -32,7 +32,7 @@ def main():
     p.add_argument("--shapes", default="qkv,o_proj,fc1,fc2")
     p.add_argument("--mx", action="store_true", help="also time the mx8 (block-scaled fp8) GEMM")
     p.add_argument("--mx-variants", default="-1", help="mme_gemm_mx_variant values to time with --mx "
-                   "(0 = 64-deep half-line kernel, -1 = production dispatch)")
+                   "(-1 = production dispatch, 9 = mx9 in libmme_dev.so)")
     p.add_argument("--torch", action="store_true", help="also time torch F.linear (hipBLASLt) on each shape")
     p.add_argument("--epi", default="none", help="epilogue: none | bias | res (residual in place) | resstats (res + LayerNorm "
                    "statistics, mme_gemm_res_stats) | gelu (bias+gelu_tanh)")

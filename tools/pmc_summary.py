@@ -25,9 +25,11 @@ def load(d, counter):
 
 
 def family(name):
-    for k in ("gemm_pipe8_kernel", "gemm_pipe6_kernel", "gemm_pipe4_kernel", "gemm_pipe3_kernel", "gemm_tn_kernel", "attn_fwd_kernel",
-              "attn_pipe_kernel", "attn_dma_kernel", "layernorm_kernel", "sim_topk_kernel",
-              "resample_v_patch_kernel", "probe_attn_kernel"):
+    for k in ("gemm_pipe9_kernel", "gemm_pipe8_kernel", "gemm_pipe6_kernel", "gemm_pipe4_kernel", "gemm_pipe3_kernel",
+              "gemm_tn_kernel", "gemm_mx_kernel", "attn_hyb_kernel", "attn_m32_kernel", "attn_short_kernel",
+              "attn_fwd_kernel", "attn_pipe_kernel", "attn_dma_kernel", "layernorm_kernel", "sim_topk_kernel",
+              "resample_patch_p_kernel", "resample_patch_fused_kernel", "resample_v_patch_kernel",
+              "probe_attn_img_kernel", "probe_attn_kernel", "row_part_combine_lds_kernel"):
         if k in name:
             return k
     return "other"
