@@ -1157,7 +1157,15 @@ __global__ __launch_bounds__(256, 3) void attn_short_kernel(AttnArgs a, int unit
 //     ring (every LDS address a lane base + immediate), 16-B O stores after a
 //     v_permlane32_swap of the two lane halves.
 // ---------------------------------------------------------------------------
-template <int HD, int NW, int MINW, bool PRIO, bool DPV = false, bool PF = false>
+// SKIP (round 3, kind 65): a tile whose second 32-key block lies wholly past the keys skips
+// that block's QK^T and PV MFMAs, as attn_hyb_kernel's kind 62 does at hd 72 -- ViT-H
+// (T = 257 = 4 x 64 + 1) ends in such a tile (1/10 of the key blocks). Its P is 0, yet the
+// outputs are not bit-identical to the unskipped kernel: an MFMA whose B operand is all zero
+// still changes the accumulator it passes through in rare cases (1-15 of 0.7-1.3 M outputs
+// differ, by one or two bf16 ulps; test_attention_m32_skip). The same skip in 8-wave blocks (DFN5B,
+// T = 730) measured 18 % slower than kind 38 (0.59 vs 0.50 ms, profiles/r03_v11_attn_dfn5b_ab.log)
+// and is not built.
+template <int HD, int NW, int MINW, bool PRIO, bool DPV = false, bool PF = false, bool SKIP = false>
 __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(MINW))) void attn_m32_kernel(AttnArgs a) {
     constexpr int NSTG = DPV ? 3 : 2;
     constexpr bool ONES = HD % 32 != 0;
@@ -1274,6 +1282,7 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(MINW)))
         }
     };
     auto qk = [&](int t, const unsigned so, f32x16(&sc)[2]) __attribute__((always_inline)) {
+        const bool half = SKIP && t * 64 + 32 >= Tk;
         if constexpr (PF) {
             qk_pf(t, so, sc);
         } else {
@@ -1281,7 +1290,11 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(MINW)))
         for (int kb = 0; kb < 2; ++kb) {
             f32x16 z;
 #pragma unroll
-            for (int e = 0; e < 16; ++e) z[e] = 0.f;
+            for (int e = 0; e < 16; ++e) z[e] = kb == 1 && half ? -INFINITY : 0.f;
+            if (kb == 1 && half) {
+                sc[kb] = z;
+                continue;
+            }
 #pragma unroll
             for (int ks = 0; ks < NKS; ++ks) {
                 const bf16x8 kf = *reinterpret_cast<const LDS_AS bf16x8*>((uintptr_t)(kb0 + so + kb * 512 + ks * 2048));
@@ -1335,9 +1348,10 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(MINW)))
 #pragma unroll
                 for (int j = 0; j < 8; ++j) pk[2 * kb + sp][j] = f2bf(sc[kb][8 * sp + j]);
     };
-    auto pv = [&](const unsigned so, const bf16x8(&pk)[4]) {
+    auto pv = [&](const unsigned so, const bf16x8(&pk)[4], bool half = false) {
 #pragma unroll
-        for (int kb = 0; kb < 2; ++kb)
+        for (int kb = 0; kb < 2; ++kb) {
+            if (SKIP && kb == 1 && half) break;
 #pragma unroll
             for (int sp = 0; sp < 2; ++sp)
 #pragma unroll
@@ -1348,6 +1362,7 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(MINW)))
                     const bf16x8 vv = __builtin_bit_cast(bf16x8, __builtin_shufflevector(v0, v1, 0, 1, 2, 3, 4, 5, 6, 7));
                     o[db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vv, pk[2 * kb + sp], o[db], 0, 0, 0);
                 }
+        }
     };
     // PF: V^T fragments read before the softmax, MFMAs after it
     auto vread = [&](const unsigned so, bf16x8(&vf)[4][NDB]) __attribute__((always_inline)) {
@@ -1402,14 +1417,14 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(MINW)))
             if (t + 1 < nkt) issue(t + 1);
             qk(t, 0, sc);
             softmax(sc, pk);
-            pv(0, pk);
+            pv(0, pk, SKIP && t * 64 + 32 >= Tk);
             if (t + 1 < nkt) {
                 vm_wait<0>();
                 __builtin_amdgcn_s_barrier();
                 if (t + 2 < nkt) issue(t + 2);
                 qk(t + 1, TILE, sc);
                 softmax(sc, pk);
-                pv(TILE, pk);
+                pv(TILE, pk, SKIP && (t + 1) * 64 + 32 >= Tk);
             }
         }
     } else {
@@ -1934,8 +1949,9 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(MINW)))
     float m = -1e30f, lsum = 0.f;  // lsum (hd 80): this lane's share of query r's weight sum
 
     auto tile_step = [&](int t, const unsigned so) __attribute__((always_inline)) {
-        // SKIP (dev): a tile whose second 32-key block lies wholly past the keys (the last tile
-        // at T = 729) skips that block's QK^T and PV MFMAs; its P is 0 either way (bit-identical)
+        // SKIP: a tile whose second 32-key block lies wholly past the keys (the last tile at
+        // T = 729) skips that block's QK^T and PV MFMAs; its P is 0 either way (outputs may still
+        // differ from the unskipped kernel by a bf16 ulp in rare cases: see attn_m32_kernel's SKIP)
         const bool half = SKIP && t * 64 + 32 >= Tk;
         f32x16 sc[2];
         if (SKIP == 2) {
@@ -2277,6 +2293,10 @@ bool launch_attn(int kind, const AttnArgs& a, int B, int T, int H, hipStream_t s
         hipLaunchKernelGGL((attn_m32_kernel<HD, 8, 1, true>), dim3(cdiv(T, 256) * H * B), dim3(512), 0, st, a);
     else if (kind == 41)  // attn_m32_kernel, 9 waves (288 queries): production for hd 80 where 9-wave blocks pad least
         hipLaunchKernelGGL((attn_m32_kernel<HD, 9, 1, true>), dim3(cdiv(T, 288) * H * B), dim3(576), 0, st, a);
+    else if (kind == 65)  // kind 41 skipping a tile's second key block when it lies past the keys: production
+                          // for hd 80 in 9-wave blocks (ViT-H T 257: +2-4 %, profiles/r03_v11_attn_vith_ab.log)
+        hipLaunchKernelGGL((attn_m32_kernel<HD, 9, 1, true, false, false, true>), dim3(cdiv(T, 288) * H * B),
+                           dim3(576), 0, st, a);
     else if (kind == 62) {  // attn_hyb_kernel skipping a tile's second key block when it lies past the keys:
                             // production for hd 72
         if constexpr (HD != 64)
@@ -2485,7 +2505,7 @@ extern "C" int mme_attention(const void* qkv, int ld_qkv, void* out, int ld_out,
     // (profiles/r02_hyb_skip_bench.log, 4 of 4 A/B pairs).
     int kind = T <= 64 ? 16
                : (T <= 128 || hd == 64) ? 0
-               : (hd == 80 && pad9 * 10 < min(pad8, pad4) * 9) ? 41
+               : (hd == 80 && pad9 * 10 < min(pad8, pad4) * 9) ? 65
                : hd == 80 && pad8 * 10 <= pad4 * 11 ? 38
                : pad9 * 10 < min(pad8, pad4) * 9 ? 35
                : (hd == 80 && pad12 <= pad8 && pad12 * 10 <= pad4 * 11) ? 23

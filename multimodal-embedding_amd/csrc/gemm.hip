@@ -1198,7 +1198,10 @@ __device__ __forceinline__ void dma4(unsigned m0base, const unsigned (&voff)[4],
         : "memory", "m0", "scc");  // s_add_u32 writes SCC
 }
 
-template <class C, int ACT, bool LATE>
+// PRIO (dev variants 81 / 82): 0 = s_setprio 1 around every compute phase (production);
+// 1 = static priority 1 for the late wave row, no per-phase flips (MI355X_MICROARCH.md, two waves
+// per SIMD, item 4); 2 = no priority changes.
+template <class C, int ACT, bool LATE, int PRIO = 0>
 __device__ __forceinline__ void pipe9_tile(const GemmArgs& p, char* lds, const int m0, const int n0, const int wave) {
     static_assert(C::BM == 256 && C::BN == 256 && C::FN == 4 && C::FM == 8 && C::NW == 8, "pipe9: 256 x 256, 8 waves");
     constexpr int UNIT = 32768;
@@ -1253,13 +1256,13 @@ __device__ __forceinline__ void pipe9_tile(const GemmArgs& p, char* lds, const i
         else if (wm_ == 4) vm_wait<4>();
         lgkm_wait<0>();
         __builtin_amdgcn_s_barrier();
-        __builtin_amdgcn_s_setprio(1);
+        if (PRIO == 0) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
         for (int i = 0; i < 8; ++i)
 #pragma unroll
             for (int j = 0; j < C::FN; ++j)
                 acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b[j], a[i], acc[i][j], 0, 0, 0);
-        __builtin_amdgcn_s_setprio(0);
+        if (PRIO == 0) __builtin_amdgcn_s_setprio(0);
         __builtin_amdgcn_sched_barrier(0);
         if (wc_ == 0) vm_wait<0>();
         else if (wc_ == 4) vm_wait<4>();
@@ -1280,6 +1283,7 @@ __device__ __forceinline__ void pipe9_tile(const GemmArgs& p, char* lds, const i
         kA += 128;
     };
 
+    if (PRIO == 1 && LATE) __builtin_amdgcn_s_setprio(1);
     // prologue: units 0..4 (A0 B0 A1 B1 A2) into slots 0..4
     dma4(lw + 0 * UNIT, offA, rA, 0);
     dma4(lw + 1 * UNIT, offB, rB, 0);
@@ -1320,7 +1324,7 @@ __device__ __forceinline__ void pipe9_tile(const GemmArgs& p, char* lds, const i
     gemm_epilogue_wave<C, ACT>(p, lds, acc, m0, n0, wave, wm, wn, g, li, lane);
 }
 
-template <class C, int GROUP_M, int ACT, bool SPLIT>
+template <class C, int GROUP_M, int ACT, bool SPLIT, int PRIO = 0>
 __global__ __launch_bounds__(C::NT, 2) void gemm_pipe9_kernel(GemmArgs p) {
     __shared__ __attribute__((aligned(16))) char lds[5 * 32768];
     const int nbm = (p.M + C::BM - 1) / C::BM;
@@ -1340,9 +1344,9 @@ __global__ __launch_bounds__(C::NT, 2) void gemm_pipe9_kernel(GemmArgs p) {
     }
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     if (wave >= C::NW / 2)
-        pipe9_tile<C, ACT, true>(p, lds, m0, n0, wave);
+        pipe9_tile<C, ACT, true, PRIO>(p, lds, m0, n0, wave);
     else
-        pipe9_tile<C, ACT, false>(p, lds, m0, n0, wave);
+        pipe9_tile<C, ACT, false, PRIO>(p, lds, m0, n0, wave);
 }
 
 template <class C, int GROUP_M, int ACT, int DIAG = 0, bool SPLIT = false, bool WEPI = false>
@@ -1430,25 +1434,25 @@ int launch_pipe8(const GemmArgs& a, hipStream_t s) {
     return mme_check_launch("mme_gemm");
 }
 
-template <class C, int GROUP_M, bool SPLIT>
+template <class C, int GROUP_M, bool SPLIT, int PRIO = 0>
 int launch_pipe9(const GemmArgs& a, hipStream_t s) {
     const int nbm = (a.M + C::BM - 1) / C::BM, nbn = (a.N + C::BN - 1) / C::BN;
     const dim3 grid(SPLIT ? split_tiles(nbm, a.N / C::BN) : nbm * nbn), block(C::NT);
     switch (a.act) {
         case MME_ACT_GELU_TANH:
-            hipLaunchKernelGGL((gemm_pipe9_kernel<C, GROUP_M, MME_ACT_GELU_TANH, SPLIT>), grid, block, 0, s, a);
+            hipLaunchKernelGGL((gemm_pipe9_kernel<C, GROUP_M, MME_ACT_GELU_TANH, SPLIT, PRIO>), grid, block, 0, s, a);
             break;
         case MME_ACT_QUICK_GELU:
-            hipLaunchKernelGGL((gemm_pipe9_kernel<C, GROUP_M, MME_ACT_QUICK_GELU, SPLIT>), grid, block, 0, s, a);
+            hipLaunchKernelGGL((gemm_pipe9_kernel<C, GROUP_M, MME_ACT_QUICK_GELU, SPLIT, PRIO>), grid, block, 0, s, a);
             break;
         case MME_ACT_GELU_ERF:
-            hipLaunchKernelGGL((gemm_pipe9_kernel<C, GROUP_M, MME_ACT_GELU_ERF, SPLIT>), grid, block, 0, s, a);
+            hipLaunchKernelGGL((gemm_pipe9_kernel<C, GROUP_M, MME_ACT_GELU_ERF, SPLIT, PRIO>), grid, block, 0, s, a);
             break;
         case MME_ACT_GEGLU_TANH:
-            hipLaunchKernelGGL((gemm_pipe9_kernel<C, GROUP_M, MME_ACT_GEGLU_TANH, SPLIT>), grid, block, 0, s, a);
+            hipLaunchKernelGGL((gemm_pipe9_kernel<C, GROUP_M, MME_ACT_GEGLU_TANH, SPLIT, PRIO>), grid, block, 0, s, a);
             break;
         default:
-            hipLaunchKernelGGL((gemm_pipe9_kernel<C, GROUP_M, MME_ACT_NONE, SPLIT>), grid, block, 0, s, a);
+            hipLaunchKernelGGL((gemm_pipe9_kernel<C, GROUP_M, MME_ACT_NONE, SPLIT, PRIO>), grid, block, 0, s, a);
             break;
     }
     return mme_check_launch("mme_gemm");
@@ -2236,6 +2240,16 @@ int gemm_dispatch(GemmArgs a, hipStream_t s) {
             if (!pipe8_ok(a)) break;
             if (N % 256 == 128) return launch_pipe9<Pipe256, 4, true>(a, s);
             return launch_pipe9<Pipe256, 4, false>(a, s);
+        case 81:  // dev: pipe9, static priority 1 for the late wave row, no per-phase setprio
+        case 82:  // dev: pipe9 without any setprio
+            if (!pipe8_ok(a)) break;
+            if (g_variant == 81)
+                return N % 256 == 128 ? launch_pipe9<Pipe256, 4, true, 1>(a, s) : launch_pipe9<Pipe256, 4, false, 1>(a, s);
+            return N % 256 == 128 ? launch_pipe9<Pipe256, 4, true, 2>(a, s) : launch_pipe9<Pipe256, 4, false, 2>(a, s);
+        case 83:  // dev: pipe9 with 8-row tile bands
+            if (!pipe8_ok(a)) break;
+            if (N % 256 == 128) return launch_pipe9<Pipe256, 8, true>(a, s);
+            return launch_pipe9<Pipe256, 8, false>(a, s);
         case 54: return launch_pipe6<Pipe256, 2, 1>(a, s);   // dev: 2-row tile bands
         case 55: return launch_pipe6<Pipe256, 16, 1>(a, s);  // dev: 16-row tile bands
         case 50: return launch_pipe7<Pipe256w, 4>(a, s);

@@ -65,10 +65,13 @@ class KernelTimer:
 
     enabled = False
     records = []
+    _pool = []   # timing events, created once and re-recorded by every timed step
+    _used = 0
 
     @classmethod
     def start(cls):
         cls.records = []
+        cls._used = 0
         cls.enabled = True
 
     @classmethod
@@ -76,10 +79,28 @@ class KernelTimer:
         cls.enabled = False
 
     @classmethod
+    def reserve(cls, n: int):
+        """Create the timing events up front (no hipEventCreate inside a timed region)."""
+        while len(cls._pool) < n:
+            cls._pool.append(torch.cuda.Event(enable_timing=True))
+
+    @classmethod
+    def used(cls) -> int:
+        return cls._used
+
+    @classmethod
+    def _event(cls):
+        if cls._used == len(cls._pool):
+            cls._pool.append(torch.cuda.Event(enable_timing=True))
+        ev = cls._pool[cls._used]
+        cls._used += 1
+        return ev
+
+    @classmethod
     def begin(cls):
         if not cls.enabled:
             return None
-        ev = torch.cuda.Event(enable_timing=True)
+        ev = cls._event()
         ev.record()
         return ev
 
@@ -87,7 +108,7 @@ class KernelTimer:
     def end(cls, ev, name: str, flops: float, nbytes: float = 0.0):
         if ev is None:
             return
-        e = torch.cuda.Event(enable_timing=True)
+        e = cls._event()
         e.record()
         cls.records.append((name, ev, e, flops, nbytes))
 

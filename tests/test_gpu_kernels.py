@@ -129,12 +129,12 @@ def test_attention(cuda, B, T, H, hd, causal, lens):
     torch.testing.assert_close(out.float(), ref, atol=2e-2, rtol=2e-2)
 
 
-PROD_ATTN_KINDS = (38, 41, 62)  # dispatched by mme_attention; the rest are development forms (libmme_dev.so)
+PROD_ATTN_KINDS = (38, 41, 62, 65)  # in the production library; the rest are development forms (libmme_dev.so)
 
 
 @pytest.mark.parametrize("kind", [k if k in PROD_ATTN_KINDS else pytest.param(k, marks=pytest.mark.dev)
                                   for k in (38, 39, 40, 41, 42, 43, 44, 45, 46, 47, 48, 49, 50, 51, 52, 54, 55, 56,
-                                            57, 58, 59, 60, 61, 62, 63)])
+                                            57, 58, 59, 60, 61, 62, 63, 65)])
 @pytest.mark.parametrize("B,T,H,hd,causal,lens", [
     (2, 729, 4, 72, False, None),       # SigLIP vision geometry
     (2, 520, 3, 72, False, [520, 301]),  # key padding, partial last tile
@@ -159,6 +159,43 @@ def test_attention_m32(cuda, kind, B, T, H, hd, causal, lens):
         lib.mme_attention_variant(0)
     ref = attn_ref(qkv, B, T, H, hd, sl, causal, hd ** -0.5)
     torch.testing.assert_close(out.float(), ref, atol=2e-2, rtol=2e-2)
+
+
+@pytest.mark.parametrize("B,T,H,causal,lens", [
+    (4, 257, 16, False, None),        # ViT-H/14-224: last tile 1 key
+    (3, 730, 4, False, None),         # T = 730: last tile 26 keys
+    (2, 300, 3, True, [300, 280]),    # key padding: the skip follows each sequence's length
+    (2, 769, 2, False, [769, 700]),   # a tile whose second block holds keys (no skip) beside one that skips
+])
+def test_attention_m32_skip(cuda, B, T, H, causal, lens):
+    """Kind 65 (production for hd 80 in 9-wave blocks: attn_m32_kernel skipping a tile's second key
+    block when it lies past the keys) against kind 41 (the same kernel without the skip). The skipped
+    block's P is 0, but an MFMA with an all-zero operand still re-rounds its accumulator in rare cases:
+    both kernels deterministic, a few bf16 ulps apart on < 1e-4 of the outputs (measured 1 / 0.70 M
+    and 15 / 1.32 M, max 0.00195)."""
+    from mme import _lib
+    lib = _lib.load()
+    g = torch.Generator(device="cuda").manual_seed(B * T)
+    qkv = rnd(B * T, 3 * H * 80, scale=1.5, gen=g)
+    sl = None if lens is None else torch.tensor(lens, dtype=torch.int32, device="cuda")
+    outs = []
+    for kind in (41, 41, 65, 65):
+        lib.mme_attention_variant(30 + kind)
+        try:
+            outs.append(ops.attention(qkv, B, T, H, 80, seq_lens=sl, causal=causal))
+            torch.cuda.synchronize()
+        finally:
+            lib.mme_attention_variant(0)
+    assert torch.equal(outs[0], outs[1]) and torch.equal(outs[2], outs[3]), "attention is not deterministic"
+    a, b = outs[0].float(), outs[2].float()
+    d = (a - b).abs()
+    # a flipped rounding of the fp32 accumulator or of the weight sum moves the bf16 output by one ulp
+    # of its binade, two when the pair straddles a power of two: bound 2^-6 |x| (measured max 0.00195)
+    ulp2 = torch.maximum(a.abs(), b.abs()) * 2.0 ** -6 + 1e-6
+    nd = int((d > 0).sum())
+    print(f"kind 65 vs 41: {nd} of {d.numel()} outputs differ, max {d.max().item():.3g}")
+    assert bool((d <= ulp2).all()), f"kind 65 differs from kind 41 beyond 2 bf16 ulps (max {d.max().item():.3g})"
+    assert nd <= max(2, int(1e-4 * d.numel()))
 
 
 def test_attention_production_full_grid(cuda):
