@@ -168,8 +168,8 @@ def retrieval_parity(tables, metrics, caps_per_image: int = 5):
 
 
 def encoder_parity(spec, imgs_u8, cap_ids, dev_img, dev_txt, bar: float = 0.999):
-    """Encoder parity of the headline job (checker; after the timed region): the job's own first images
-    and T2I captions encoded by the fp32 oracle (oracle/encoders.py: the PIL-exact processor and the
+    """Encoder parity of the headline job (checker; after the timed region): the job's own images and
+    T2I captions at the first, middle and last rows encoded by the fp32 oracle (oracle/encoders.py: the PIL-exact processor and the
     transformers towers restated, validated against main.encode_data) with the job's own weights,
     against the device embeddings the job produced (cosine per item; the SURVEY §8d bar is 0.999, 0.99 for
     the mx-fp8 encoder GEMMs)."""
@@ -184,7 +184,7 @@ def encoder_parity(spec, imgs_u8, cap_ids, dev_img, dev_txt, bar: float = 0.999)
     ci, ct = cos(dev_img, oi), cos(dev_txt, ot)
     return {"items": int(len(imgs_u8)), "img_cos_min": round(float(ci.min()), 6), "txt_cos_min": round(float(ct.min()), 6),
             "bar": bar, "ok": bool(ci.min() >= bar and ct.min() >= bar),
-            "checker": "oracle/encoders.py fp32 on the job's own first images / T2I captions and weights",
+            "checker": "oracle/encoders.py fp32 on the job's own images / T2I captions (rows listed) and weights",
             "seconds": round(time.time() - t0, 2)}
 
 
@@ -485,7 +485,11 @@ def main():
     my_t2i = my_caps[::caps].contiguous()
     del imgs, ids
     torch.cuda.synchronize()
-    n_enc = min(2, my_imgs.shape[0])
+    # encoder parity items: the first, middle and last images / T2I captions of this rank's job, i.e.
+    # rows at both ends of different execution batches (7 items, ~7 s of fp32 CPU work for SigLIP-400M)
+    nl = my_imgs.shape[0]
+    enc_idx = sorted({i for i in (0, 1, nl // 4, nl // 2, 3 * nl // 4, nl - 2, nl - 1) if 0 <= i < nl})
+    n_enc = len(enc_idx)
 
     last = {}
     ev = {}
@@ -617,8 +621,10 @@ def main():
     if rank == 0 and not args.no_parity:
         out["parity"] = retrieval_parity(last["tables"], metrics, caps)
         if n_enc:
-            out["parity"]["encoders"] = encoder_parity(spec, my_imgs[:n_enc], my_t2i[:n_enc], last["img"][:n_enc],
-                                                       last["t2i"][:n_enc], bar=0.99 if args.fp8 else 0.999)
+            ii = torch.tensor(enc_idx, device=my_imgs.device)
+            out["parity"]["encoders"] = encoder_parity(spec, my_imgs[ii], my_t2i[ii], last["img"][ii], last["t2i"][ii],
+                                                       bar=0.99 if args.fp8 else 0.999)
+            out["parity"]["encoders"]["rows"] = enc_idx
     if args.host_inputs:
         host_imgs = my_imgs.cpu().pin_memory()
         barrier()

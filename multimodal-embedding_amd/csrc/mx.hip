@@ -212,10 +212,91 @@ struct MxCfg {
 
 __device__ __forceinline__ int mxswz(int row, int chunk) { return chunk ^ ((row >> 2) & 3); }
 
-template <int GROUP_M, int ACT>
+// Per-wave epilogue of the mx8 GEMMs (gemm_mx_kernel WEPI, mx9): each wave stages its own 128 x 64
+// sub-tile in its own LDS region (pitch 144 B, 18 KiB; 144 KiB for the 8 waves), reads it back as
+// 16-B row chunks and stores it (bf16, + residual) or re-quantises it to mx8 -- no workgroup barrier,
+// so the early wave row's epilogue runs beside the late row's last MFMAs. Same arithmetic as the
+// whole-tile epilogue of gemm_mx_kernel (bit-identical outputs).
+constexpr int MXW_PITCH = 144, MXW_LDS = 8 * 128 * MXW_PITCH;
+template <int ACT>
+__device__ __forceinline__ void mx_epilogue_wave(const MxArgs& p, char* lds, f32x16 (&acc)[4][2], int m0, int n0,
+                                                 int wave, int lane) {
+    constexpr int TM = 128, TN = 64, MX9_PITCH = MXW_PITCH;
+    const int wm = wave / 4, wn = wave % 4;
+    const int h = lane >> 5, r32 = lane & 31;
+    // lane (r32, h) holds row i*32 + r32, columns j*32 + 8q + 4h + (0..3)
+    char* reg = lds + wave * (128 * MX9_PITCH);
+    const int rm0 = m0 + wm * TM, cn0 = n0 + wn * TN;
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int qd = 0; qd < 4; ++qd) {
+            const int nl = j * 32 + 8 * qd + 4 * h;
+            float bv[4] = {0.f, 0.f, 0.f, 0.f};
+            if (p.bias) {
+#pragma unroll
+                for (int r = 0; r < 4; ++r) bv[r] = bf2f(p.bias[min(cn0 + nl + r, p.N - 1)]);
+            }
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                bf16x4 o;
+#pragma unroll
+                for (int r = 0; r < 4; ++r) o[r] = f2bf(apply_act(acc[i][j][4 * qd + r] + bv[r], ACT));
+                *reinterpret_cast<bf16x4*>(reg + (i * 32 + r32) * MX9_PITCH + nl * 2) = o;
+            }
+        }
+    // the wave's own LDS writes precede its reads
+    const int rr = lane >> 3, cc = lane & 7;
+    if (!p.out_mx) {
+        bf16* Cout = reinterpret_cast<bf16*>(p.C);
+#pragma unroll 4
+        for (int q = 0; q < 16; ++q) {
+            const int row = q * 8 + rr, gr = rm0 + row, gc = cn0 + cc * 8;
+            const u16x8 v = *reinterpret_cast<const u16x8*>(reg + row * MX9_PITCH + cc * 16);
+            if (gr >= p.M || gc >= p.N) continue;
+            if (p.res) {
+                const int r2 = p.res_period ? gr % p.res_period : gr;
+                const u16x8 rv = *reinterpret_cast<const u16x8*>(p.res + (size_t)r2 * p.ldr + gc);
+                u16x8 o;
+#pragma unroll
+                for (int e = 0; e < 8; ++e) o[e] = __builtin_bit_cast(unsigned short, f2bf(bits2f(v[e]) + bits2f(rv[e])));
+                __builtin_nontemporal_store(o, reinterpret_cast<u16x8*>(Cout + (size_t)gr * p.ldc + gc));
+            } else {
+                __builtin_nontemporal_store(v, reinterpret_cast<u16x8*>(Cout + (size_t)gr * p.ldc + gc));
+            }
+        }
+    } else {
+        // mx8 output: lanes cc = 0..3 / 4..7 of a row hold its two 32-column blocks
+        uint8_t* Cq = reinterpret_cast<uint8_t*>(p.C);
+#pragma unroll 4
+        for (int q = 0; q < 16; ++q) {  // same trip count for every lane (shuffles)
+            const int row = q * 8 + rr, gr = rm0 + row, gc = cn0 + cc * 8;
+            const u16x8 v = *reinterpret_cast<const u16x8*>(reg + row * MX9_PITCH + cc * 16);
+            float f[8];
+            float a = 0.f;
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+                f[e] = bits2f(v[e]);
+                a = fmaxf(a, fabsf(f[e]));
+            }
+            const int sbyte = mx_scale_byte(block_amax(a));
+            if (gr < p.M && gc < p.N) {
+                *reinterpret_cast<uint2*>(Cq + (size_t)gr * p.ldc + gc) = mx_pack8(f, sbyte);
+                if ((cc & 3) == 0) p.sc[(size_t)(gc >> 5) * p.sc_rows + gr] = (uint8_t)sbyte;
+            }
+        }
+    }
+}
+
+// WEPI (round 3): the per-wave epilogue above instead of the whole-tile LDS epilogue below; the
+// late wave row's closing barrier and the early row's extra one are both dropped (equal counts).
+// SC1 (round 3): wave 0 alone DMAs a stage's 1 KiB scale piece (all 64 lanes) instead of every
+// wave issuing an 8-lane slice of it: 33 instead of 40 LDS-DMA issues per stage and workgroup;
+// wave 0's vmcnt then counts PPW + 1 per stage, the other waves' PPW.
+template <int GROUP_M, int ACT, bool WEPI = false, bool SC1 = false>
 __global__ __launch_bounds__(512, 2) void gemm_mx_kernel(MxArgs p) {
     using C = MxCfg;
-    __shared__ __attribute__((aligned(16))) char lds[C::LDS];
+    __shared__ __attribute__((aligned(16))) char lds[WEPI && MXW_LDS > C::LDS ? MXW_LDS : C::LDS];
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int wm = wave / C::WN, wn = wave % C::WN;
@@ -240,7 +321,7 @@ __global__ __launch_bounds__(512, 2) void gemm_mx_kernel(MxArgs p) {
                      : p.B + (size_t)min(n0 + prow, p.N - 1) * p.ldb + logical * 16;
     }
     // scale piece: lane L -> part L/16 (A b0, A b1, B b0, B b1), 16 rows (L%16)*16..; this wave owns lanes 8w..8w+7
-    const bool sc_mine = (lane >> 3) == wave;
+    const bool sc_mine = SC1 ? wave == 0 : (lane >> 3) == wave;
     const int part = lane >> 4, srow = (lane & 15) * 16;
     const uint8_t* sc_src = part < 2 ? p.sa + (size_t)part * p.sa_rows + m0 + srow
                                      : p.sb + (size_t)(part - 2) * p.sb_rows + n0 + srow;
@@ -251,7 +332,11 @@ __global__ __launch_bounds__(512, 2) void gemm_mx_kernel(MxArgs p) {
         const int k0 = st * C::BK;
 #pragma unroll
         for (int q = 0; q < C::PPW; ++q) glds16(src[q] + k0, base + (wave * C::PPW + q) * 1024);
-        if (sc_mine) glds16(sc_src + st * sc_step, base + C::A_ST + C::B_ST);
+        if (SC1) {
+            if (wave == 0) glds16(sc_src + st * sc_step, base + C::A_ST + C::B_ST);
+        } else if (sc_mine) {
+            glds16(sc_src + st * sc_step, base + C::A_ST + C::B_ST);
+        }
     };
 
     const unsigned lds0 = (unsigned)(uintptr_t)(LDS_AS char*)lds;
@@ -272,6 +357,12 @@ __global__ __launch_bounds__(512, 2) void gemm_mx_kernel(MxArgs p) {
 
     const int nk = p.K / C::BK;
     auto wait_rem = [&](int rem) {  // own DMA (PPW + 1 per stage) retired except `rem` later stages
+        if (SC1 && wave != 0) {  // SC1: waves 1..7 issue PPW per stage
+            if (rem >= 2) vm_wait<2 * C::PPW>();
+            else if (rem == 1) vm_wait<C::PPW>();
+            else vm_wait<0>();
+            return;
+        }
         if (rem >= 2) vm_wait<2 * (C::PPW + 1)>();
         else if (rem == 1) vm_wait<C::PPW + 1>();
         else vm_wait<0>();
@@ -331,7 +422,13 @@ __global__ __launch_bounds__(512, 2) void gemm_mx_kernel(MxArgs p) {
             }
         __builtin_amdgcn_s_setprio(0);
         __builtin_amdgcn_sched_barrier(0);
-        __builtin_amdgcn_s_barrier();
+        if (!(WEPI && wm == 1 && t == nk - 1)) __builtin_amdgcn_s_barrier();
+    }
+    if constexpr (WEPI) {
+        // no LDS hazard: every wave's last fragment reads and DMA waits precede the barrier closing
+        // the late row's last memory phase, which the early row passes before it writes its region
+        mx_epilogue_wave<ACT>(p, lds, acc, m0, n0, wave, lane);
+        return;
     }
     if (wm == 0) __builtin_amdgcn_s_barrier();
 
@@ -568,69 +665,7 @@ __device__ __forceinline__ void mx9_tile(const MxArgs& p, char* lds, const int m
         kS += 4u * (unsigned)sc_rows;
     }
 
-    // ---- per-wave epilogue: the wave's 128 x 64 tile in its own LDS region (pitch 144 B); lane
-    // (r32, h) holds row i*32 + r32, columns j*32 + 8q + 4h + (0..3)
-    char* reg = lds + wave * (128 * MX9_PITCH);
-    const int rm0 = m0 + wm * TM, cn0 = n0 + wn * TN;
-#pragma unroll
-    for (int j = 0; j < 2; ++j)
-#pragma unroll
-        for (int qd = 0; qd < 4; ++qd) {
-            const int nl = j * 32 + 8 * qd + 4 * h;
-            float bv[4] = {0.f, 0.f, 0.f, 0.f};
-            if (p.bias) {
-#pragma unroll
-                for (int r = 0; r < 4; ++r) bv[r] = bf2f(p.bias[min(cn0 + nl + r, p.N - 1)]);
-            }
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                bf16x4 o;
-#pragma unroll
-                for (int r = 0; r < 4; ++r) o[r] = f2bf(apply_act(acc[i][j][4 * qd + r] + bv[r], ACT));
-                *reinterpret_cast<bf16x4*>(reg + (i * 32 + r32) * MX9_PITCH + nl * 2) = o;
-            }
-        }
-    // the wave's own LDS writes precede its reads
-    const int rr = lane >> 3, cc = lane & 7;
-    if (!p.out_mx) {
-        bf16* Cout = reinterpret_cast<bf16*>(p.C);
-#pragma unroll 4
-        for (int q = 0; q < 16; ++q) {
-            const int row = q * 8 + rr, gr = rm0 + row, gc = cn0 + cc * 8;
-            const u16x8 v = *reinterpret_cast<const u16x8*>(reg + row * MX9_PITCH + cc * 16);
-            if (gr >= p.M || gc >= p.N) continue;
-            if (p.res) {
-                const int r2 = p.res_period ? gr % p.res_period : gr;
-                const u16x8 rv = *reinterpret_cast<const u16x8*>(p.res + (size_t)r2 * p.ldr + gc);
-                u16x8 o;
-#pragma unroll
-                for (int e = 0; e < 8; ++e) o[e] = __builtin_bit_cast(unsigned short, f2bf(bits2f(v[e]) + bits2f(rv[e])));
-                __builtin_nontemporal_store(o, reinterpret_cast<u16x8*>(Cout + (size_t)gr * p.ldc + gc));
-            } else {
-                __builtin_nontemporal_store(v, reinterpret_cast<u16x8*>(Cout + (size_t)gr * p.ldc + gc));
-            }
-        }
-    } else {
-        // mx8 output: lanes cc = 0..3 / 4..7 of a row hold its two 32-column blocks
-        uint8_t* Cq = reinterpret_cast<uint8_t*>(p.C);
-#pragma unroll 4
-        for (int q = 0; q < 16; ++q) {  // same trip count for every lane (shuffles)
-            const int row = q * 8 + rr, gr = rm0 + row, gc = cn0 + cc * 8;
-            const u16x8 v = *reinterpret_cast<const u16x8*>(reg + row * MX9_PITCH + cc * 16);
-            float f[8];
-            float a = 0.f;
-#pragma unroll
-            for (int e = 0; e < 8; ++e) {
-                f[e] = bits2f(v[e]);
-                a = fmaxf(a, fabsf(f[e]));
-            }
-            const int sbyte = mx_scale_byte(block_amax(a));
-            if (gr < p.M && gc < p.N) {
-                *reinterpret_cast<uint2*>(Cq + (size_t)gr * p.ldc + gc) = mx_pack8(f, sbyte);
-                if ((cc & 3) == 0) p.sc[(size_t)(gc >> 5) * p.sc_rows + gr] = (uint8_t)sbyte;
-            }
-        }
-    }
+    mx_epilogue_wave<ACT>(p, lds, acc, m0, n0, wave, lane);
 }
 
 template <int GROUP_M, int ACT>
@@ -671,22 +706,22 @@ int launch_mx9(const MxArgs& a, hipStream_t s) {
 
 int g_mx_variant = -1;  // dev: 9 = mx9 where its geometry holds
 
-template <int GROUP_M>
+template <int GROUP_M, bool WEPI = false, bool SC1 = false>
 int launch_mx(const MxArgs& a, hipStream_t s) {
     const int nbm = (a.M + 255) / 256, nbn = (a.N + 255) / 256;
     const dim3 grid(nbm * nbn), block(512);
     switch (a.act) {
         case MME_ACT_GELU_TANH:
-            hipLaunchKernelGGL((gemm_mx_kernel<GROUP_M, MME_ACT_GELU_TANH>), grid, block, 0, s, a);
+            hipLaunchKernelGGL((gemm_mx_kernel<GROUP_M, MME_ACT_GELU_TANH, WEPI, SC1>), grid, block, 0, s, a);
             break;
         case MME_ACT_QUICK_GELU:
-            hipLaunchKernelGGL((gemm_mx_kernel<GROUP_M, MME_ACT_QUICK_GELU>), grid, block, 0, s, a);
+            hipLaunchKernelGGL((gemm_mx_kernel<GROUP_M, MME_ACT_QUICK_GELU, WEPI, SC1>), grid, block, 0, s, a);
             break;
         case MME_ACT_GELU_ERF:
-            hipLaunchKernelGGL((gemm_mx_kernel<GROUP_M, MME_ACT_GELU_ERF>), grid, block, 0, s, a);
+            hipLaunchKernelGGL((gemm_mx_kernel<GROUP_M, MME_ACT_GELU_ERF, WEPI, SC1>), grid, block, 0, s, a);
             break;
         default:
-            hipLaunchKernelGGL((gemm_mx_kernel<GROUP_M, MME_ACT_NONE>), grid, block, 0, s, a);
+            hipLaunchKernelGGL((gemm_mx_kernel<GROUP_M, MME_ACT_NONE, WEPI, SC1>), grid, block, 0, s, a);
             break;
     }
     return mme_check_launch("mme_gemm_mx");
@@ -722,7 +757,7 @@ extern "C" int mme_layernorm_mx(const void* x, int ldx, const void* gamma, const
 }
 
 extern "C" int mme_gemm_mx_variant(int v) {  // dev / tests: 9 = mx9 (MME_DEV builds), -1 / 0 = production
-    MME_REQUIRE(v == -1 || v == 0 || v == 9, "mme_gemm_mx_variant: unknown variant %d", v);
+    MME_REQUIRE(v == -1 || v == 0 || v == 2 || v == 3 || v == 9, "mme_gemm_mx_variant: unknown variant %d", v);
 #ifndef MME_DEV
     MME_REQUIRE(v != 9, "mme_gemm_mx_variant: variant 9 (mx9) is a development form (build libmme_dev.so: make dev)");
 #endif
@@ -761,5 +796,7 @@ extern "C" int mme_gemm_mx(const void* A, int lda, const void* sa, int sa_rows, 
         (size_t)N * ldb < (1ull << 32) && (size_t)(K / 32) * (sa_rows > sb_rows ? sa_rows : sb_rows) < (1ull << 32))
         return launch_mx9<4>(a, as_stream(stream));
 #endif
+    if (g_mx_variant == 2) return launch_mx<4, true>(a, as_stream(stream));  // per-wave epilogue (A/B)
+    if (g_mx_variant == 3) return launch_mx<4, true, true>(a, as_stream(stream));  // + one scale-DMA wave
     return launch_mx<4>(a, as_stream(stream));
 }

@@ -12,6 +12,7 @@ oracle/mx.py restates them on the CPU.
 """
 from __future__ import annotations
 
+import os
 from dataclasses import dataclass
 from typing import Optional
 
@@ -79,10 +80,28 @@ def layernorm(x: torch.Tensor, g: torch.Tensor, b: torch.Tensor, eps: float, out
     return MXTensor(out.q, out.scales, rows, d)
 
 
+_variant_set = False
+
+
+def _apply_variant_env():
+    """MME_MX_VARIANT=<v>: mme_gemm_mx_variant(v) for every later mx GEMM (job-level A/B of kernel forms)."""
+    global _variant_set
+    _variant_set = True
+    v = os.environ.get("MME_MX_VARIANT")
+    if v is not None:
+        import ctypes
+        from . import _lib
+        lib = _lib.load()
+        lib.mme_gemm_mx_variant.argtypes = [ctypes.c_int]
+        lib.mme_gemm_mx_variant(int(v))
+
+
 def gemm(a: MXTensor, w: MXTensor, bias: Optional[torch.Tensor] = None, *, residual: Optional[torch.Tensor] = None,
          res_period: int = 0, act: int = ACT_NONE, out: Optional[torch.Tensor] = None,
          out_mx: Optional[MXTensor] = None, algo_flops: Optional[float] = None):
     """act(a @ w.T + bias) (+ residual): bf16 [M, N] into `out`, or mx8 into `out_mx`."""
+    if not _variant_set:
+        _apply_variant_env()
     if a.k != w.k:
         raise ValueError(f"gemm_mx: K mismatch {a.k} vs {w.k}")
     M, N, K = a.rows, w.rows, a.k

@@ -220,3 +220,38 @@ def test_gemm_mx9_bit_identical_to_mx(cuda, M, N, K):
     torch.cuda.synchronize()
     for o_, n_, what in zip(old, new, ("bf16 + act", "residual", "mx8 values", "mx8 scales")):
         assert torch.equal(o_, n_), f"mx9 differs from the half-line kernel ({what}, {M}x{N}x{K})"
+
+
+# gemm_mx_kernel's per-wave epilogue (mme_gemm_mx_variant(2), round 3) runs the whole-tile epilogue's
+# arithmetic in each wave's own LDS region, and variant 3 adds the single-wave scale DMA: bit-identical outputs (bf16 + bias, + residual in place,
+# mx8 re-quantised output with an activation), ragged M and N off the 256 grid included.
+@pytest.mark.parametrize("M,N,K,kind", [(1000, 3840, 1280, "bias"), (777, 1280, 5120, "res"),
+                                         (2048, 5120, 1280, "mx_out"), (300, 544, 192, "mx_out"),
+                                         (129, 96, 192, "res")])
+def test_gemm_mx_wave_epilogue_bit_identical(cuda, M, N, K, kind):
+    import ctypes
+    lib = _lib.load()
+    lib.mme_gemm_mx_variant.argtypes = [ctypes.c_int]
+    g = torch.Generator(device="cuda").manual_seed(M + N + K)
+    a = mx.quantize(rnd(M, K, gen=g))
+    w = mx.quantize(rnd(N, K, scale=1 / math.sqrt(K), gen=g))
+    bias = rnd(N, scale=0.1, gen=g)
+    res0 = rnd(M, N, gen=g)
+    outs = []
+    for v in (-1, 2, 3):
+        assert lib.mme_gemm_mx_variant(v) == 0
+        try:
+            if kind == "mx_out":
+                o = mx.MXTensor.empty(M, N, "cuda")
+                mx.gemm(a, w, bias, act=_lib.ACT_QUICK_GELU, out_mx=o)
+                outs.append((o.q[:M, :N].clone(), o.scales[:, :M].clone()))
+            else:
+                x = res0.clone()
+                y = mx.gemm(a, w, bias, residual=x if kind == "res" else None, out=x)
+                outs.append((y.clone(),))
+            torch.cuda.synchronize()
+        finally:
+            lib.mme_gemm_mx_variant(-1)
+    for o in outs[1:]:
+        for p, q in zip(outs[0], o):
+            assert torch.equal(p, q), f"per-wave mx epilogue / single-wave scale DMA differs ({kind}, {M}x{N}x{K})"

@@ -33,6 +33,8 @@ def main():
     p.add_argument("--mx", action="store_true", help="also time the mx8 (block-scaled fp8) GEMM")
     p.add_argument("--mx-variants", default="-1", help="mme_gemm_mx_variant values to time with --mx "
                    "(-1 = production dispatch, 9 = mx9 in libmme_dev.so)")
+    p.add_argument("--mx-epi", default="none", help="mx8 epilogue: none | job (the fp8 job's: QKV bias, fc1 "
+                   "bias + quick_gelu to an mx8 output, fc2 bias + residual in place)")
     p.add_argument("--torch", action="store_true", help="also time torch F.linear (hipBLASLt) on each shape")
     p.add_argument("--epi", default="none", help="epilogue: none | bias | res (residual in place) | resstats (res + LayerNorm "
                    "statistics, mme_gemm_res_stats) | gelu (bias+gelu_tanh)")
@@ -116,23 +118,39 @@ def main():
             from mme import mx
             lib.mme_gemm_mx_variant.argtypes = [ctypes.c_int]
             Aq, Wq = mx.quantize(A), mx.quantize(W)
+            mkw, omx = {}, None
+            if a.mx_epi == "job":
+                mkw = {"bias": bias}
+                if name.endswith("fc1"):
+                    omx = mx.MXTensor.empty(M, N, "cuda")
+                    mkw.update(act=_lib.ACT_QUICK_GELU, out_mx=omx)
+                elif name.endswith("fc2"):
+                    mkw.update(residual=C)
+            if "out_mx" not in mkw:
+                mkw["out"] = C
             first = None
             for mv in [int(v) for v in a.mx_variants.split(",")]:
                 lib.mme_gemm_mx_variant(mv)
-                Cm = mx.gemm(Aq, Wq, out=C)
-                err = (Cm.float() - ref.float()).abs().max().item() if ref is not None else 0.0
+                C0 = C.clone()
+                Cm = mx.gemm(Aq, Wq, **mkw)
+                snap = (omx.q.clone(), omx.scales[:, :M].clone()) if omx is not None else (Cm.clone(),)
+                if omx is None:
+                    err = (Cm.float() - ref.float()).abs().max().item() if ref is not None and not a.mx_epi == "job" else 0.0
+                else:
+                    err = 0.0
+                C.copy_(C0)  # in-place residual: restore the operand between variants
                 if first is None:
-                    first = Cm.clone()
-                same = bool(torch.equal(Cm, first))
+                    first = snap
+                same = all(bool(torch.equal(x, y)) for x, y in zip(snap, first))
                 for _ in range(3):
-                    mx.gemm(Aq, Wq, out=C)
+                    mx.gemm(Aq, Wq, **mkw)
                 torch.cuda.synchronize()
                 s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 ms = 1e30
                 for rep in range(3):  # best of 3 timed groups
                     s.record()
                     for _ in range(a.iters):
-                        mx.gemm(Aq, Wq, out=C)
+                        mx.gemm(Aq, Wq, **mkw)
                     e.record()
                     torch.cuda.synchronize()
                     ms = min(ms, s.elapsed_time(e) / a.iters)
