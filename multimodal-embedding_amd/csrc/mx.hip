@@ -756,8 +756,9 @@ extern "C" int mme_layernorm_mx(const void* x, int ldx, const void* gamma, const
     return mme_check_launch("mme_layernorm_mx");
 }
 
-extern "C" int mme_gemm_mx_variant(int v) {  // dev / tests: 9 = mx9 (MME_DEV builds), -1 / 0 = production
-    MME_REQUIRE(v == -1 || v == 0 || v == 2 || v == 3 || v == 9, "mme_gemm_mx_variant: unknown variant %d", v);
+extern "C" int mme_gemm_mx_variant(int v) {  // A/B and tests: -1 = production, 0 = round-2 form, 2 = per-wave
+                                             // epilogue alone, 9 = mx9 (MME_DEV builds)
+    MME_REQUIRE(v == -1 || v == 0 || v == 2 || v == 9, "mme_gemm_mx_variant: unknown variant %d", v);
 #ifndef MME_DEV
     MME_REQUIRE(v != 9, "mme_gemm_mx_variant: variant 9 (mx9) is a development form (build libmme_dev.so: make dev)");
 #endif
@@ -796,7 +797,9 @@ extern "C" int mme_gemm_mx(const void* A, int lda, const void* sa, int sa_rows, 
         (size_t)N * ldb < (1ull << 32) && (size_t)(K / 32) * (sa_rows > sb_rows ? sa_rows : sb_rows) < (1ull << 32))
         return launch_mx9<4>(a, as_stream(stream));
 #endif
-    if (g_mx_variant == 2) return launch_mx<4, true>(a, as_stream(stream));  // per-wave epilogue (A/B)
-    if (g_mx_variant == 3) return launch_mx<4, true, true>(a, as_stream(stream));  // + one scale-DMA wave
-    return launch_mx<4>(a, as_stream(stream));
+    // production since round 3: per-wave epilogue + one scale-DMA wave (DFN5B-H fp8 job 1 016 -> 1 028
+    // img/s, profiles/r03_v14_*); variant 0 = the round-2 form, 2 = the per-wave epilogue alone (A/B)
+    if (g_mx_variant == 0) return launch_mx<4>(a, as_stream(stream));
+    if (g_mx_variant == 2) return launch_mx<4, true>(a, as_stream(stream));
+    return launch_mx<4, true, true>(a, as_stream(stream));
 }

@@ -32,7 +32,7 @@ def main():
     p.add_argument("--shapes", default="qkv,o_proj,fc1,fc2")
     p.add_argument("--mx", action="store_true", help="also time the mx8 (block-scaled fp8) GEMM")
     p.add_argument("--mx-variants", default="-1", help="mme_gemm_mx_variant values to time with --mx "
-                   "(-1 = production dispatch, 9 = mx9 in libmme_dev.so)")
+                   "(-1 = production, 0 = round-2 form, 2 = per-wave epilogue alone, 9 = mx9 in libmme_dev.so)")
     p.add_argument("--mx-epi", default="none", help="mx8 epilogue: none | job (the fp8 job's: QKV bias, fc1 "
                    "bias + quick_gelu to an mx8 output, fc2 bias + residual in place)")
     p.add_argument("--torch", action="store_true", help="also time torch F.linear (hipBLASLt) on each shape")
@@ -129,16 +129,16 @@ def main():
             if "out_mx" not in mkw:
                 mkw["out"] = C
             first = None
+            C0 = C.clone()  # the in-place residual's operand, restored before every variant's check
             for mv in [int(v) for v in a.mx_variants.split(",")]:
                 lib.mme_gemm_mx_variant(mv)
-                C0 = C.clone()
+                C.copy_(C0)
                 Cm = mx.gemm(Aq, Wq, **mkw)
                 snap = (omx.q.clone(), omx.scales[:, :M].clone()) if omx is not None else (Cm.clone(),)
                 if omx is None:
                     err = (Cm.float() - ref.float()).abs().max().item() if ref is not None and not a.mx_epi == "job" else 0.0
                 else:
                     err = 0.0
-                C.copy_(C0)  # in-place residual: restore the operand between variants
                 if first is None:
                     first = snap
                 same = all(bool(torch.equal(x, y)) for x, y in zip(snap, first))
