@@ -211,6 +211,36 @@ struct MxCfg {
 };
 
 __device__ __forceinline__ int mxswz(int row, int chunk) { return chunk ^ ((row >> 2) & 3); }
+template <int V>
+struct IC2 {  // an int as a type (compile-time ds offsets through generic lambdas)
+    static constexpr int value = V;
+};
+
+// Raw-buffer LDS-DMA helpers (mx9 / mx10): four 1 KiB pieces LDS m0base + q KiB <- rsrc base +
+// voff[q] + soff, M0 stepped by s_add (its SCC write declared).
+typedef int i32x4v __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ i32x4v mx_rsrc(const void* base, unsigned bytes) {
+    const unsigned long long b = (unsigned long long)(uintptr_t)base;
+    i32x4v r;
+    r[0] = __builtin_amdgcn_readfirstlane((int)(unsigned)b);
+    r[1] = __builtin_amdgcn_readfirstlane((int)(unsigned)(b >> 32));
+    r[2] = __builtin_amdgcn_readfirstlane((int)bytes);
+    r[3] = 0x00020000;
+    return r;
+}
+__device__ __forceinline__ void mx_dma4(unsigned m0base, const unsigned (&voff)[4], i32x4v rsrc, unsigned soff) {
+    asm volatile(
+        "s_mov_b32 m0, %0\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %5, %6 offen lds\n\t"
+        "s_add_u32 m0, m0, 0x400\n\ts_nop 0\n\tbuffer_load_dwordx4 %2, %5, %6 offen lds\n\t"
+        "s_add_u32 m0, m0, 0x400\n\ts_nop 0\n\tbuffer_load_dwordx4 %3, %5, %6 offen lds\n\t"
+        "s_add_u32 m0, m0, 0x400\n\ts_nop 0\n\tbuffer_load_dwordx4 %4, %5, %6 offen lds"
+        ::"s"(m0base), "v"(voff[0]), "v"(voff[1]), "v"(voff[2]), "v"(voff[3]), "s"(rsrc), "s"(soff)
+        : "memory", "m0", "scc");  // s_add_u32 writes SCC
+}
+__device__ __forceinline__ void mx_dma1(unsigned m0base, unsigned voff, i32x4v rsrc, unsigned soff) {
+    asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, %3 offen lds"
+                 ::"s"(m0base), "v"(voff), "s"(rsrc), "s"(soff) : "memory", "m0", "scc");
+}
 
 // Per-wave epilogue of the mx8 GEMMs (gemm_mx_kernel WEPI, mx9): each wave stages its own 128 x 64
 // sub-tile in its own LDS region (pitch 144 B, 18 KiB; 144 KiB for the 8 waves), reads it back as
@@ -496,6 +526,187 @@ __global__ __launch_bounds__(512, 2) void gemm_mx_kernel(MxArgs p) {
     }
 }
 
+
+// ---------------------------------------------------------------------------
+// mx10 (round 3): gemm_mx_kernel's LDS layout, 4-slot ring, K order, MFMA sequence and per-wave
+// epilogue (so bit-identical outputs), with pipe9's treatment of the per-stage bookkeeping:
+//   * the wave rows (LATE) and the scale-DMA wave (SCW, wave 0) run separate instantiations, so
+//     every wait count and barrier is static;
+//   * steady-state stages are unrolled by the ring depth (4): ring slots are immediates, and the
+//     fragment / scale reads take them as ds offset fields (two bases: slots 0-1 and 2-3, since the
+//     field holds 16 bits);
+//   * the data pieces are buffer_load_dwordx4 ... lds with per-lane row offsets fixed for the tile
+//     and the K offset in soffset (one SGPR add per stage) instead of a 64-bit address per piece.
+// Needs K % 64 == 0, K >= 256 (4 stages) and operands < 4 GiB (32-bit offsets).
+// ---------------------------------------------------------------------------
+template <int ACT, bool LATE, bool SCW>
+__device__ __forceinline__ void mx10_tile(const MxArgs& p, char* lds, const int m0, const int n0, const int wave) {
+    using C = MxCfg;
+    static_assert(C::PPW == 4 && C::NSTAGE == 4, "mx10: 4 data pieces per wave, 4-slot ring");
+    const int lane = threadIdx.x & 63;
+    const int wm = wave / C::WN, wn = wave % C::WN;
+    const int h = lane >> 5, r32 = lane & 31;
+    // data pieces: waves 0-3 carry A, waves 4-7 B; piece q = 16 rows x 64 B, lane -> row lane / 4
+    const bool isA = wave < 4;
+    unsigned voff[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const int prow = ((wave & 3) * 4 + q) * 16 + (lane >> 2);
+        const int logical = mxswz(prow, lane & 3);
+        voff[q] = isA ? (unsigned)min(m0 + prow, p.M - 1) * (unsigned)p.lda + logical * 16
+                      : (unsigned)min(n0 + prow, p.N - 1) * (unsigned)p.ldb + logical * 16;
+    }
+    const i32x4v rs = isA ? mx_rsrc(p.A, (unsigned)((size_t)p.M * p.lda)) : mx_rsrc(p.B, (unsigned)((size_t)p.N * p.ldb));
+    // scale piece (wave 0, all lanes): part = lane / 16 (A b0, A b1, B b0, B b1), rows (lane % 16) * 16..
+    const int part = lane >> 4, srow = (lane & 15) * 16;
+    const uint8_t* sc_src = part < 2 ? p.sa + (size_t)part * p.sa_rows + m0 + srow
+                                     : p.sb + (size_t)(part - 2) * p.sb_rows + n0 + srow;
+    const size_t sc_step = part < 2 ? (size_t)2 * p.sa_rows : (size_t)2 * p.sb_rows;
+    const unsigned lds0 = (unsigned)(uintptr_t)(LDS_AS char*)lds;
+    const unsigned lw = __builtin_amdgcn_readfirstlane(lds0 + wave * 4096);
+    char* lds_sc = lds + C::A_ST + C::B_ST;  // + slot * STAGE
+
+    const int sw = (lane >> 2) & 3;
+    const unsigned c0 = (unsigned)((h ^ sw) << 4), c1 = (unsigned)(((2 + h) ^ sw) << 4);
+    // two bases per operand: slots 0 / 1 at base + {0, STAGE}, slots 2 / 3 at base2 + {0, STAGE}
+    const unsigned a0 = lds0 + (wm * C::TM + r32) * 64 + c0, a1 = lds0 + (wm * C::TM + r32) * 64 + c1;
+    const unsigned b0 = lds0 + C::A_ST + (wn * C::TN + r32) * 64 + c0, b1 = lds0 + C::A_ST + (wn * C::TN + r32) * 64 + c1;
+    const unsigned sa_l = lds0 + C::A_ST + C::B_ST + h * 256 + wm * C::TM + r32;
+    const unsigned sb_l = lds0 + C::A_ST + C::B_ST + 512 + h * 256 + wn * C::TN + r32;
+    constexpr unsigned HI = 2 * C::STAGE;
+
+    f32x16 acc[C::FM][C::FN];
+#pragma unroll
+    for (int i = 0; i < C::FM; ++i)
+#pragma unroll
+        for (int j = 0; j < C::FN; ++j)
+#pragma unroll
+            for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
+
+    constexpr int PER = C::PPW + (SCW ? 1 : 0);  // this wave's DMA instructions per stage
+    auto wait = [&](int rem) __attribute__((always_inline)) {
+        if (rem >= 2) vm_wait<2 * PER>();
+        else if (rem == 1) vm_wait<PER>();
+        else vm_wait<0>();
+    };
+    auto issue = [&](int st, int slot) __attribute__((always_inline)) {  // slot: run-time or immediate
+        mx_dma4(lw + (unsigned)slot * C::STAGE, voff, rs, (unsigned)st * C::BK);
+        if (SCW) glds16(sc_src + st * sc_step, lds_sc + slot * C::STAGE);
+    };
+    // one stage: fragment / scale reads of slot SL (reads at base + OFF, OFF an immediate),
+    // optional DMA of stage `ist` into slot `isl`, counted wait, barrier, 8 MFMAs, barrier
+    auto stage = [&](auto SLc, unsigned abase0, unsigned abase1, unsigned bbase0, unsigned bbase1, unsigned sab,
+                     unsigned sbb, bool dma, int ist, int isl, int rem, bool end_barrier) __attribute__((always_inline)) {
+        constexpr int OFF = decltype(SLc)::value;
+        bf16x8 a[C::FM][2], b[C::FN][2];
+        unsigned sa[C::FM], sbv[C::FN];
+        ds_read16<OFF + 0 * 2048>(b[0][0], bbase0);
+        ds_read16<OFF + 0 * 2048>(b[0][1], bbase1);
+        ds_read16<OFF + 1 * 2048>(b[1][0], bbase0);
+        ds_read16<OFF + 1 * 2048>(b[1][1], bbase1);
+#pragma unroll
+        for (int i = 0; i < C::FM; ++i) {
+            if (i == 0) { ds_read16<OFF + 0 * 2048>(a[0][0], abase0); ds_read16<OFF + 0 * 2048>(a[0][1], abase1); }
+            if (i == 1) { ds_read16<OFF + 1 * 2048>(a[1][0], abase0); ds_read16<OFF + 1 * 2048>(a[1][1], abase1); }
+            if (i == 2) { ds_read16<OFF + 2 * 2048>(a[2][0], abase0); ds_read16<OFF + 2 * 2048>(a[2][1], abase1); }
+            if (i == 3) { ds_read16<OFF + 3 * 2048>(a[3][0], abase0); ds_read16<OFF + 3 * 2048>(a[3][1], abase1); }
+        }
+        asm volatile("ds_read_u8 %0, %1 offset:%2" : "=v"(sbv[0]) : "v"(sbb), "n"(OFF + 0) : "memory");
+        asm volatile("ds_read_u8 %0, %1 offset:%2" : "=v"(sbv[1]) : "v"(sbb), "n"(OFF + 32) : "memory");
+        asm volatile("ds_read_u8 %0, %1 offset:%2" : "=v"(sa[0]) : "v"(sab), "n"(OFF + 0) : "memory");
+        asm volatile("ds_read_u8 %0, %1 offset:%2" : "=v"(sa[1]) : "v"(sab), "n"(OFF + 32) : "memory");
+        asm volatile("ds_read_u8 %0, %1 offset:%2" : "=v"(sa[2]) : "v"(sab), "n"(OFF + 64) : "memory");
+        asm volatile("ds_read_u8 %0, %1 offset:%2" : "=v"(sa[3]) : "v"(sab), "n"(OFF + 96) : "memory");
+        if (dma) issue(ist, isl);
+        wait(rem);
+        lgkm_wait<0>();
+        __builtin_amdgcn_s_barrier();
+        __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+        for (int i = 0; i < C::FM; ++i)
+#pragma unroll
+            for (int j = 0; j < C::FN; ++j) {
+                const i32x8 bo = __builtin_bit_cast(i32x8, __builtin_shufflevector(b[j][0], b[j][1], 0, 1, 2, 3, 4, 5, 6,
+                                                                                  7, 8, 9, 10, 11, 12, 13, 14, 15));
+                const i32x8 ao = __builtin_bit_cast(i32x8, __builtin_shufflevector(a[i][0], a[i][1], 0, 1, 2, 3, 4, 5, 6,
+                                                                                  7, 8, 9, 10, 11, 12, 13, 14, 15));
+                acc[i][j] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(bo, ao, acc[i][j], 0, 0, 0, (int)sbv[j], 0,
+                                                                             (int)sa[i]);
+            }
+        __builtin_amdgcn_s_setprio(0);
+        __builtin_amdgcn_sched_barrier(0);
+        if (end_barrier) __builtin_amdgcn_s_barrier();
+    };
+    using S0 = IC2<0>;
+    using S1 = IC2<C::STAGE>;
+    const int nk = p.K / C::BK;
+
+    // prologue: stages 0..2 into slots 0..2
+    issue(0, 0);
+    issue(1, 1);
+    issue(2, 2);
+    wait(2);  // stage 0 landed
+    __builtin_amdgcn_s_barrier();
+    if (LATE) __builtin_amdgcn_s_barrier();
+
+    // steady state: stage t (slot t & 3) issues stage t + 3 into slot (t + 3) & 3 while t + 3 < nk
+    int t = 0;
+    for (; t + 4 <= nk - 3; t += 4) {
+        stage(S0{}, a0, a1, b0, b1, sa_l, sb_l, true, t + 3, 3, 2, true);
+        stage(S1{}, a0, a1, b0, b1, sa_l, sb_l, true, t + 4, 0, 2, true);
+        stage(S0{}, a0 + HI, a1 + HI, b0 + HI, b1 + HI, sa_l + HI, sb_l + HI, true, t + 5, 1, 2, true);
+        stage(S1{}, a0 + HI, a1 + HI, b0 + HI, b1 + HI, sa_l + HI, sb_l + HI, true, t + 6, 2, 2, true);
+    }
+    // remaining steady stages (0..3) and the last three stages: run-time slots (base + slot * STAGE)
+    for (; t < nk; ++t) {
+        const unsigned so = (unsigned)(t & 3) * C::STAGE;
+        const bool dma = t + 3 < nk;
+        const int rem = dma ? 2 : (nk - 2 - t > 0 ? nk - 2 - t : 0);
+        stage(S0{}, a0 + so, a1 + so, b0 + so, b1 + so, sa_l + so, sb_l + so, dma, t + 3, (t + 3) & 3, rem,
+              !(LATE && t == nk - 1));
+    }
+    // no LDS hazard: every wave's last fragment reads and DMA waits precede the barrier closing the
+    // late row's last memory phase, which the early row passes before it writes its region
+    mx_epilogue_wave<ACT>(p, lds, acc, m0, n0, wave, lane);
+}
+
+template <int GROUP_M, int ACT>
+__global__ __launch_bounds__(512, 2) void gemm_mx10_kernel(MxArgs p) {
+    using C = MxCfg;
+    __shared__ __attribute__((aligned(16))) char lds[MXW_LDS > C::LDS ? MXW_LDS : C::LDS];
+    const int nbm = (p.M + C::BM - 1) / C::BM, nbn = (p.N + C::BN - 1) / C::BN;
+    const int tile = xcd_remap(blockIdx.x, gridDim.x);
+    int bm, bn;
+    tile_coords<GROUP_M>(tile, nbm, nbn, bm, bn);
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    if (wave == 0)
+        mx10_tile<ACT, false, true>(p, lds, bm * C::BM, bn * C::BN, wave);
+    else if (wave < 4)
+        mx10_tile<ACT, false, false>(p, lds, bm * C::BM, bn * C::BN, wave);
+    else
+        mx10_tile<ACT, true, false>(p, lds, bm * C::BM, bn * C::BN, wave);
+}
+
+template <int GROUP_M>
+int launch_mx10(const MxArgs& a, hipStream_t s) {
+    const dim3 grid(((a.M + 255) / 256) * ((a.N + 255) / 256)), block(512);
+    switch (a.act) {
+        case MME_ACT_GELU_TANH:
+            hipLaunchKernelGGL((gemm_mx10_kernel<GROUP_M, MME_ACT_GELU_TANH>), grid, block, 0, s, a);
+            break;
+        case MME_ACT_QUICK_GELU:
+            hipLaunchKernelGGL((gemm_mx10_kernel<GROUP_M, MME_ACT_QUICK_GELU>), grid, block, 0, s, a);
+            break;
+        case MME_ACT_GELU_ERF:
+            hipLaunchKernelGGL((gemm_mx10_kernel<GROUP_M, MME_ACT_GELU_ERF>), grid, block, 0, s, a);
+            break;
+        default:
+            hipLaunchKernelGGL((gemm_mx10_kernel<GROUP_M, MME_ACT_NONE>), grid, block, 0, s, a);
+            break;
+    }
+    return mme_check_launch("mme_gemm_mx");
+}
+
 #ifdef MME_DEV
 // ---------------------------------------------------------------------------
 // mx9 (dev variant 9, round 3; MME_DEV builds only): the block-scaled fp8 GEMM on
@@ -514,30 +725,6 @@ __global__ __launch_bounds__(512, 2) void gemm_mx_kernel(MxArgs p) {
 // (stage loop unrolled by 2), DMA by buffer_load ... lds with the K offset in soffset.
 // Per-wave epilogue (no workgroup barrier), bf16 + residual or mx8 re-quantisation.
 // ---------------------------------------------------------------------------
-typedef int i32x4v __attribute__((ext_vector_type(4)));
-__device__ __forceinline__ i32x4v mx_rsrc(const void* base, unsigned bytes) {
-    const unsigned long long b = (unsigned long long)(uintptr_t)base;
-    i32x4v r;
-    r[0] = __builtin_amdgcn_readfirstlane((int)(unsigned)b);
-    r[1] = __builtin_amdgcn_readfirstlane((int)(unsigned)(b >> 32));
-    r[2] = __builtin_amdgcn_readfirstlane((int)bytes);
-    r[3] = 0x00020000;
-    return r;
-}
-__device__ __forceinline__ void mx_dma4(unsigned m0base, const unsigned (&voff)[4], i32x4v rsrc, unsigned soff) {
-    asm volatile(
-        "s_mov_b32 m0, %0\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %5, %6 offen lds\n\t"
-        "s_add_u32 m0, m0, 0x400\n\ts_nop 0\n\tbuffer_load_dwordx4 %2, %5, %6 offen lds\n\t"
-        "s_add_u32 m0, m0, 0x400\n\ts_nop 0\n\tbuffer_load_dwordx4 %3, %5, %6 offen lds\n\t"
-        "s_add_u32 m0, m0, 0x400\n\ts_nop 0\n\tbuffer_load_dwordx4 %4, %5, %6 offen lds"
-        ::"s"(m0base), "v"(voff[0]), "v"(voff[1]), "v"(voff[2]), "v"(voff[3]), "s"(rsrc), "s"(soff)
-        : "memory", "m0", "scc");  // s_add_u32 writes SCC
-}
-__device__ __forceinline__ void mx_dma1(unsigned m0base, unsigned voff, i32x4v rsrc, unsigned soff) {
-    asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, %3 offen lds"
-                 ::"s"(m0base), "v"(voff), "s"(rsrc), "s"(soff) : "memory", "m0", "scc");
-}
-
 constexpr int MX9_UNIT = 32768, MX9_SC = 4 * MX9_UNIT, MX9_PITCH = 144;
 constexpr int MX9_LDS = 8 * 128 * MX9_PITCH;  // per-wave epilogue tiles; the main loop uses less
 static_assert(MX9_SC + 4096 + 5 * 1024 + 2048 + 1024 <= MX9_LDS, "mx9: scale slots + scratch pieces fit");
@@ -756,9 +943,9 @@ extern "C" int mme_layernorm_mx(const void* x, int ldx, const void* gamma, const
     return mme_check_launch("mme_layernorm_mx");
 }
 
-extern "C" int mme_gemm_mx_variant(int v) {  // A/B and tests: -1 = production, 0 = round-2 form, 2 = per-wave
-                                             // epilogue alone, 9 = mx9 (MME_DEV builds)
-    MME_REQUIRE(v == -1 || v == 0 || v == 2 || v == 9, "mme_gemm_mx_variant: unknown variant %d", v);
+extern "C" int mme_gemm_mx_variant(int v) {  // A/B and tests: -1 = production (mx10), 0 = round-2 form,
+                                             // 2 = + per-wave epilogue, 3 = + scale wave, 9 = mx9 (MME_DEV)
+    MME_REQUIRE(v == -1 || v == 0 || v == 2 || v == 3 || v == 9, "mme_gemm_mx_variant: unknown variant %d", v);
 #ifndef MME_DEV
     MME_REQUIRE(v != 9, "mme_gemm_mx_variant: variant 9 (mx9) is a development form (build libmme_dev.so: make dev)");
 #endif
@@ -797,9 +984,14 @@ extern "C" int mme_gemm_mx(const void* A, int lda, const void* sa, int sa_rows, 
         (size_t)N * ldb < (1ull << 32) && (size_t)(K / 32) * (sa_rows > sb_rows ? sa_rows : sb_rows) < (1ull << 32))
         return launch_mx9<4>(a, as_stream(stream));
 #endif
-    // production since round 3: per-wave epilogue + one scale-DMA wave (DFN5B-H fp8 job 1 016 -> 1 028
-    // img/s, profiles/r03_v14_*); variant 0 = the round-2 form, 2 = the per-wave epilogue alone (A/B)
+    // production since round 3: mx10 (static slots / waits, buffer-load DMA, per-wave epilogue, one
+    // scale-DMA wave) where its geometry holds: DFN5B-H fp8 job 1 016 -> 1 028 (per-wave epilogue +
+    // scale wave, profiles/r03_v14_*) -> 1 041 img/s (mx10, profiles/r03_v15_*); elsewhere the
+    // gemm_mx_kernel form with the same epilogue and scale wave. A/B forms: variant 0 = the round-2
+    // kernel, 2 = its per-wave epilogue alone, 3 = + the scale wave (mx10's fallback).
+    const bool mx10_ok = K >= 256 && (size_t)M * lda < (1ull << 32) && (size_t)N * ldb < (1ull << 32);
     if (g_mx_variant == 0) return launch_mx<4>(a, as_stream(stream));
     if (g_mx_variant == 2) return launch_mx<4, true>(a, as_stream(stream));
-    return launch_mx<4, true, true>(a, as_stream(stream));
+    if (g_mx_variant == 3 || !mx10_ok) return launch_mx<4, true, true>(a, as_stream(stream));
+    return launch_mx10<4>(a, as_stream(stream));
 }

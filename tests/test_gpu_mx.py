@@ -222,13 +222,14 @@ def test_gemm_mx9_bit_identical_to_mx(cuda, M, N, K):
         assert torch.equal(o_, n_), f"mx9 differs from the half-line kernel ({what}, {M}x{N}x{K})"
 
 
-# gemm_mx_kernel's per-wave epilogue (round 3; variant 2 alone, production with the single-wave scale
-# DMA) runs the whole-tile epilogue's arithmetic (variant 0, the round-2 form) in each wave's own LDS
-# region: bit-identical outputs (bf16 + bias, + residual in place,
+# Round 3's fp8 GEMM forms against the round-2 kernel (variant 0): its per-wave epilogue (2), + the
+# single-wave scale DMA (3), and mx10 (production: static slots / waits, buffer-load DMA) run the same
+# MFMA sequence and epilogue arithmetic: bit-identical outputs (bf16 + bias, + residual in place,
 # mx8 re-quantised output with an activation), ragged M and N off the 256 grid included.
 @pytest.mark.parametrize("M,N,K,kind", [(1000, 3840, 1280, "bias"), (777, 1280, 5120, "res"),
                                          (2048, 5120, 1280, "mx_out"), (300, 544, 192, "mx_out"),
-                                         (129, 96, 192, "res")])
+                                         (129, 96, 192, "res"), (513, 256, 256, "bias"), (300, 512, 320, "res"),
+                                         (257, 768, 448, "mx_out"), (600, 1024, 512, "bias"), (64, 256, 576, "bias")])
 def test_gemm_mx_wave_epilogue_bit_identical(cuda, M, N, K, kind):
     import ctypes
     lib = _lib.load()
@@ -239,7 +240,7 @@ def test_gemm_mx_wave_epilogue_bit_identical(cuda, M, N, K, kind):
     bias = rnd(N, scale=0.1, gen=g)
     res0 = rnd(M, N, gen=g)
     outs = []
-    for v in (0, 2, -1):  # round-2 form, per-wave epilogue alone, production (+ single-wave scale DMA)
+    for v in (0, 2, 3, -1):  # round-2 form, + per-wave epilogue, + single-wave scale DMA, production (mx10)
         assert lib.mme_gemm_mx_variant(v) == 0
         try:
             if kind == "mx_out":
