@@ -1857,7 +1857,8 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(2))) vo
 //   the running max lives with the S^T lanes, so the (lazy) rescale shuffles alpha over.
 // ---------------------------------------------------------------------------
 // SKIP: 0 none; 1 = a tile whose second 32-key block lies wholly past the keys skips that
-// block's MFMAs (kind 62); 2 = the same with literal-zero accumulator starts (kind 63).
+// block's MFMAs (round 2's kind 62, now dev kind 63); 2 = the same with literal-zero accumulator
+// starts (production kind 62 since round 3).
 template <int HD, int NW, int MINW, bool PRIO, int SKIP = 0>
 __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(MINW))) void attn_hyb_kernel(AttnArgs a) {
     static_assert(HD == 72 || HD == 80, "80-deep QK^T, 80 PV rows");
@@ -2297,10 +2298,11 @@ bool launch_attn(int kind, const AttnArgs& a, int B, int T, int H, hipStream_t s
                           // for hd 80 in 9-wave blocks (ViT-H T 257: +2-4 %, profiles/r03_v11_attn_vith_ab.log)
         hipLaunchKernelGGL((attn_m32_kernel<HD, 9, 1, true, false, false, true>), dim3(cdiv(T, 288) * H * B),
                            dim3(576), 0, st, a);
-    else if (kind == 62) {  // attn_hyb_kernel skipping a tile's second key block when it lies past the keys:
-                            // production for hd 72
+    else if (kind == 62) {  // attn_hyb_kernel skipping a tile's second key block when it lies past the keys,
+                            // literal-zero QK^T starts (since round 3: +0.5-0.7 %, bit-identical,
+                            // profiles/r03_v18_attn_bufdma_literal_zero_ab.log): production for hd 72
         if constexpr (HD != 64)
-            hipLaunchKernelGGL((attn_hyb_kernel<HD, 8, 4, true, 1>), dim3(cdiv(T, 256) * H * B), dim3(512), 0, st, a);
+            hipLaunchKernelGGL((attn_hyb_kernel<HD, 8, 4, true, 2>), dim3(cdiv(T, 256) * H * B), dim3(512), 0, st, a);
         else
             hipLaunchKernelGGL((attn_m32_kernel<HD, 8, 1, true>), dim3(cdiv(T, 256) * H * B), dim3(512), 0, st, a);
     } else
@@ -2431,9 +2433,10 @@ bool launch_attn_dev(int kind, const AttnArgs& a, int B, int T, int H, hipStream
         } else {
             hipLaunchKernelGGL((attn_m32_kernel<HD, 8, 1, true>), dim3(cdiv(T, 256) * H * B), dim3(512), 0, st, a);
         }
-    } else if (kind == 63) {  // kind 62 with literal-zero QK^T accumulator starts (no per-tile register init)
+    } else if (kind == 63) {  // dev: kind 62 as in round 2 (the skipped block's fill and the accumulator
+                              // init as per-tile register moves)
         if constexpr (HD != 64)
-            hipLaunchKernelGGL((attn_hyb_kernel<HD, 8, 4, true, 2>), dim3(cdiv(T, 256) * H * B), dim3(512), 0, st, a);
+            hipLaunchKernelGGL((attn_hyb_kernel<HD, 8, 4, true, 1>), dim3(cdiv(T, 256) * H * B), dim3(512), 0, st, a);
         else
             hipLaunchKernelGGL((attn_m32_kernel<HD, 8, 1, true>), dim3(cdiv(T, 256) * H * B), dim3(512), 0, st, a);
     } else if (kind == 12)  // dev: pipelined + lazy + ones
@@ -2523,7 +2526,7 @@ extern "C" int mme_attention(const void* qkv, int ld_qkv, void* out, int ld_out,
     }
 #endif
     if (g_attn_variant >= 9 && g_attn_variant <= 16) kind = g_attn_variant - 9;  // dev: force a kernel
-    if (g_attn_variant >= 30 && g_attn_variant <= 99) kind = g_attn_variant - 30;  // dev: force a kernel
+    if (g_attn_variant >= 30 && g_attn_variant <= 199) kind = g_attn_variant - 30;  // dev: force a kernel
     if ((kind == 16 || kind == 19) && T > 64) kind = 0;  // the short kernels hold one 64-key tile
 #ifdef MME_DEV
     if (g_attn_variant >= 21 && g_attn_variant <= 26 && hd == 72) {  // dev: attn_dma_kernel<72,8,2> diagnostics
