@@ -32,6 +32,7 @@ sys.path.insert(0, os.path.join(ROOT, "multimodal-embedding_amd"))
 
 import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
+from mme.config import EXEC_IMG_BATCH, EXEC_TXT_BATCH  # noqa: E402  (no HIP call: the library loads lazily)
 
 A40_PUBLISHED_IMG_S = 47.1  # SigLIP-400M end-to-end img/s, A40 bf16 bs32
 A40_COLPALI_IMG_S = 2.9     # ColPali-v1.3 img/s (encoder + MaxSim), A40 bf16 bs4 (5k job)
@@ -49,9 +50,10 @@ def parse():
     p.add_argument("--model", default="SigLIP-400M")
     p.add_argument("--n-images", type=int, default=5000)
     p.add_argument("--caps", type=int, default=5)
-    p.add_argument("--img-batch", type=int, default=256)
-    p.add_argument("--txt-batch", type=int, default=2048,
-                   help="captions per text-tower launch (2048 x 64 tokens tiles the N = 1152 / 3456 GEMMs exactly)")
+    p.add_argument("--img-batch", type=int, default=EXEC_IMG_BATCH,
+                   help="images per vision-tower batch before the tail-aware split (mme.config.EXEC_IMG_BATCH)")
+    p.add_argument("--txt-batch", type=int, default=EXEC_TXT_BATCH,
+                   help="captions per text-tower batch before the tail-aware split (mme.config.EXEC_TXT_BATCH)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline sample duration")
     p.add_argument("--no-kernel-timer", action="store_true")
@@ -469,6 +471,8 @@ def main():
             args.n_images = 1000  # BASELINE configs[3]: 1 000 images x 5 000 captions
         if "--img-batch" not in sys.argv:
             args.img_batch = 32
+        if "--txt-batch" not in sys.argv:
+            args.txt_batch = 2048
         return main_colpali(args, rank, world, dev)
 
     from mme import get_spec, ops

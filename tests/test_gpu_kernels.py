@@ -199,10 +199,11 @@ def test_attention_m32_skip(cuda, B, T, H, causal, lens):
 
 
 def test_attention_production_full_grid(cuda):
-    """The production hd-72 kernel over the bench's full launch grid (239 images x 16 heads x
-    3 query blocks of SigLIP vision) against the fp32 reference on the first and last images
-    (grid-to-(batch, head, query block) mapping at production size)."""
-    B, T, H, hd = 239, 729, 16, 72
+    """The production hd-72 kernel over the bench's full launch grid (417 images x 16 heads x
+    3 query blocks of SigLIP vision; 239 before round 3's larger execution batches) against the fp32
+    reference on the first and last images (grid-to-(batch, head, query block) mapping at production
+    size)."""
+    B, T, H, hd = 417, 729, 16, 72
     g = torch.Generator(device="cuda").manual_seed(729)
     qkv = rnd(B * T, 3 * H * hd, scale=1.5, gen=g)
     out = ops.attention(qkv, B, T, H, hd).float().view(B, T, H * hd)
@@ -255,7 +256,8 @@ def test_attention_strided_qkv(cuda):
 
 # (image, all heads) blocks for H * hd <= 1152 (SigLIP MAP head: 16 x 72); per-(image, head)
 # blocks otherwise (H = 5: 256 % H != 0)
-@pytest.mark.parametrize("B,T,H,hd", [(3, 729, 16, 72), (2, 49, 8, 72), (239, 729, 16, 72), (2, 100, 5, 64)])
+@pytest.mark.parametrize("B,T,H,hd", [(3, 729, 16, 72), (2, 49, 8, 72), (239, 729, 16, 72), (417, 729, 16, 72),
+                                     (2, 100, 5, 64)])
 def test_probe_attention(cuda, B, T, H, hd):
     g = torch.Generator(device="cuda").manual_seed(T)
     d = H * hd
