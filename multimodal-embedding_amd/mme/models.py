@@ -30,6 +30,11 @@ LN_FOLD = os.environ.get("MME_LN_FOLD", "1") != "0"
 # the o_proj / fc2 residual GEMMs leave the next LayerNorm's row statistics
 # (mme_gemm_res_stats) instead of a separate mme_rowstats pass over the residual stream
 FUSED_STATS = os.environ.get("MME_FUSED_STATS", "1") != "0"
+# The pooled towers read the last layer's output at one row per item (CLIP image CLS, text EOS /
+# argmax / last token): that layer's o_proj, layer_norm2 and MLP are row-wise, so they run on the
+# pooled rows alone (every row's dead computation skipped; the kept rows' arithmetic unchanged).
+# MME_PRUNE_LAST=0 runs them on every row.
+PRUNE_LAST = os.environ.get("MME_PRUNE_LAST", "1") != "0"
 
 
 class _Bufs:
@@ -50,27 +55,42 @@ class _Bufs:
             if FUSED_STATS and d % 64 == 0 else None
 
 
+def _pooled(a: torch.Tensor, x: torch.Tensor, rows: Optional[torch.Tensor]):
+    """The attention output and residual stream at the pooled rows only (a row gather: data
+    movement), or both unchanged without `rows`."""
+    if rows is None:
+        return a, x
+    return a.index_select(0, rows), x.index_select(0, rows)
+
+
 def encoder_layer(x: torch.Tensor, L: LayerW, cfg: TowerConfig, B: int, T: int, bufs: _Bufs, *,
                   seq_lens: Optional[torch.Tensor] = None, causal: bool = False, stats_in: bool = False,
-                  stats_out: bool = False) -> bool:
+                  stats_out: bool = False, rows: Optional[torch.Tensor] = None) -> Tuple[bool, torch.Tensor]:
     """Pre-LN transformer block, in place on x (SiglipEncoderLayer.forward, TF:…siglip.py:341-357).
 
     LayerNorm-folded path: stats_in = bufs.stats already holds x's row statistics (left by
     the previous layer's fc2); stats_out = leave the statistics of the output x there for
-    the next layer. Returns whether it did (mme_gemm_res_stats on the fc2 residual GEMM)."""
+    the next layer. Returns (whether it did — mme_gemm_res_stats on the fc2 residual GEMM —,
+    the output rows).
+
+    rows (int32 [n], the last layer of a pooled tower): only these rows of the output are
+    read by the pooling head, so after the attention (which every token's K / V feed) the
+    row-wise rest — o_proj + residual, layer_norm2, fc1, fc2 — runs on the gathered rows and
+    the layer returns them as a new [n, d] tensor (x is left as the attention input)."""
     d, H, hd = cfg.hidden, cfg.heads, cfg.head_dim
     act = ACTS[cfg.act]
     if L.mx is not None:  # fp8 mode: QKV / fc1 / fc2 on the block-scaled fp8 MFMA (mme/mx.py)
-        mlp_flops = 2.0 * x.shape[0] * d * cfg.intermediate
         hq = mx.layernorm(x, L.ln1_g, L.ln1_b, cfg.eps, out=bufs.hq)
         qkv = mx.gemm(hq, L.mx.qkv, L.qkv_b, out=bufs.wide[:, : 3 * d])
         a = ops.attention(qkv, B, T, H, hd, seq_lens=seq_lens, causal=causal, out=bufs.h)
+        a, x = _pooled(a, x, rows)
+        n = x.shape[0]
+        mlp_flops = 2.0 * n * d * cfg.intermediate
         ops.gemm(a, L.o_w, L.o_b, residual=x, out=x)
         hq = mx.layernorm(x, L.ln2_g, L.ln2_b, cfg.eps, out=bufs.hq)
         midq = mx.gemm(hq, L.mx.fc1, L.fc1_b, act=act, out_mx=bufs.midq, algo_flops=mlp_flops)
         mx.gemm(midq, L.mx.fc2, L.fc2_b, residual=x, out=x, algo_flops=mlp_flops)
-        return False
-    mlp_flops = 2.0 * x.shape[0] * d * cfg.intermediate  # unpadded intermediate width
+        return False, x
     if LN_FOLD:  # layer_norm1 -> qkv and layer_norm2 -> fc1 folded (mme.h mme_gemm_lnfold)
         if L.fold is None:
             L.fold = (ops.LNFolded(L.qkv_w, L.qkv_b, L.ln1_g, L.ln1_b), ops.LNFolded(L.fc1_w, L.fc1_b, L.ln2_g, L.ln2_b))
@@ -78,26 +98,32 @@ def encoder_layer(x: torch.Tensor, L: LayerW, cfg: TowerConfig, B: int, T: int, 
         st = bufs.stats if (stats_in and fused) else ops.rowstats(x, cfg.eps, d=d, out=bufs.stats)
         qkv = ops.gemm_lnfold(x, L.fold[0], st, out=bufs.wide[:, : 3 * d])
         a = ops.attention(qkv, B, T, H, hd, seq_lens=seq_lens, causal=causal, out=bufs.h)
+        a, x = _pooled(a, x, rows)
+        n = x.shape[0]
+        mlp_flops = 2.0 * n * d * cfg.intermediate  # unpadded intermediate width
         if fused:  # o_proj + residual, with layer_norm2's statistics from the epilogue
             ops.gemm_res_stats(a, L.o_w, L.o_b, x, cfg.eps, bufs.stats, bufs.part, out=x)
             st = bufs.stats
         else:
             ops.gemm(a, L.o_w, L.o_b, residual=x, out=x)
             st = ops.rowstats(x, cfg.eps, d=d, out=bufs.stats)
-        mid = ops.gemm_lnfold(x, L.fold[1], st, act=act, out=bufs.wide[:, : cfg.inter_pad], algo_flops=mlp_flops)
+        mid = ops.gemm_lnfold(x, L.fold[1], st, act=act, out=bufs.wide[:n, : cfg.inter_pad], algo_flops=mlp_flops)
         if fused and stats_out:
             ops.gemm_res_stats(mid, L.fc2_w, L.fc2_b, x, cfg.eps, bufs.stats, bufs.part, out=x, algo_flops=mlp_flops)
-            return True
+            return True, x
         ops.gemm(mid, L.fc2_w, L.fc2_b, residual=x, out=x, algo_flops=mlp_flops)
-        return False
+        return False, x
     h = ops.layernorm(x, L.ln1_g, L.ln1_b, cfg.eps, out=bufs.h)
     qkv = ops.gemm(h, L.qkv_w, L.qkv_b, out=bufs.wide[:, : 3 * d])
     a = ops.attention(qkv, B, T, H, hd, seq_lens=seq_lens, causal=causal, out=bufs.h)
+    a, x = _pooled(a, x, rows)
+    n = x.shape[0]
+    mlp_flops = 2.0 * n * d * cfg.intermediate
     ops.gemm(a, L.o_w, L.o_b, residual=x, out=x)
-    h = ops.layernorm(x, L.ln2_g, L.ln2_b, cfg.eps, out=bufs.h)
-    mid = ops.gemm(h, L.fc1_w, L.fc1_b, act=act, out=bufs.wide[:, : cfg.inter_pad], algo_flops=mlp_flops)
+    h = ops.layernorm(x, L.ln2_g, L.ln2_b, cfg.eps, out=bufs.h[:n])
+    mid = ops.gemm(h, L.fc1_w, L.fc1_b, act=act, out=bufs.wide[:n, : cfg.inter_pad], algo_flops=mlp_flops)
     ops.gemm(mid, L.fc2_w, L.fc2_b, residual=x, out=x, algo_flops=mlp_flops)
-    return False
+    return False, x
 
 
 class VisionTower:
@@ -119,11 +145,12 @@ class VisionTower:
             x = ops.clip_embed_ln(pe, w.cls, w.pos, w.pre_ln_g, w.pre_ln_b, cfg.eps, B, P)
             del pe
         bufs = _Bufs(B * T, cfg, dev, fp8=w.layers[0].mx is not None)
-        run_layers(x, w.layers, cfg, B, T, bufs)
-        if self.spec.family == "siglip":
+        if self.spec.family == "siglip":  # the MAP head attends over every token
+            run_layers(x, w.layers, cfg, B, T, bufs)
             return self._map_head(x, B, T, bufs)
-        rows = torch.arange(B, device=dev, dtype=torch.int32) * T  # CLS rows
-        pooled = ops.layernorm(x, w.post_ln_g, w.post_ln_b, cfg.eps, rows_idx=rows)
+        cls = torch.arange(B, device=dev, dtype=torch.int32) * T  # CLS rows
+        y, rows = run_layers(x, w.layers, cfg, B, T, bufs, pooled_rows=cls)
+        pooled = ops.layernorm(y, w.post_ln_g, w.post_ln_b, cfg.eps, rows_idx=rows)
         return ops.gemm(pooled, w.proj_w)
 
     def forward_tokens(self, patches: torch.Tensor, B: int) -> torch.Tensor:
@@ -160,10 +187,10 @@ class TextTower:
         B, L = ids.shape
         x = ops.token_embed(ids, w.tok, w.pos)
         bufs = _Bufs(B * L, cfg, ids.device, fp8=self.w.layers[0].mx is not None)
-        run_layers(x, w.layers, cfg, B, L, bufs, seq_lens=seq_lens, causal=cfg.causal)
         mode = {"eos": 0, "argmax": 1, "last": 2}[cfg.pool]
-        rows = ops.text_pool_rows(ids, cfg.eos_id, mode)
-        pooled = ops.layernorm(x, w.final_ln_g, w.final_ln_b, cfg.eps, rows_idx=rows)
+        pool = ops.text_pool_rows(ids, cfg.eos_id, mode)
+        y, rows = run_layers(x, w.layers, cfg, B, L, bufs, pooled_rows=pool, seq_lens=seq_lens, causal=cfg.causal)
+        pooled = ops.layernorm(y, w.final_ln_g, w.final_ln_b, cfg.eps, rows_idx=rows)
         return ops.gemm(pooled, w.head_w, w.head_b)
 
 
@@ -197,8 +224,9 @@ def tail_aware_batch(n: int, batch: int, rows_per_item: int, cfg: Optional[Tower
     the `cus` CUs one workgroup each; the last, partial wave of a launch leaves CUs idle.
     Among splits into ceil(n / batch) .. + 3 equal batches this picks the one with the
     least modelled time (sum over launches of waves x K; ties -> fewer batches).
-    SigLIP-400M: 5 000 images -> 21 x 239 (o_proj / fc2 in 12.0 waves) instead of
-    20 x 250 (12.5 -> 13 waves); 25 000 captions -> 14 x 1 786 instead of 13 x 1 924.
+    SigLIP-400M at the 512 / 4 096 defaults (`mme.config.EXEC_*_BATCH`): 5 000 images ->
+    12 x 417, 25 000 captions -> 10 x 2 500; at 256 / 2 048 it picked 21 x 239 (o_proj / fc2
+    in 12.0 waves) instead of 20 x 250 (12.5 -> 13 waves).
     Without `cfg` it is `balanced` (equal batches, no tail model). Items never interact, but the
     batch picks the GEMM kernel (the pipelined one from M·N >= 2^20, the generic one below), so
     the fp32 summation order, and with it the output bits, may change with the batch: results
@@ -271,11 +299,22 @@ def _seq_lens(attention_mask: Optional[torch.Tensor], B: int, L: int, device) ->
     return lens
 
 
-def run_layers(x: torch.Tensor, layers, cfg: TowerConfig, B: int, T: int, bufs: _Bufs, **kw) -> None:
-    """The encoder stack; each layer's fc2 hands the next layer its LayerNorm statistics."""
+def run_layers(x: torch.Tensor, layers, cfg: TowerConfig, B: int, T: int, bufs: _Bufs, *,
+               pooled_rows: Optional[torch.Tensor] = None, **kw) -> Tuple[torch.Tensor, Optional[torch.Tensor]]:
+    """The encoder stack; each layer's fc2 hands the next layer its LayerNorm statistics.
+
+    pooled_rows (int32): the rows the tower's pooling head reads (CLIP CLS, text EOS / argmax /
+    last token). With PRUNE_LAST the last layer's row-wise half runs on those rows alone and
+    this returns ([n, d] pooled output, None); otherwise (x, pooled_rows) — either way the
+    head reads `out[rows]` (rows None = every row in order)."""
     have = False
+    last = len(layers) - 1
     for i, L in enumerate(layers):
-        have = encoder_layer(x, L, cfg, B, T, bufs, stats_in=have, stats_out=i + 1 < len(layers), **kw)
+        rows = pooled_rows if (PRUNE_LAST and i == last) else None
+        have, y = encoder_layer(x, L, cfg, B, T, bufs, stats_in=have, stats_out=i < last, rows=rows, **kw)
+        if rows is not None:
+            return y, None
+    return x, pooled_rows
 
 
 class DualEncoder:

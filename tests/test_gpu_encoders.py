@@ -179,3 +179,35 @@ def test_fused_statistics_at_production_geometry(cuda, monkeypatch):
         print(f"{what}: fused vs separate statistics cos min {c.min().item():.6f}, "
               f"{torch.equal(out[True][k], out[False][k])=}")
         assert c.min() >= 0.9999
+
+
+@pytest.mark.slow
+@pytest.mark.parametrize("name", ["SigLIP-400M", "OpenAI-CLIP-L"])
+def test_pruned_last_layer_at_production_geometry(cuda, monkeypatch, name):
+    """The last encoder layer's row-wise half (o_proj, layer_norm2, MLP) on the pooled rows only
+    (models.PRUNE_LAST: CLIP CLS / EOS rows, SigLIP text last token) against the same layer on
+    every row, at the bench's execution batches: the pooled rows' arithmetic is unchanged, so the
+    embeddings agree bit for bit where both forms run the same GEMM kernel (M·N >= 2^20 on both
+    sides) and within fp32 summation noise where the pruned M drops to the generic kernel."""
+    from mme import models
+    from mme.processor import synthetic_caption_ids, synthetic_images
+    from mme.weights import random_state_dict
+    spec = get_spec(name)
+    cls = SiglipModel if spec.family == "siglip" else CLIPModel
+    model = cls.from_spec(spec, device="cuda", state_dict=random_state_dict(spec, seed=0, device="cuda"))
+    bi, bt = production_batches(spec)
+    monkeypatch.setenv("MME_TAIL_AWARE_BATCH", "0")
+    imgs = torch.from_numpy(synthetic_images(bi, seed=5)).cuda()
+    ids = torch.from_numpy(synthetic_caption_ids(spec, bt, seed=5)).cuda()
+    out = {}
+    for prune in (True, False):
+        monkeypatch.setattr(models, "PRUNE_LAST", prune)
+        out[prune] = (model.encode_images(imgs, batch=bi).cpu(), model.encode_texts(ids, exec_batch=bt).cpu())
+    for k, what in ((0, "images"), (1, "captions")):
+        same = torch.equal(out[True][k], out[False][k])
+        c = row_cos(out[True][k], out[False][k])
+        print(f"{name} {what}: pruned vs full last layer cos min {c.min().item():.7f}, bit-identical {same}")
+        assert same or c.min() >= 0.99999
+    # SigLIP's captions: o_proj / fc1 / fc2 at M = 2 500 run the same pipelined kernel as at 160 000 rows
+    if spec.family == "siglip":
+        assert torch.equal(out[True][1], out[False][1])
