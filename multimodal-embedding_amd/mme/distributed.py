@@ -34,8 +34,14 @@ def all_gather_rows(x: torch.Tensor, world: int, group=None) -> torch.Tensor:
     """Concatenate every rank's [n_r, D] rows in rank order (ragged n_r allowed)."""
     if world == 1:
         return x
+    return _gather_ragged(x, world, group)
+
+
+def _gather_ragged(x: torch.Tensor, world: int, group=None) -> torch.Tensor:
+    """all_gather_rows' collective: exchange the row counts, gather rows padded to the largest,
+    strip the padding (device tensors: one all_gather_into_tensor over RCCL)."""
     if x.is_cuda and dist.get_backend(group) == "gloo":  # gloo gathers host tensors (CPU rehearsal of N > 1)
-        return all_gather_rows(x.cpu(), world, group).to(x.device)
+        return _gather_ragged(x.cpu(), world, group).to(x.device)
     n = torch.tensor([x.shape[0]], dtype=torch.int64, device=x.device)
     sizes = [torch.zeros_like(n) for _ in range(world)]
     dist.all_gather(sizes, n, group=group)
