@@ -149,6 +149,16 @@ int mme_attention(const void* qkv, int ld_qkv, void* out, int ld_out, int B, int
 int mme_probe_attention(const void* q, const void* kv, int ld_kv, void* out, int ld_out, int B, int T, int H,
                         int hd, float scale, void* stream);
 
+/* SigLIP MAP pooling head with the probe query absorbed into the key projection
+ * (round 3): S: fp32 [B*T, ld_s] = x . [U_hi; U_lo]^T, the two bf16 halves of
+ * U_h = W_k,h^T q_h / sqrt(hd) (cols 0..H-1 and H..2H-1); x: bf16 [B*T, ld_x], the
+ * post-LayerNorm tokens. out: bf16 [B*H, ld_out], row b*H + h = sum_t softmax_t(S_h) x_t
+ * over the first D columns; W_v,h (out row) + b_v,h then gives the head's attention output.
+ * T <= 1024, H <= 16, D even <= 1152. Replaces the K / V projections and the attention of
+ * SiglipMultiheadAttentionPoolingHead (TF:models/siglip/modeling_siglip.py:622-644). */
+int mme_map_pool(const float* S, int ld_s, const void* x, int ld_x, void* out, int ld_out, int B, int T, int H,
+                 int D, void* stream);
+
 /* out[b*L + t, :] = tok[ids[b,t]] + pos[t] (bf16). Replaces SiglipTextEmbeddings /
  * CLIPTextEmbeddings (TF:models/siglip/modeling_siglip.py:189-224). */
 int mme_token_embed(const int64_t* ids, int B, int L, const void* tok, const void* pos, int d, void* out,

@@ -2550,6 +2550,111 @@ extern "C" int mme_attention(const void* qkv, int ld_qkv, void* out, int ld_out,
     return mme_check_launch("mme_attention");
 }
 
+namespace {
+// map_pool_kernel: the MAP head's attention with the probe query absorbed into the key
+// projection (round 3). SigLIP's pooling head scores each token t of image b per head h as
+// q_h . (W_k,h x_t + b_k,h) / sqrt(hd) = x_t . U_h + const_h with U_h = W_k,h^T q_h / sqrt(hd),
+// and the constant drops out of the softmax; its output per head is
+// sum_t p_t (W_v,h x_t + b_v,h) = W_v,h (sum_t p_t x_t) + b_v,h (the weights sum to 1). So
+// the K and V projections of all T tokens (a [B*T, 2d] GEMM) become the [B*T, 2H] score GEMM
+// S = x . [U_hi; U_lo]^T (U split into two bf16 halves, so the scores carry ~16 mantissa bits)
+// and, after this kernel, one [B*H, d] GEMM of the pooled rows with W_v.
+// One block per image, thread i = columns 2i, 2i+1: s[t][h] = S[t][h] + S[t][H + h] -> LDS
+// (t-major, so the 16 weights of one token are one broadcast read), softmax per head
+// (exp and normalisation as probe_attn_img_kernel), then out[b*H + h][c] =
+// bf16(sum_t p[t][h] * x[t][c] / sum_t p[t][h]) with fp32 accumulation.
+typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+constexpr int MAPP_MAXT = 1024, MAPP_H = 16, MAPP_NT = 576;  // D <= 2 * 576 = 1152
+__global__ __launch_bounds__(MAPP_NT) void map_pool_kernel(const float* __restrict__ S, int lds,
+                                                           const bf16* __restrict__ x, int ldx,
+                                                           bf16* __restrict__ out, int ldo, int T, int H, int D) {
+    __shared__ __attribute__((aligned(16))) float pt[MAPP_MAXT * MAPP_H];
+    __shared__ float hinv[MAPP_H];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, nw = MAPP_NT / 64;
+    const int b = blockIdx.x;
+    const float* Sb = S + (size_t)b * T * lds;
+    for (int i = tid; i < T * MAPP_H; i += MAPP_NT) {
+        const int t = i / MAPP_H, h = i % MAPP_H;
+        pt[i] = h < H ? Sb[(size_t)t * lds + h] + Sb[(size_t)t * lds + H + h] : 0.f;
+    }
+    __syncthreads();
+    for (int h = wave; h < H; h += nw) {
+        float mx = -INFINITY;
+        for (int t = lane; t < T; t += 64) mx = fmaxf(mx, pt[t * MAPP_H + h]);
+        mx = wave_max(mx);
+        float sum = 0.f;
+        for (int t = lane; t < T; t += 64) {
+            const float p = __expf(pt[t * MAPP_H + h] - mx);
+            pt[t * MAPP_H + h] = p;
+            sum += p;
+        }
+        sum = wave_sum(sum);
+        if (lane == 0) hinv[h] = 1.f / sum;
+    }
+    __syncthreads();
+    const int c = 2 * tid;
+    if (c >= D) return;
+    const bf16* xb = x + (size_t)b * T * ldx + c;
+    float acc[MAPP_H][2];
+#pragma unroll
+    for (int h = 0; h < MAPP_H; ++h) acc[h][0] = acc[h][1] = 0.f;
+    constexpr int U = 8;
+    int t = 0;
+    for (; t + U <= T; t += U) {
+        u16x2 xv[U];
+#pragma unroll
+        for (int j = 0; j < U; ++j) xv[j] = *reinterpret_cast<const u16x2*>(xb + (size_t)(t + j) * ldx);
+#pragma unroll
+        for (int j = 0; j < U; ++j) {
+            const float x0 = bits2f(xv[j][0]), x1 = bits2f(xv[j][1]);
+            const float4* pr = reinterpret_cast<const float4*>(pt + (t + j) * MAPP_H);
+#pragma unroll
+            for (int q = 0; q < MAPP_H / 4; ++q) {
+                const float4 p = pr[q];
+                acc[4 * q][0] += p.x * x0; acc[4 * q][1] += p.x * x1;
+                acc[4 * q + 1][0] += p.y * x0; acc[4 * q + 1][1] += p.y * x1;
+                acc[4 * q + 2][0] += p.z * x0; acc[4 * q + 2][1] += p.z * x1;
+                acc[4 * q + 3][0] += p.w * x0; acc[4 * q + 3][1] += p.w * x1;
+            }
+        }
+    }
+    for (; t < T; ++t) {
+        const u16x2 xv = *reinterpret_cast<const u16x2*>(xb + (size_t)t * ldx);
+        const float x0 = bits2f(xv[0]), x1 = bits2f(xv[1]);
+#pragma unroll
+        for (int h = 0; h < MAPP_H; ++h) {
+            acc[h][0] += pt[t * MAPP_H + h] * x0;
+            acc[h][1] += pt[t * MAPP_H + h] * x1;
+        }
+    }
+#pragma unroll
+    for (int h = 0; h < MAPP_H; ++h) {
+        if (h >= H) break;
+        const float inv = hinv[h];
+        bf16x2 o;
+        o[0] = f2bf(acc[h][0] * inv);
+        o[1] = f2bf(acc[h][1] * inv);
+        *reinterpret_cast<bf16x2*>(out + (size_t)(b * H + h) * ldo + c) = o;
+    }
+}
+}  // namespace
+
+extern "C" int mme_map_pool(const float* S, int ld_s, const void* x, int ld_x, void* out, int ld_out, int B, int T,
+                            int H, int D, void* stream) {
+    MME_REQUIRE(S && x && out, "mme_map_pool: null pointer");
+    MME_REQUIRE(B >= 0 && T > 0 && T <= MAPP_MAXT && H > 0 && H <= MAPP_H, "mme_map_pool: bad shape (T<=%d, H<=%d)",
+                MAPP_MAXT, MAPP_H);
+    MME_REQUIRE(D > 0 && D % 2 == 0 && D <= 2 * MAPP_NT, "mme_map_pool: D=%d must be even and <= %d", D, 2 * MAPP_NT);
+    MME_REQUIRE(ld_s >= 2 * H && ld_x >= D && ld_x % 2 == 0 && ld_out >= D && ld_out % 2 == 0,
+                "mme_map_pool: bad leading dims");
+    MME_REQUIRE(((uintptr_t)x & 3) == 0 && ((uintptr_t)out & 3) == 0, "mme_map_pool: x / out must be 4-byte aligned");
+    if (B == 0) return MME_OK;
+    hipLaunchKernelGGL(map_pool_kernel, dim3(B), dim3(MAPP_NT), 0, as_stream(stream), S, ld_s, (const bf16*)x, ld_x,
+                       (bf16*)out, ld_out, T, H, D);
+    return mme_check_launch("mme_map_pool");
+}
+
 extern "C" int mme_probe_attention(const void* q, const void* kv, int ld_kv, void* out, int ld_out, int B, int T,
                                    int H, int hd, float scale, void* stream) {
     MME_REQUIRE(q && kv && out, "mme_probe_attention: null pointer");

@@ -40,6 +40,7 @@ SIGNATURES = {
     "mme_layernorm": (c_int, [_P, c_int, _P, _P, _P, c_int, c_int, c_int, c_float, _P, _P]),
     "mme_attention": (c_int, [_P, c_int, _P, c_int, c_int, c_int, c_int, c_int, _P, c_int, c_float, _P]),
     "mme_probe_attention": (c_int, [_P, _P, c_int, _P, c_int, c_int, c_int, c_int, c_int, c_float, _P]),
+    "mme_map_pool": (c_int, [_P, c_int, _P, c_int, _P, c_int, c_int, c_int, c_int, c_int, _P]),
     "mme_token_embed": (c_int, [_P, c_int, c_int, _P, _P, c_int, _P, c_int, _P]),
     "mme_clip_embed_ln": (c_int, [_P, c_int, _P, _P, _P, _P, c_float, _P, c_int, c_int, c_int, c_int, _P]),
     "mme_text_pool_rows": (c_int, [_P, c_int, c_int, c_int64, c_int, _P, _P]),

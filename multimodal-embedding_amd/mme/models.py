@@ -35,6 +35,9 @@ FUSED_STATS = os.environ.get("MME_FUSED_STATS", "1") != "0"
 # pooled rows alone (every row's dead computation skipped; the kept rows' arithmetic unchanged).
 # MME_PRUNE_LAST=0 runs them on every row.
 PRUNE_LAST = os.environ.get("MME_PRUNE_LAST", "1") != "0"
+# SigLIP's MAP head with the probe query absorbed into the key projection (mme_map_pool):
+# no [B*T, 2d] K / V projection; MME_MAP_ABSORB=0 runs the K / V GEMM + mme_probe_attention.
+MAP_ABSORB = os.environ.get("MME_MAP_ABSORB", "1") != "0"
 
 
 class _Bufs:
@@ -168,9 +171,18 @@ class VisionTower:
         """post_layernorm + SiglipMultiheadAttentionPoolingHead (TF:…siglip.py:611-644)."""
         cfg, w, hw = self.cfg, self.w, self.w.head
         d = cfg.hidden
+        H, hd = cfg.heads, cfg.head_dim
         h = ops.layernorm(x, w.post_ln_g, w.post_ln_b, cfg.eps, out=bufs.h)
-        kv = ops.gemm(h, hw.kv_w, hw.kv_b, out=bufs.wide[:, : 2 * d])
-        a = ops.probe_attention(hw.q, kv, B, T, cfg.heads, cfg.head_dim)
+        if MAP_ABSORB and hw.u is not None and H <= 16 and T <= 1024 and d <= 1152 and d % 2 == 0:
+            # probe query absorbed into the key projection (attention.hip map_pool_kernel): scores
+            # x . U_h, softmax-weighted token sums per head, then W_v on the B*H pooled rows
+            S = ops.gemm(h, hw.u, out_f32=True, out=bufs.wide.view(torch.float32)[:, : 2 * H])
+            pooled = ops.map_pool(S, h, B, T, H)
+            g = ops.gemm(pooled, hw.v_w, hw.v_b)  # [B*H, d]: row b*H + h holds head h's block
+            a = g.view(B, H, H, hd).diagonal(dim1=1, dim2=2).permute(0, 2, 1).reshape(B, d)
+        else:
+            kv = ops.gemm(h, hw.kv_w, hw.kv_b, out=bufs.wide[:, : 2 * d])
+            a = ops.probe_attention(hw.q, kv, B, T, H, hd)
         y = ops.gemm(a, hw.out_w, hw.out_b)
         z = ops.layernorm(y, hw.ln_g, hw.ln_b, cfg.eps)
         m = ops.gemm(z, hw.fc1_w, hw.fc1_b, act=ACTS[cfg.act])

@@ -297,6 +297,21 @@ def probe_attention(q: torch.Tensor, kv: torch.Tensor, B: int, T: int, H: int, h
     return out
 
 
+def map_pool(S: torch.Tensor, x: torch.Tensor, B: int, T: int, H: int, *,
+             out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """SigLIP MAP head, probe absorbed (mme_map_pool): S fp32 [B*T, >= 2H] (x . [U_hi; U_lo]^T),
+    x bf16 [B*T, D] -> bf16 [B*H, D], row b*H + h = sum_t softmax_t(S[., h] + S[., H + h]) x_t."""
+    _dev(S, x, out)
+    D = x.shape[1]
+    if S.dtype != torch.float32 or S.shape[0] < B * T or x.shape[0] < B * T:
+        raise ValueError(f"map_pool: S {tuple(S.shape)} {S.dtype} / x {tuple(x.shape)} vs B*T = {B * T}")
+    if out is None:
+        out = torch.empty(B * H, D, dtype=BF16, device=x.device)
+    call("mme_map_pool", S.data_ptr(), _rowmajor(S, "S"), x.data_ptr(), _rowmajor(x, "x"), out.data_ptr(),
+         _rowmajor(out, "out"), B, T, H, D, _stream())
+    return out
+
+
 # ---------------------------------------------------------------- Gemma / ColPali pieces
 def rmsnorm(x: torch.Tensor, w: torch.Tensor, eps: float, *, unit_offset: bool = True,
             out: Optional[torch.Tensor] = None) -> torch.Tensor:

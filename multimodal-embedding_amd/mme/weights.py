@@ -57,6 +57,11 @@ class MapHeadW:  # SiglipMultiheadAttentionPoolingHead
     fc1_b: torch.Tensor
     fc2_w: torch.Tensor
     fc2_b: torch.Tensor
+    # the probe query absorbed into the key projection (mme_map_pool): rows 0..H-1 = bf16(U_h),
+    # rows H..2H-1 = bf16(U_h - bf16(U_h)), U_h = W_k,h^T q_h / sqrt(hd) (fp32 at load time)
+    u: Optional[torch.Tensor] = None     # [2H, d]
+    v_w: Optional[torch.Tensor] = None   # [d, d] = W_v (view of kv_w)
+    v_b: Optional[torch.Tensor] = None   # [d]
 
 
 @dataclass
@@ -147,8 +152,14 @@ def from_hf_state_dict(spec: ModelSpec, sd: Dict[str, torch.Tensor], device="cud
         in_w, in_b = b("vision_model.head.attention.in_proj_weight"), b("vision_model.head.attention.in_proj_bias")
         probe = b("vision_model.head.probe").reshape(1, d)
         q = ops.gemm(probe.contiguous(), in_w[:d].contiguous(), in_b[:d].contiguous()).reshape(d)
+        H, hd = v.heads, v.head_dim
+        wk = in_w[d:2 * d].float().reshape(H, hd, d)
+        u = torch.einsum("hj,hjc->hc", q.float().reshape(H, hd), wk) * hd ** -0.5  # [H, d] fp32 (load time)
+        u_hi = u.to(BF16)
+        u2 = torch.cat([u_hi, (u - u_hi.float()).to(BF16)]).contiguous()
+        kv_w, kv_b = in_w[d:].contiguous(), in_b[d:].contiguous()
         head = MapHeadW(
-            q=q, kv_w=in_w[d:].contiguous(), kv_b=in_b[d:].contiguous(),
+            q=q, kv_w=kv_w, kv_b=kv_b, u=u2, v_w=kv_w[d:], v_b=kv_b[d:],
             out_w=b("vision_model.head.attention.out_proj.weight"), out_b=b("vision_model.head.attention.out_proj.bias"),
             ln_g=b("vision_model.head.layernorm.weight"), ln_b=b("vision_model.head.layernorm.bias"),
             fc1_w=_pad_rows(b("vision_model.head.mlp.fc1.weight"), v.inter_pad),

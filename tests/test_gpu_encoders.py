@@ -211,3 +211,26 @@ def test_pruned_last_layer_at_production_geometry(cuda, monkeypatch, name):
     # SigLIP's captions: o_proj / fc1 / fc2 at M = 2 500 run the same pipelined kernel as at 160 000 rows
     if spec.family == "siglip":
         assert torch.equal(out[True][1], out[False][1])
+
+
+@pytest.mark.slow
+def test_map_head_absorbed_at_production_geometry(cuda, monkeypatch):
+    """SigLIP's MAP head with the probe query absorbed into the key projection (models.MAP_ABSORB:
+    score GEMM x . [U_hi; U_lo]^T, mme_map_pool, W_v on the B*H pooled rows) against the K / V
+    projection + mme_probe_attention form, at the bench's execution batch (417 images): the two
+    differ only in where bf16 rounding falls (K / V rows vs the pooled rows)."""
+    from mme import models
+    from mme.processor import synthetic_images
+    from mme.weights import random_state_dict
+    spec = get_spec("SigLIP-400M")
+    model = SiglipModel.from_spec(spec, device="cuda", state_dict=random_state_dict(spec, seed=0, device="cuda"))
+    bi, _ = production_batches(spec)
+    monkeypatch.setenv("MME_TAIL_AWARE_BATCH", "0")
+    imgs = torch.from_numpy(synthetic_images(bi, seed=6)).cuda()
+    out = {}
+    for absorb in (True, False):
+        monkeypatch.setattr(models, "MAP_ABSORB", absorb)
+        out[absorb] = model.encode_images(imgs, batch=bi).cpu()
+    c = row_cos(out[True], out[False])
+    print(f"MAP head absorbed vs K / V projection: cos min {c.min().item():.7f} mean {c.mean().item():.7f}")
+    assert c.min() >= 0.9999

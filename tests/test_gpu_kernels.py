@@ -272,6 +272,26 @@ def test_probe_attention(cuda, B, T, H, hd):
     torch.testing.assert_close(out.float(), ref, atol=2e-2, rtol=2e-2)
 
 
+# SigLIP MAP head with the probe absorbed into the key projection (mme_map_pool): the full
+# head geometry (16 heads, d 1152, T 729) at the production batch, tiny heads, odd T, and the
+# score halves of a real U (hi + lo) against an fp32 torch reference of the same op
+@pytest.mark.parametrize("B,T,H,D", [(3, 729, 16, 1152), (417, 729, 16, 1152), (2, 49, 4, 64), (2, 17, 5, 320)])
+def test_map_pool(cuda, B, T, H, D):
+    g = torch.Generator(device="cuda").manual_seed(T + D)
+    x = rnd(B * T, D, gen=g)
+    u = torch.randn(H, D, generator=g, device="cuda") * D ** -0.5 * 3.0
+    u_hi = u.to(torch.bfloat16)
+    u2 = torch.cat([u_hi, (u - u_hi.float()).to(torch.bfloat16)]).contiguous()
+    S = ops.gemm(x, u2, out_f32=True)
+    out = ops.map_pool(S, x, B, T, H)
+    s_ref = (x.float() @ u.t()).view(B, T, H)                  # fp32 scores with the unsplit U
+    p = torch.softmax(s_ref, dim=1)                            # over tokens
+    ref = torch.einsum("bth,btc->bhc", p, x.float().view(B, T, D)).reshape(B * H, D)
+    torch.testing.assert_close(out.float(), ref, atol=2e-3, rtol=1e-2)
+    # the hi / lo split carries the scores to ~2^-16 relative
+    torch.testing.assert_close((S[:, :H] + S[:, H:2 * H]).view(B, T, H), s_ref, atol=1e-4, rtol=1e-4)
+
+
 @pytest.mark.parametrize("rows,d", [(1, 64), (1000, 1152), (37, 1280), (5, 768), (9, 320)])
 def test_layernorm(cuda, rows, d):
     g = torch.Generator(device="cuda").manual_seed(rows + d)
