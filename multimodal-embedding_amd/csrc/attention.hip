@@ -1126,6 +1126,208 @@ __global__ __launch_bounds__(256, 3) void attn_short_kernel(AttnArgs a, int unit
     }
 }
 
+#ifdef MME_DEV
+// attn_short_pf_kernel (dev, round 3): attn_short_kernel as a persistent loop over unit pairs
+// whose next pair's Q fragments and K / V chunks are loaded into registers while the current
+// pair computes (the short kernel's workgroups each load, then compute, then store, with no
+// loads in flight across those phases). Same per-pair math, so bit-identical to kind 16.
+template <int HD>
+__global__ __launch_bounds__(256, 2) void attn_short_pf_kernel(AttnArgs a, int units, int npairs) {
+    constexpr int HDP = HD == 64 ? 64 : 96;
+    constexpr int NKS = HDP / 32;
+    constexpr int KS = HDP + 8;
+    constexpr int VS = 80;
+    constexpr int NCHL = HD / 8;
+    constexpr int NDT = (HD + 15) / 16;
+    constexpr int NCH = 64 * NCHL;
+    constexpr int NLD = 4 * NCH / 256;  // 16-B K / V chunks per thread and pair
+    static_assert((4 * NCH) % 256 == 0, "K + V tiles of both slots split evenly over 256 threads");
+    __shared__ __attribute__((aligned(16))) bf16 sm[2 * 64 * KS + 2 * 64 * VS];
+    bf16 (*Ks)[64 * KS] = reinterpret_cast<bf16 (*)[64 * KS]>(sm);
+    bf16 (*Vs)[64 * VS] = reinterpret_cast<bf16 (*)[64 * VS]>(sm + 2 * 64 * KS);
+
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int g = lane >> 4, li = lane & 15;
+    const int T = a.T, D = a.H * HD;
+    const int slot = wave >> 1, qw0 = (wave & 1) * 32;
+    const float c = a.scale_log2;
+    // XCD-aware pair order: the block's XCD owns a contiguous range of pairs (neighbouring heads
+    // of one sequence share 128-B lines), walked by the blocks of that XCD in turn
+    const int bid = blockIdx.x, nwg = gridDim.x;
+    const int xcd = bid & 7, loc = bid >> 3, q8 = nwg >> 3, r8 = nwg & 7;
+    const int nblk = xcd < r8 ? q8 + 1 : q8;  // blocks on this XCD
+    const int p8 = npairs >> 3, pr8 = npairs & 7;
+    const int pbeg = xcd < pr8 ? xcd * (p8 + 1) : pr8 * (p8 + 1) + (xcd - pr8) * p8;
+    const int pend = pbeg + (xcd < pr8 ? p8 + 1 : p8);
+
+    if (KS > HD || VS > HD) {  // padding columns: zeroed once, never overwritten by the tiles
+        for (int i = tid; i < 2 * 64; i += 256) {
+            bf16* kr = &Ks[i >> 6][(i & 63) * KS];
+            for (int col = HD; col < KS; col += 8) *reinterpret_cast<u16x8*>(kr + col) = u16x8{0, 0, 0, 0, 0, 0, 0, 0};
+            bf16* vr = &Vs[i >> 6][(i & 63) * VS];
+            for (int col = HD; col < VS; col += 8) *reinterpret_cast<u16x8*>(vr + col) = u16x8{0, 0, 0, 0, 0, 0, 0, 0};
+        }
+    }
+    bf16x8 qf[2][NKS];
+    u16x8 kvn[NLD];
+    auto load_q = [&](int pair) {  // Q fragments of this wave's unit (dead after QK^T: reloaded there)
+        const int uc = min(pair * 2 + slot, units - 1);
+        const int b = uc / a.H, h = uc % a.H;
+        const bf16* base = a.qkv + (long)b * T * a.ld;
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+            const bf16* qrow = base + (long)min(qw0 + u * 16 + li, T - 1) * a.ld + h * HD;
+#pragma unroll
+            for (int ks = 0; ks < NKS; ++ks) {
+                const int col = ks * 32 + 8 * g;
+                qf[u][ks] = col < HD ? *reinterpret_cast<const bf16x8*>(qrow + col) : bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
+            }
+        }
+    };
+    // per-thread chunk offsets within a unit's rows (pair-invariant; slot s of chunk i is
+    // compile-time: NCH * 2 chunks per slot, 256 threads, so i < NLD / 2 is slot 0 when NLD is even)
+    int koff[NLD];
+#pragma unroll
+    for (int i = 0; i < NLD; ++i) {
+        const int ci = tid + i * 256;
+        const int r = ci % (2 * NCH);
+        const bool isV = r >= NCH;
+        const int row = (r % NCH) / NCHL, ch = (r % NCH) % NCHL;
+        koff[i] = min(row, T - 1) * a.ld + (isV ? 2 : 1) * D + ch * 8;
+    }
+    auto load = [&](int pair) {  // K / V chunks of both units into registers
+        const int u0 = min(pair * 2, units - 1), u1 = min(pair * 2 + 1, units - 1);
+        const bf16* b0 = a.qkv + (long)(u0 / a.H) * T * a.ld + (u0 % a.H) * HD;
+        const bf16* b1 = a.qkv + (long)(u1 / a.H) * T * a.ld + (u1 % a.H) * HD;
+#pragma unroll
+        for (int i = 0; i < NLD; ++i) {
+            const int s = (tid + i * 256) / (2 * NCH);
+            kvn[i] = *reinterpret_cast<const u16x8*>((s ? b1 : b0) + koff[i]);
+        }
+    };
+    int pair = pbeg + loc;
+    if (pair < pend) {
+        load_q(pair);
+        load(pair);
+    }
+    for (; pair < pend; pair += nblk) {
+        // the prefetched pair -> LDS / fragments (every wave is past the previous pair's LDS reads)
+#pragma unroll
+        for (int i = 0; i < NLD; ++i) {
+            const int ci = tid + i * 256;
+            const int s = ci / (2 * NCH), r = ci % (2 * NCH);
+            const bool isV = r >= NCH;
+            const int row = (r % NCH) / NCHL, ch = (r % NCH) % NCHL;
+            if (isV)
+                *reinterpret_cast<u16x8*>(&Vs[s][row * VS + ch * 8]) = kvn[i];
+            else
+                *reinterpret_cast<u16x8*>(&Ks[s][row * KS + ch * 8]) = kvn[i];
+        }
+        __syncthreads();
+        const int unit = pair * 2 + slot;
+        const int uc = min(unit, units - 1);
+        const int b = uc / a.H, h = uc % a.H;
+        const int Tk = a.seq_lens ? a.seq_lens[b] : T;
+        if (pair + nblk < pend) load(pair + nblk);  // next pair's loads fly under this pair's math
+
+        const bf16* Kb = Ks[slot];
+        const bf16* Vb = Vs[slot];
+        f32x4 sc[2][4];
+#pragma unroll
+        for (int kt = 0; kt < 4; ++kt) {
+            const bf16* krow = Kb + (kt * 16 + li) * KS;
+            bf16x8 kf[NKS];
+#pragma unroll
+            for (int ks = 0; ks < NKS; ++ks) kf[ks] = *reinterpret_cast<const bf16x8*>(krow + ks * 32 + 8 * g);
+#pragma unroll
+            for (int u = 0; u < 2; ++u) {
+                f32x4 z = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+                for (int ks = 0; ks < NKS; ++ks) z = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf[ks], qf[u][ks], z, 0, 0, 0);
+                sc[u][kt] = z;
+            }
+        }
+        if (pair + nblk < pend) load_q(pair + nblk);
+        if (Tk < 64 || a.causal) {
+#pragma unroll
+            for (int u = 0; u < 2; ++u) {
+                const int q = qw0 + u * 16 + li;
+                const int lim = a.causal ? min(Tk, q + 1) : Tk;
+#pragma unroll
+                for (int kt = 0; kt < 4; ++kt)
+#pragma unroll
+                    for (int r = 0; r < 4; ++r)
+                        if (kt * 16 + 4 * g + r >= lim) sc[u][kt][r] = -INFINITY;
+            }
+        }
+        float lsum[2];
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+            float mloc = -1e30f;
+#pragma unroll
+            for (int kt = 0; kt < 4; ++kt)
+                mloc = fmaxf(mloc, fmaxf(fmaxf(sc[u][kt][0], sc[u][kt][1]), fmaxf(sc[u][kt][2], sc[u][kt][3])));
+            mloc = xmax32(xmax16(mloc));
+            const float mc = mloc * c;
+            float psum = 0.f;
+#pragma unroll
+            for (int kt = 0; kt < 4; ++kt)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const float pv = __builtin_amdgcn_exp2f(sc[u][kt][r] * c - mc);
+                    sc[u][kt][r] = pv;
+                    psum += pv;
+                }
+            lsum[u] = xsum32(xsum16(psum));
+        }
+        f32x4 o[2][NDT];
+#pragma unroll
+        for (int u = 0; u < 2; ++u)
+#pragma unroll
+            for (int i = 0; i < NDT; ++i) o[u][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int hh = 0; hh < 2; ++hh) {
+            bf16x8 pb[2];
+#pragma unroll
+            for (int u = 0; u < 2; ++u)
+                pb[u] = __builtin_convertvector(__builtin_shufflevector(sc[u][2 * hh], sc[u][2 * hh + 1], 0, 1, 2, 3, 4,
+                                                                        5, 6, 7), bf16x8);
+            const int r1 = 32 * hh + 4 * g + (li >> 2);
+#pragma unroll
+            for (int dt = 0; dt < NDT; ++dt) {
+                const int col = dt * 16 + 4 * (li & 3);
+                const s16x4 v0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS_AS s16x4*)(Vb + r1 * VS + col));
+                const s16x4 v1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS_AS s16x4*)(Vb + (r1 + 16) * VS + col));
+                const bf16x8 vv = __builtin_bit_cast(bf16x8, __builtin_shufflevector(v0, v1, 0, 1, 2, 3, 4, 5, 6, 7));
+#pragma unroll
+                for (int u = 0; u < 2; ++u) o[u][dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vv, pb[u], o[u][dt], 0, 0, 0);
+            }
+        }
+        if (unit < units) {
+#pragma unroll
+            for (int u = 0; u < 2; ++u) {
+                const float inv = 1.0f / lsum[u];
+                const int q = qw0 + u * 16 + li;
+                if (q < T) {
+                    bf16* orow = a.out + ((long)b * T + q) * a.ldo + h * HD;
+#pragma unroll
+                    for (int dt = 0; dt < NDT; ++dt) {
+                        const int d0 = dt * 16 + 4 * g;
+                        if (d0 < HD) {
+                            bf16x4 v;
+#pragma unroll
+                            for (int r = 0; r < 4; ++r) v[r] = f2bf(o[u][dt][r] * inv);
+                            *reinterpret_cast<bf16x4*>(orow + d0) = v;
+                        }
+                    }
+                }
+            }
+        }
+        __syncthreads();  // every wave is done reading this pair's K / V before the next overwrite
+    }
+}
+#endif
+
 // ---------------------------------------------------------------------------
 // attn_m32_kernel: the LDS-DMA flash loop on v_mfma_f32_32x32x16_bf16 (round 2).
 // attn_pipe_kernel's counters (profiles/r02_pmc_attn_siglip_vision.json) put the
@@ -2316,6 +2518,10 @@ template <int HD>
 bool launch_attn_dev(int kind, const AttnArgs& a, int B, int T, int H, hipStream_t st) {
     if (kind == 19)  // dev: short kernel, compact K pitch (4 blocks per CU): no gain, HBM-bound (0.138 / 0.136 ms)
         hipLaunchKernelGGL((attn_short_kernel<HD, true>), dim3(cdiv(B * H, 2)), dim3(256), 0, st, a, B * H);
+    else if (kind == 66) {  // dev: short kernel as a persistent loop with the next pair's loads in flight
+        const int npairs = cdiv(B * H, 2);
+        hipLaunchKernelGGL((attn_short_pf_kernel<HD>), dim3(min(npairs, 256 * 2)), dim3(256), 0, st, a, B * H, npairs);
+    }
     else if (kind == 1)
         hipLaunchKernelGGL((attn_dma_kernel<HD, 4, 2>), dim3(cdiv(T, 128) * H * B), dim3(256), 0, st, a);
     else if (kind == 3)
@@ -2527,7 +2733,7 @@ extern "C" int mme_attention(const void* qkv, int ld_qkv, void* out, int ld_out,
 #endif
     if (g_attn_variant >= 9 && g_attn_variant <= 16) kind = g_attn_variant - 9;  // dev: force a kernel
     if (g_attn_variant >= 30 && g_attn_variant <= 199) kind = g_attn_variant - 30;  // dev: force a kernel
-    if ((kind == 16 || kind == 19) && T > 64) kind = 0;  // the short kernels hold one 64-key tile
+    if ((kind == 16 || kind == 19 || kind == 66) && T > 64) kind = 0;  // the short kernels hold one 64-key tile
 #ifdef MME_DEV
     if (g_attn_variant >= 21 && g_attn_variant <= 26 && hd == 72) {  // dev: attn_dma_kernel<72,8,2> diagnostics
         const dim3 grid(cdiv(T, 256) * H * B), blk(512);

@@ -21,6 +21,7 @@ CASES = [  # name, B, T, H, hd, causal
     ("siglip_vision", 256, 729, 16, 72, False),
     ("siglip_text", 1024, 64, 16, 72, False),
     ("siglip_text_pad", 1000, 64, 16, 72, False),
+    ("siglip_text_2500", 2500, 64, 16, 72, False),
     ("clipL_vision", 256, 577, 16, 64, False),
     ("vitH_vision", 256, 257, 16, 80, False),
     ("dfn5b_vision", 128, 730, 16, 80, False),
