@@ -236,8 +236,8 @@ def tail_aware_batch(n: int, batch: int, rows_per_item: int, cfg: Optional[Tower
     the `cus` CUs one workgroup each; the last, partial wave of a launch leaves CUs idle.
     Among splits into ceil(n / batch) .. + 3 equal batches this picks the one with the
     least modelled time (sum over launches of waves x K; ties -> fewer batches).
-    SigLIP-400M at the 512 / 4 096 defaults (`mme.config.EXEC_*_BATCH`): 5 000 images ->
-    12 x 417, 25 000 captions -> 10 x 2 500; at 256 / 2 048 it picked 21 x 239 (o_proj / fc2
+    SigLIP-400M at the round-3 defaults (`mme.config.EXEC_*_BATCH`): 5 000 images ->
+    12 x 417 (cap 512), 25 000 captions -> 5 x 5 000 (cap 8 192); at 256 / 2 048 it picked 21 x 239 (o_proj / fc2
     in 12.0 waves) instead of 20 x 250 (12.5 -> 13 waves).
     Without `cfg` it is `balanced` (equal batches, no tail model). Items never interact, but the
     batch picks the GEMM kernel (the pipelined one from M·N >= 2^20, the generic one below), so

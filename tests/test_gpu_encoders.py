@@ -68,7 +68,7 @@ def test_fast_paths_match_surface(cuda, golden, name):
 
 def production_batches(spec, n_img: int = 5000, caps: int = 5):
     """The execution batches bench.py's 5k x 25k job runs (tail_aware_batch over 256 CUs of
-    mme.config.EXEC_IMG_BATCH / EXEC_TXT_BATCH): SigLIP-400M 417 images / 2 500 captions."""
+    mme.config.EXEC_IMG_BATCH / EXEC_TXT_BATCH): SigLIP-400M 417 images / 5 000 captions."""
     from mme.config import EXEC_IMG_BATCH, EXEC_TXT_BATCH
     from mme.models import tail_aware_batch
     v = spec.vision
@@ -83,7 +83,7 @@ def production_batches(spec, n_img: int = 5000, caps: int = 5):
 def test_full_size_towers_vs_oracle(cuda, monkeypatch, name, n_img, n_cap):
     """Full-size towers (random weights at the exact architecture) vs the fp32 oracle, at two launch
     geometries: the items alone, and the same items at the first / last rows of ONE production
-    execution batch (SigLIP: 417 images = 303 993 GEMM rows, 2 500 captions; the other rows are
+    execution batch (SigLIP: 417 images = 303 993 GEMM rows, 5 000 captions; the other rows are
     other synthetic inputs). Both must reach cos >= 0.999; the production-batch embeddings of
     the oracle items are compared with the small-batch ones (bit-identical or cos >= 0.9999:
     small shapes run the generic GEMM kernel, production shapes the pipelined one, so the fp32
@@ -159,7 +159,7 @@ def test_encode_images_from_host_memory(cuda, golden):
 def test_fused_statistics_at_production_geometry(cuda, monkeypatch):
     """The residual-GEMM LayerNorm statistics (mme_gemm_res_stats: split grid, tail tiles, the stats
     hand-off between layers) against the separate mme_rowstats pass, at the bench's execution batches
-    (SigLIP-400M: 417 images = 303 993 rows, 2 500 captions): same embeddings within fp32 summation
+    (SigLIP-400M: 417 images = 303 993 rows, 5 000 captions): same embeddings within fp32 summation
     noise (the statistics differ only in summation order)."""
     from mme import models
     from mme.processor import synthetic_caption_ids, synthetic_images
@@ -208,7 +208,7 @@ def test_pruned_last_layer_at_production_geometry(cuda, monkeypatch, name):
         c = row_cos(out[True][k], out[False][k])
         print(f"{name} {what}: pruned vs full last layer cos min {c.min().item():.7f}, bit-identical {same}")
         assert same or c.min() >= 0.99999
-    # SigLIP's captions: o_proj / fc1 / fc2 at M = 2 500 run the same pipelined kernel as at 160 000 rows
+    # SigLIP's captions: o_proj / fc1 / fc2 at M = 5 000 run the same pipelined kernel as at 320 000 rows
     if spec.family == "siglip":
         assert torch.equal(out[True][1], out[False][1])
 
