@@ -32,7 +32,7 @@ sys.path.insert(0, os.path.join(ROOT, "multimodal-embedding_amd"))
 
 import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
-from mme.config import EXEC_IMG_BATCH, EXEC_TXT_BATCH  # noqa: E402  (no HIP call: the library loads lazily)
+from mme.config import EXEC_IMG_BATCH, EXEC_TXT_BATCH, exec_batches  # noqa: E402  (no HIP call: the library loads lazily)
 
 A40_PUBLISHED_IMG_S = 47.1  # SigLIP-400M end-to-end img/s, A40 bf16 bs32
 A40_COLPALI_IMG_S = 2.9     # ColPali-v1.3 img/s (encoder + MaxSim), A40 bf16 bs4 (5k job)
@@ -53,7 +53,8 @@ def parse():
     p.add_argument("--img-batch", type=int, default=EXEC_IMG_BATCH,
                    help="images per vision-tower batch before the tail-aware split (mme.config.EXEC_IMG_BATCH)")
     p.add_argument("--txt-batch", type=int, default=EXEC_TXT_BATCH,
-                   help="captions per text-tower batch before the tail-aware split (mme.config.EXEC_TXT_BATCH)")
+                   help="captions per text-tower batch before the tail-aware split (mme.config.exec_batches: "
+                        "EXEC_TXT_BATCH, SigLIP EXEC_TXT_BATCH_SIGLIP)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline sample duration")
     p.add_argument("--no-kernel-timer", action="store_true")
@@ -480,6 +481,8 @@ def main():
     from mme.models import load_model
 
     spec = get_spec(args.model)
+    if "--txt-batch" not in sys.argv:
+        args.txt_batch = exec_batches(spec)[1]
     model, _ = load_model(args.model, seed=0, device=dev, fp8=args.fp8)
     n, caps = args.n_images, args.caps
     imgs, ids = synth_inputs(spec, n, caps, dev)

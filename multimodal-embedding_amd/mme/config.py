@@ -15,13 +15,16 @@ from ._lib import ACT_GELU_ERF, ACT_GELU_TANH, ACT_QUICK_GELU
 OPENAI_CLIP_MEAN = (0.48145466, 0.4578275, 0.40821073)
 OPENAI_CLIP_STD = (0.26862954, 0.26130258, 0.27577711)
 # Execution batches of the dense jobs (images / captions per tower launch sequence; tail_aware_batch
-# then picks equal splits): 512 / 8192 since round 3 -- SigLIP-400M's 5k x 25k job runs 12 x 417
+# then picks equal splits): 512 / 4096 (SigLIP 512 / 8192) since round 3 -- SigLIP-400M's 5k x 25k job runs 12 x 417
 # images and 5 x 5 000 (+ 1 x 5 000 T2I) captions: 512 / 4096 gained +0.5-1.0 % over 256 / 2048
 # (239 / 1 563; fewer launches and fill / drain edges; profiles/r03_v20_batch_sweep.log), 8192
-# captions another -1 % of the text tower's time (profiles/r03_v28_txt_batch_8192.log). bench.py's
-# defaults and the tests' production geometry (tests/test_gpu_encoders.py) read these.
+# captions another -1 % of SigLIP's text tower time (profiles/r03_v28_txt_batch_8192.log) but +1.6 %
+# on LAION-CLIP-H's (level on CLIP-L; profiles/r03_v29_clip_txt_batch_8192.log), so the 8192 cap is
+# SigLIP's only. bench.py's defaults and the tests' production geometry (tests/test_gpu_encoders.py)
+# read exec_batches().
 EXEC_IMG_BATCH = 512
-EXEC_TXT_BATCH = 8192
+EXEC_TXT_BATCH = 4096
+EXEC_TXT_BATCH_SIGLIP = 8192
 
 IMAGENET_STANDARD_MEAN = (0.5, 0.5, 0.5)
 IMAGENET_STANDARD_STD = (0.5, 0.5, 0.5)
@@ -268,3 +271,8 @@ def text_flops(spec: ModelSpec, L: int) -> float:
     f = t.layers * (2.0 * L * d * (3 * d + d + 2 * I) + 4.0 * L * L * d)
     f += 2.0 * d * spec.proj_dim
     return f
+
+
+def exec_batches(spec: "ModelSpec"):
+    """(image, caption) execution-batch caps of a dual-encoder job (see EXEC_IMG_BATCH above)."""
+    return EXEC_IMG_BATCH, EXEC_TXT_BATCH_SIGLIP if spec.family == "siglip" else EXEC_TXT_BATCH

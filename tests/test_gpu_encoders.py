@@ -68,13 +68,14 @@ def test_fast_paths_match_surface(cuda, golden, name):
 
 def production_batches(spec, n_img: int = 5000, caps: int = 5):
     """The execution batches bench.py's 5k x 25k job runs (tail_aware_batch over 256 CUs of
-    mme.config.EXEC_IMG_BATCH / EXEC_TXT_BATCH): SigLIP-400M 417 images / 5 000 captions."""
-    from mme.config import EXEC_IMG_BATCH, EXEC_TXT_BATCH
+    mme.config.exec_batches): SigLIP-400M 417 images / 5 000 captions."""
+    from mme.config import exec_batches
     from mme.models import tail_aware_batch
     v = spec.vision
     T = v.num_patches + (0 if spec.family == "siglip" else 1)
-    return (tail_aware_batch(n_img, EXEC_IMG_BATCH, T, v, 256),
-            tail_aware_batch(caps * n_img, EXEC_TXT_BATCH, spec.text.max_pos, spec.text, 256))
+    ib, tb = exec_batches(spec)
+    return (tail_aware_batch(n_img, ib, T, v, 256),
+            tail_aware_batch(caps * n_img, tb, spec.text.max_pos, spec.text, 256))
 
 
 @pytest.mark.slow
