@@ -167,3 +167,16 @@ def test_tail_aware_batch_siglip_shapes():
     spec = get_spec("SigLIP-400M")
     assert tail_aware_batch(5000, 256, 729, spec.vision) == 239  # o_proj / fc2: 12.0 waves of 256 tiles
     assert tail_aware_batch(25000, 2048, 64, spec.text) == 1563
+
+
+def test_exec_batches_per_family():
+    """bench.py's default execution batches (mme.config.exec_batches): the 8192-caption cap is SigLIP's
+    only (profiles/r03_v28_*, r03_v29_*); the tail-aware split of the 5k x 25k job follows."""
+    from mme.config import REGISTRY, exec_batches
+    from mme.models import tail_aware_batch
+    sig = REGISTRY["SigLIP-400M"]
+    assert exec_batches(sig) == (512, 8192)
+    assert tail_aware_batch(25000, 8192, sig.text.max_pos, sig.text) == 5000
+    assert tail_aware_batch(5000, 512, sig.vision.num_patches, sig.vision) == 417
+    for name in ("OpenAI-CLIP-L", "LAION-CLIP-H", "Apple-DFN5B-H"):
+        assert exec_batches(REGISTRY[name]) == (512, 4096)
