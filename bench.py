@@ -32,7 +32,7 @@ sys.path.insert(0, os.path.join(ROOT, "multimodal-embedding_amd"))
 
 import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
-from mme.config import EXEC_IMG_BATCH, EXEC_TXT_BATCH, exec_batches  # noqa: E402  (no HIP call: the library loads lazily)
+from mme.config import exec_batches  # noqa: E402  (no HIP call: the library loads lazily)
 
 A40_PUBLISHED_IMG_S = 47.1  # SigLIP-400M end-to-end img/s, A40 bf16 bs32
 A40_COLPALI_IMG_S = 2.9     # ColPali-v1.3 img/s (encoder + MaxSim), A40 bf16 bs4 (5k job)
@@ -48,13 +48,14 @@ def parse():
     p.add_argument("--steps", type=int, default=2)
     p.add_argument("--warmup", type=int, default=1)
     p.add_argument("--model", default="SigLIP-400M")
-    p.add_argument("--n-images", type=int, default=5000)
+    p.add_argument("--n-images", type=int, default=None, help="images of the job (default 5 000; ColPali 1 000)")
     p.add_argument("--caps", type=int, default=5)
-    p.add_argument("--img-batch", type=int, default=EXEC_IMG_BATCH,
-                   help="images per vision-tower batch before the tail-aware split (mme.config.EXEC_IMG_BATCH)")
-    p.add_argument("--txt-batch", type=int, default=EXEC_TXT_BATCH,
-                   help="captions per text-tower batch before the tail-aware split (mme.config.exec_batches: "
-                        "EXEC_TXT_BATCH, SigLIP EXEC_TXT_BATCH_SIGLIP)")
+    p.add_argument("--img-batch", type=int, default=None,
+                   help="images per vision-tower batch before the tail-aware split (default mme.config.exec_batches: "
+                        "EXEC_IMG_BATCH; ColPali 32)")
+    p.add_argument("--txt-batch", type=int, default=None,
+                   help="captions per text-tower batch before the tail-aware split (default mme.config.exec_batches: "
+                        "EXEC_TXT_BATCH, SigLIP EXEC_TXT_BATCH_SIGLIP; ColPali 2048)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline sample duration")
     p.add_argument("--no-kernel-timer", action="store_true")
@@ -100,7 +101,7 @@ def cpu_baseline(spec, seconds: float, tables=None, caps_per_image: int = 5):
     batch size 32 (main.py:73,395), timed on the host cores on a bounded sample: whole batches of
     images and captions until the time budget is spent (at least one of each), extrapolated to the
     job's n images + 6n captions; plus the CPU retrieval of the job itself (oracle/retrieval.py:
-    fp32 matmul + ordered top-10 + recall, main.py:471-473,331-378), timed in full on the job's
+    fp32 matmul + top-10 in torch.topk's order + recall, main.py:471-473,331-378), timed in full on the job's
     own embedding tables."""
     from oracle import encoders as oe
     from oracle import retrieval as R
@@ -129,7 +130,7 @@ def cpu_baseline(spec, seconds: float, tables=None, caps_per_image: int = 5):
         n = img.shape[0]
         t0 = time.time()
         for q, d, tc_ in ((t2i, img, 1), (img, allc, caps_per_image), (img, t2i, 1)):
-            R.recall(R.topk(R.scores(q, d), 10)[0], tc_)
+            R.hits(R.scores(q, d), tc_).sum(0)
         ret_s = time.time() - t0
     per_img = 1.0 / img_s + 6.0 / cap_s + (ret_s / n if n else 0.0)
     return {"value": round(1.0 / per_img, 4), "unit": "images/sec", "cores": threads, "kind": "port",
@@ -142,12 +143,13 @@ def cpu_baseline(spec, seconds: float, tables=None, caps_per_image: int = 5):
 
 def retrieval_parity(tables, metrics, caps_per_image: int = 5):
     """R@1 parity of the headline job (checker; runs after the timed region): the job's own
-    embedding tables ranked on the device (mme_sim_topk) vs the oracle (numpy fp32 matmul +
-    ordered top-k, oracle/retrieval.py restating main.py:471-473 and 331-378), row by row;
-    the job's device recall vs the oracle's recall of the same tables."""
+    embedding tables ranked on the device (mme.retrieval.rank_rows: fused sim/top-11, exact-tie rows
+    re-selected in torch.topk's CPU order) vs the oracle (numpy fp32 matmul + torch.topk's order,
+    oracle/retrieval.py restating main.py:471-473 and 331-378), row by row; the job's device recall
+    vs the oracle's recall of the same tables (one selection per k, as compute_metrics_detailed)."""
     sys.path.insert(0, ROOT)
     from oracle import retrieval as R
-    from mme import ops
+    from mme.retrieval import rank_rows
     t0 = time.time()
     host = {k: tables[k].float().cpu().numpy() for k in ("img", "t2i", "all")}
     n = host["img"].shape[0]
@@ -156,17 +158,21 @@ def retrieval_parity(tables, metrics, caps_per_image: int = 5):
     for name, qk, dk, tc in (("T2I", "t2i", "img", 1), ("I2T", "img", "all", caps_per_image),
                              ("I2T_Sym", "img", "t2i", 1)):
         k = min(10, host[dk].shape[0])  # the reference clamps k to the column count (main.py:335)
-        idx, _ = ops.sim_topk(tables[qk].contiguous(), tables[dk].contiguous(), k)
-        ridx, rsc = R.topk(R.scores(host[qk], host[dk]), k + 1)
-        same, near = R.compare_topk(idx.cpu().numpy(), ridx, rsc)
+        ranked = rank_rows(tables[qk], tables[dk], tc)
+        s = R.scores(host[qk], host[dk])
+        ridx, _ = R.topk(s, k)
+        _, rsc = R.topk(s, k + 1)
+        same, near = R.compare_topk(ranked.idx.cpu().numpy(), ridx, rsc)
         rows[name] = {"rows_identical": f"{int(same.sum())}/{len(same)}", "near_tie_rows": int(near.sum()),
-                      "decisive_rows_differing": int((~same & ~near).sum())}
-        for kr, h in zip((1, 5, 10), R.recall(ridx[:, :k], tc, [min(x, k) for x in (1, 5, 10)])):
+                      "decisive_rows_differing": int((~same & ~near).sum()),
+                      "exact_tie_rows_torch_order": int(ranked.tie_rows.numel())}
+        for kr, h in zip((1, 5, 10), R.hits(s, tc).sum(0)):
             ref_metrics[f"{name}_R@{kr}"] = 100.0 * h / n
     return {"recall_identical": all(ref_metrics[k] == metrics[k] for k in ref_metrics),
             "oracle_recall": {k: round(v, 2) for k, v in ref_metrics.items()}, "rows": rows,
-            "near_tie_rule": "neighbouring oracle scores among the top 11 within 1e-5*|s1|",
-            "checker": "oracle/retrieval.py on the job's own embeddings (numpy fp32, host)",
+            "near_tie_rule": "unequal neighbouring oracle scores among the top 11 within 1e-5*|s1|; exact ties "
+                             "are not exempt (torch.topk's order, replayed on both sides)",
+            "checker": "oracle/retrieval.py on the job's own embeddings (numpy fp32 + torch.topk order, host)",
             "seconds": round(time.time() - t0, 2)}
 
 
@@ -468,11 +474,11 @@ def main():
         print(f"bench.py: {e}", file=sys.stderr, flush=True)
         sys.exit(3)
     if args.model.startswith("ColPali"):
-        if args.n_images == 5000 and "--n-images" not in sys.argv:
+        if args.n_images is None:
             args.n_images = 1000  # BASELINE configs[3]: 1 000 images x 5 000 captions
-        if "--img-batch" not in sys.argv:
+        if args.img_batch is None:
             args.img_batch = 32
-        if "--txt-batch" not in sys.argv:
+        if args.txt_batch is None:
             args.txt_batch = 2048
         return main_colpali(args, rank, world, dev)
 
@@ -481,8 +487,11 @@ def main():
     from mme.models import load_model
 
     spec = get_spec(args.model)
-    if "--txt-batch" not in sys.argv:
-        args.txt_batch = exec_batches(spec)[1]
+    if args.n_images is None:
+        args.n_images = 5000  # BASELINE configs[1], [2], [4]: 5 000 images x 25 000 captions
+    eb_img, eb_txt = exec_batches(spec)
+    args.img_batch = eb_img if args.img_batch is None else args.img_batch
+    args.txt_batch = eb_txt if args.txt_batch is None else args.txt_batch
     model, _ = load_model(args.model, seed=0, device=dev, fp8=args.fp8)
     n, caps = args.n_images, args.caps
     imgs, ids = synth_inputs(spec, n, caps, dev)

@@ -35,7 +35,8 @@ extern "C" {
 #define MME_ERR_HIP 2         /* HIP runtime error at launch               */
 #define MME_ERR_UNSUPPORTED 3 /* valid request this build does not handle  */
 
-#define MME_ABI_VERSION 7  /* 6: mme_gemm_res_stats row_part is [M][N / 64][2]; 7: mme_build_flags, mme_topk_rows_torch */
+#define MME_ABI_VERSION 8  /* 6: mme_gemm_res_stats row_part is [M][N / 64][2]; 7: mme_build_flags, mme_topk_rows_torch;
+                              8: mme_recall_hits skip mask, mme_sim_scores, mme_tie_rows */
 
 /* mme_build_flags() bits */
 #define MME_BUILD_DEV 1 /* development / diagnostic kernel forms compiled in (libmme_dev.so) */
@@ -234,11 +235,25 @@ int mme_recall_hits_groups(const int32_t* topk_idx, int rows, int k, int R, int 
 int mme_winoground(const void* text, const void* image, int n, int D, float* scores, int64_t* counts, void* stream);
 
 /* Recall hit counts. For row r the targets are columns
- *   [tgt_start[r], tgt_start[r] + tgt_count)   (tgt_start nullable -> r*tgt_count)
- * hits[j] += #rows whose first kk[j] indices contain a target, j < nk.
+ *   [tgt_start[r], tgt_start[r] + tgt_count)   (tgt_start nullable -> (r + row_offset)*tgt_count)
+ * hits[j] += #rows whose first kk[j] indices contain a target, j < nk; rows with
+ * skip[r] != 0 are not counted (skip nullable; ABI 8: the rows re-ranked in torch's order).
  * Replaces the counting loops of compute_metrics_detailed (main.py:331-378). */
 int mme_recall_hits(const int32_t* topk_idx, int rows, int k, const int32_t* tgt_start, int tgt_count,
-                    int row_offset, const int32_t* kk, int nk, int64_t* hits, void* stream);
+                    int row_offset, const int32_t* kk, int nk, const uint8_t* skip, int64_t* hits, void* stream);
+
+/* Exact score ties on the dense path (ABI 8). torch.topk (main.py:335,365,375) orders EXACTLY
+ * tied values as its libstdc++ selection leaves them, not by column; only rows whose sorted
+ * top-(k+1) holds two equal neighbours can differ from mme_sim_topk's (score desc, column asc)
+ * order (duplicated images / captions tie in every row).
+ *   mme_tie_rows:   flags[r] = 1 iff scores[r][j] == scores[r][j-1] for some 0 < j < k
+ *                   (scores [rows, k] = a sorted mme_sim_topk table).
+ *   mme_sim_scores: out[r][c] = Q[r] . Db[c] fp32 [nq, ldo], through mme_sim_topk's own main
+ *                   loop, so every score is bit-identical to the one it ranked; the flagged rows
+ *                   are re-selected from these by mme_topk_rows_torch, once per k. */
+int mme_tie_rows(const float* scores, int rows, int k, uint8_t* flags, void* stream);
+int mme_sim_scores(const void* Q, int ldq, const void* Db, int ldd, int nq, int nd, int D, float* out, long ldo,
+                   void* stream);
 
 /* ---------------------------------------------------------------- a8 ----
  * ColPali late-interaction MaxSim (colpali_engine processor.score,

@@ -155,11 +155,50 @@ __global__ __launch_bounds__(256) void topk_merge_kernel(const float* __restrict
     }
 }
 
-__global__ void recall_kernel(const int32_t* __restrict__ idx, int rows, int k, const int32_t* __restrict__ tstart,
-                              int tcount, int row_offset, const int32_t* __restrict__ kk, int nk,
-                              unsigned long long* __restrict__ hits) {
+// Full fp32 score rows through sim_topk_kernel's own main loop: the same MFMA sequence per
+// output element, so every score is bit-identical to the one sim_topk ranked. Used for the
+// few rows whose top-(k+1) holds an EXACT tie (duplicated images / captions): torch.topk's
+// order among tied values (main.py:335,365,375) is re-selected from these rows by
+// topk_rows_torch_kernel. 16 lanes store 64 contiguous bytes per row segment.
+__global__ __launch_bounds__(SimCfg::NT) void sim_scores_kernel(const bf16* __restrict__ Q, int ldq, int nq,
+                                                                const bf16* __restrict__ Dm, int ldd, int nd, int D,
+                                                                float* __restrict__ out, long ldo) {
+    __shared__ __attribute__((aligned(16))) char lds[SimCfg::LDS];
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wm = wave / SimCfg::WN, wn = wave % SimCfg::WN;
+    const int m0 = blockIdx.x * SimCfg::BM, n0 = blockIdx.y * SimCfg::BN;
+    f32x4 acc[SimCfg::FM][SimCfg::FN];
+    mainloop<SimCfg>(Q, ldq, nq, m0, Dm, ldd, nd, n0, D, lds, acc, wave, lane);
+#pragma unroll
+    for (int i = 0; i < SimCfg::FM; ++i)
+#pragma unroll
+        for (int j = 0; j < SimCfg::FN; ++j)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int row = m0 + wm * SimCfg::TM + i * 16 + 4 * (lane >> 4) + r;
+                const int col = n0 + wn * SimCfg::TN + j * 16 + (lane & 15);
+                if (row < nq && col < nd) out[(long)row * ldo + col] = acc[i][j][r];
+            }
+}
+
+// flags[r] = 1 when the sorted top-k list of row r holds two EXACTLY equal neighbours: only
+// then can torch.topk's choice among tied columns differ from the (score desc, column asc)
+// order sim_topk produced.
+__global__ void tie_rows_kernel(const float* __restrict__ sc, int rows, int k, uint8_t* __restrict__ flags) {
     const int r = blockIdx.x * blockDim.x + threadIdx.x;
     if (r >= rows) return;
+    const float* s = sc + (long)r * k;
+    bool t = false;
+    for (int j = 1; j < k; ++j) t |= s[j] == s[j - 1];
+    flags[r] = t ? 1 : 0;
+}
+
+__global__ void recall_kernel(const int32_t* __restrict__ idx, int rows, int k, const int32_t* __restrict__ tstart,
+                              int tcount, int row_offset, const int32_t* __restrict__ kk, int nk,
+                              const uint8_t* __restrict__ skip, unsigned long long* __restrict__ hits) {
+    const int r = blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= rows || (skip && skip[r])) return;
     const int lo = tstart ? tstart[r] : (r + row_offset) * tcount;
     const int hi = lo + tcount;
     int first = k;  // first rank holding a target
@@ -600,11 +639,32 @@ extern "C" int mme_winoground(const void* text, const void* image, int n, int D,
 }
 
 extern "C" int mme_recall_hits(const int32_t* topk_idx, int rows, int k, const int32_t* tgt_start, int tgt_count,
-                               int row_offset, const int32_t* kk, int nk, int64_t* hits, void* stream) {
+                               int row_offset, const int32_t* kk, int nk, const uint8_t* skip, int64_t* hits,
+                               void* stream) {
     MME_REQUIRE(topk_idx && kk && hits, "mme_recall_hits: null pointer");
     MME_REQUIRE(rows >= 0 && k >= 1 && tgt_count >= 1 && nk >= 1, "mme_recall_hits: bad args");
     if (rows == 0) return MME_OK;
     hipLaunchKernelGGL(recall_kernel, dim3(cdiv(rows, 256)), dim3(256), 0, as_stream(stream), topk_idx, rows, k,
-                       tgt_start, tgt_count, row_offset, kk, nk, (unsigned long long*)hits);
+                       tgt_start, tgt_count, row_offset, kk, nk, skip, (unsigned long long*)hits);
     return mme_check_launch("mme_recall_hits");
+}
+
+extern "C" int mme_sim_scores(const void* Q, int ldq, const void* Db, int ldd, int nq, int nd, int D, float* out,
+                              long ldo, void* stream) {
+    MME_REQUIRE(Q && Db && out, "mme_sim_scores: null pointer");
+    MME_REQUIRE(nq >= 0 && nd > 0 && D > 0 && D % 64 == 0, "mme_sim_scores: D=%d must be a multiple of 64", D);
+    MME_REQUIRE(ldq % 8 == 0 && ldd % 8 == 0 && ldq >= D && ldd >= D && ldo >= nd, "mme_sim_scores: bad leading dims");
+    MME_REQUIRE(cdiv(nd, SimCfg::BN) <= 65535, "mme_sim_scores: nd=%d too large", nd);
+    if (nq == 0) return MME_OK;
+    hipLaunchKernelGGL(sim_scores_kernel, dim3(cdiv(nq, SimCfg::BM), cdiv(nd, SimCfg::BN)), dim3(SimCfg::NT), 0,
+                       as_stream(stream), (const bf16*)Q, ldq, nq, (const bf16*)Db, ldd, nd, D, out, ldo);
+    return mme_check_launch("mme_sim_scores");
+}
+
+extern "C" int mme_tie_rows(const float* scores, int rows, int k, uint8_t* flags, void* stream) {
+    MME_REQUIRE(scores && flags, "mme_tie_rows: null pointer");
+    MME_REQUIRE(rows >= 0 && k >= 1, "mme_tie_rows: bad args");
+    if (rows == 0) return MME_OK;
+    hipLaunchKernelGGL(tie_rows_kernel, dim3(cdiv(rows, 256)), dim3(256), 0, as_stream(stream), scores, rows, k, flags);
+    return mme_check_launch("mme_tie_rows");
 }

@@ -18,7 +18,7 @@ LIB_PATH = os.environ.get("MME_LIB", os.path.join(_HERE, "libmme_dev.so" if DEV 
 # MME_ACT_* / MME_PIX_* from include/mme.h
 ACT_NONE, ACT_GELU_TANH, ACT_QUICK_GELU, ACT_GELU_ERF, ACT_GEGLU_TANH = 0, 1, 2, 3, 4
 PIX_F32_NCHW, PIX_PATCHES = 0, 1
-ABI_VERSION = 7
+ABI_VERSION = 8
 BUILD_DEV = 1  # MME_BUILD_DEV
 
 # name -> (restype, argtypes)
@@ -54,7 +54,9 @@ SIGNATURES = {
     "mme_topk_rows": (c_int, [_P, c_int, c_int, c_int, c_int, c_int, _P, _P, _P]),
     "mme_topk_rows_torch_workspace_bytes": (c_size_t, [c_int, c_int, c_int]),
     "mme_topk_rows_torch": (c_int, [_P, c_int, c_int, c_int, c_int, c_int, _P, _P, _P, c_size_t, _P]),
-    "mme_recall_hits":(c_int, [_P, c_int, c_int, _P, c_int, c_int, _P, c_int, _P, _P]),
+    "mme_recall_hits": (c_int, [_P, c_int, c_int, _P, c_int, c_int, _P, c_int, _P, _P, _P]),
+    "mme_tie_rows": (c_int, [_P, c_int, c_int, _P, _P]),
+    "mme_sim_scores": (c_int, [_P, c_int, _P, c_int, c_int, c_int, c_int, _P, ctypes.c_long, _P]),
     "mme_maxsim_workspace_bytes": (c_size_t, [c_int, c_int, c_int]),
     "mme_maxsim": (c_int, [_P, _P, c_int, c_int, _P, _P, _P, c_int, c_int, c_int, _P, _P, c_size_t, _P]),
     "mme_mx_quant": (c_int, [_P, c_int, c_int, c_int, _P, c_int, _P, c_int, _P]),

@@ -48,6 +48,12 @@ def sample_indices(n: int, iterations: int, seed: Optional[int] = 0, device="cud
     return torch.from_numpy(rng.integers(0, n, (iterations, n)).astype(np.int32)).to(device)
 
 
+def ops_ws_bytes(rows: int, cols: int, k: int) -> int:
+    """mme_topk_rows_torch's workspace for one resample's [rows, cols] matrix (rows·cols·8 B when
+    torch's nth_element branch, k·64 > cols, runs; else 0)."""
+    return 8 * rows * cols if k * 64 > cols else 0
+
+
 @torch.no_grad()
 def bootstrap_hits(s_t2i: torch.Tensor, s_i2t: torch.Tensor, samples: torch.Tensor, caps_per_image: int = 5,
                    ks: Sequence[int] = KS, batch: Optional[int] = None) -> torch.Tensor:
@@ -56,8 +62,9 @@ def bootstrap_hits(s_t2i: torch.Tensor, s_i2t: torch.Tensor, samples: torch.Tens
     if s_t2i.shape != (n, n) or s_i2t.shape != (n, caps_per_image * n):
         raise ValueError("bootstrap_hits: expected T2I [n, n] and I2T [n, caps*n] score matrices")
     s_sym = s_t2i.t().contiguous()
-    if batch is None:  # ~2 GiB of gathered scores per batch
-        batch = max(1, min(iters, (2 << 30) // max(1, 4 * n * n * (2 + caps_per_image))))
+    if batch is None:  # ~2 GiB per batch: one gathered matrix at a time + its torch-order selection workspace
+        per = max(4 * n * c + ops_ws_bytes(n, c, min(max(ks), c)) for c in (n, caps_per_image * n))
+        batch = max(1, min(iters, (2 << 30) // max(1, per)))
     out = torch.empty(iters, 3 * len(ks), dtype=torch.int64, device=samples.device)
     for b0 in range(0, iters, batch):
         smp = samples[b0:b0 + batch].contiguous()

@@ -71,15 +71,14 @@ def all_reduce_(t: torch.Tensor, op=dist.ReduceOp.SUM, group=None) -> torch.Tens
 
 
 class DeviceOps:
-    """Default compute: libmme fused sim/top-k + recall counters."""
+    """Default compute: libmme fused sim/top-k + recall counters, in torch.topk's order on exact ties
+    (mme.retrieval.rank_rows)."""
 
-    def topk(self, q: torch.Tensor, d: torch.Tensor, k: int) -> torch.Tensor:
-        from . import ops
-        return ops.sim_topk(q.contiguous(), d.contiguous(), k)[0]
-
-    def hits(self, idx: torch.Tensor, tgt_count: int, ks: Sequence[int], row_offset: int) -> torch.Tensor:
-        from . import ops
-        return ops.recall_hits(idx, tgt_count, ks, row_offset=row_offset)
+    def rank(self, q: torch.Tensor, d: torch.Tensor, tgt_count: int, ks: Sequence[int], row_offset: int):
+        """(hit counts int64 [len(ks)], top-max(ks) index table in torch.topk's order)."""
+        from .retrieval import rank_rows
+        r = rank_rows(q, d, tgt_count, ks, row_offset)
+        return r.hits, r.idx
 
 
 def rank_hit_counts(img_l: torch.Tensor, t2i_l: torch.Tensor, img_all: torch.Tensor, t2i_all: torch.Tensor,
@@ -89,18 +88,15 @@ def rank_hit_counts(img_l: torch.Tensor, t2i_l: torch.Tensor, img_all: torch.Ten
 
     T2I: the rank's caption-0 queries vs all images; I2T: its images vs all captions;
     I2T-Sym: its images vs all T2I captions. ``row_offset`` = the rank's first global
-    image (targets are global indices). Returns int64 [3·len(ks)] (and the top-k
-    index tables when ``return_idx``)."""
+    image (targets are global indices). ``compute.rank(q, d, tgt_count, ks, row_offset)``
+    returns (hit counts, top-k table) with compute_metrics_detailed's per-k torch.topk
+    semantics. Returns int64 [3·len(ks)] (and the top-k index tables when ``return_idx``)."""
     compute = compute or DeviceOps()
-    kmax = max(ks)
     res, idxs = [], {}
     for name, q, d, tcount in (("T2I", t2i_l, img_all, 1), ("I2T", img_l, all_all, caps_per_image),
                                ("I2T_Sym", img_l, t2i_all, 1)):
-        k = min(kmax, d.shape[0])
-        kk = [min(x, k) for x in ks]
         if q.shape[0]:
-            idx = compute.topk(q, d, k)
-            h = compute.hits(idx, tcount, kk, row_offset)
+            h, idx = compute.rank(q, d, tcount, ks, row_offset)
             idxs[name] = idx
         else:
             h = torch.zeros(len(ks), dtype=torch.int64, device=q.device)

@@ -26,8 +26,13 @@ METRIC_KEYS = [f"{p}_R@{k}" for p in ("T2I", "I2T", "I2T_Sym") for k in KS]
 
 
 def encode_job(model, images_u8: torch.Tensor, caption_ids: torch.Tensor, caption_lens: Optional[torch.Tensor] = None,
-               caps_per_image: int = 5, img_batch: int = 256, txt_batch: int = 2048):
-    """Encode n images, their caption-0 T2I queries and all 5n captions (main.py:551-557)."""
+               caps_per_image: int = 5, img_batch: Optional[int] = None, txt_batch: Optional[int] = None):
+    """Encode n images, their caption-0 T2I queries and all 5n captions (main.py:551-557). Execution
+    batches default to the measured geometry bench.py runs (mme.config.exec_batches)."""
+    from .config import exec_batches
+    eb_img, eb_txt = exec_batches(model.spec)
+    img_batch = eb_img if img_batch is None else img_batch
+    txt_batch = eb_txt if txt_batch is None else txt_batch
     n = images_u8.shape[0]
     img = model.encode_images(images_u8, batch=img_batch)
     sel = torch.arange(0, caps_per_image * n, caps_per_image, device=caption_ids.device)

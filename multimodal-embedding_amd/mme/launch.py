@@ -101,8 +101,11 @@ def spawn_ranks(nprocs: int, argv: Sequence[str], poll_s: float = 0.2, timeout_s
     except _Signalled as e:
         return 128 + int(e.signum)
     finally:
-        for sig, h in old.items():
-            signal.signal(sig, h)
+        # a second signal during cleanup (a scheduler re-sending SIGTERM) must not kill this parent
+        # before every rank is terminated and reaped: ignore them until then, restore the old
+        # handlers last
+        for sig in old:
+            signal.signal(sig, signal.SIG_IGN)
         for p in procs:
             if p.poll() is None:
                 p.terminate()
@@ -112,6 +115,8 @@ def spawn_ranks(nprocs: int, argv: Sequence[str], poll_s: float = 0.2, timeout_s
             except subprocess.TimeoutExpired:
                 p.kill()
                 p.wait()
+        for sig, h in old.items():
+            signal.signal(sig, h)
 
 
 def env_rank_world() -> Tuple[int, int, int]:

@@ -242,7 +242,14 @@ def tail_aware_batch(n: int, batch: int, rows_per_item: int, cfg: Optional[Tower
     Without `cfg` it is `balanced` (equal batches, no tail model). Items never interact, but the
     batch picks the GEMM kernel (the pipelined one from M·N >= 2^20, the generic one below), so
     the fp32 summation order, and with it the output bits, may change with the batch: results
-    agree within tolerance (cos >= 0.9999, tests/test_gpu_encoders.py), not bit for bit."""
+    agree within tolerance (cos >= 0.9999, tests/test_gpu_encoders.py), not bit for bit.
+    With `cfg`, a batch is also capped so that the widest GEMM operand (the [rows, max(3d, I_pad)]
+    activation buffer, fc2's A) stays below 4 GiB: the pipelined GEMMs address operands with 32-bit
+    offsets and would otherwise fall back to the slower generic kernel (SigLIP text, L = 64:
+    7 710 captions)."""
+    if cfg is not None:
+        widest = rows_per_item * max(3 * cfg.hidden, cfg.inter_pad) * 2
+        batch = max(1, min(batch, ((1 << 32) - 1) // widest))
     if cfg is None or n <= 0 or os.environ.get("MME_TAIL_AWARE_BATCH", "1") == "0":
         return balanced(n, batch)
     d, ff = cfg.hidden, cfg.inter_pad

@@ -587,16 +587,55 @@ def winoground(text: torch.Tensor, image: torch.Tensor):
 
 
 def recall_hits(topk_idx: torch.Tensor, tgt_count: int, ks: Sequence[int], *, tgt_start: Optional[torch.Tensor] = None,
-                row_offset: int = 0, hits: Optional[torch.Tensor] = None) -> torch.Tensor:
-    """int64 [len(ks)] counts of rows whose first ks[j] indices contain a target column."""
-    _dev(topk_idx, tgt_start, hits)
+                row_offset: int = 0, hits: Optional[torch.Tensor] = None,
+                skip: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """int64 [len(ks)] counts of rows whose first ks[j] indices contain a target column (rows with
+    skip[r] != 0 not counted)."""
+    _dev(topk_idx, tgt_start, hits, skip)
     rows, k = topk_idx.shape
+    if tgt_start is not None and (tgt_start.dtype != torch.int32 or tgt_start.numel() != rows):
+        raise ValueError("recall_hits: tgt_start must be int32 [rows]")
+    if skip is not None and (skip.dtype != torch.uint8 or skip.numel() != rows):
+        raise ValueError("recall_hits: skip must be uint8 [rows]")
     kk = torch.tensor(list(ks), dtype=torch.int32, device=topk_idx.device)
     if hits is None:
         hits = torch.zeros(len(ks), dtype=torch.int64, device=topk_idx.device)
     call("mme_recall_hits", topk_idx.contiguous().data_ptr(), rows, k, _ptr(tgt_start), tgt_count, row_offset,
-         kk.data_ptr(), len(ks), hits.data_ptr(), _stream())
+         kk.data_ptr(), len(ks), _ptr(skip), hits.data_ptr(), _stream())
     return hits
+
+
+def tie_rows(scores: torch.Tensor) -> torch.Tensor:
+    """uint8 [rows]: 1 where a sorted top-k score row holds two exactly equal neighbours."""
+    _dev(scores)
+    if scores.dtype != torch.float32 or not scores.is_contiguous():
+        raise ValueError("tie_rows: scores must be contiguous fp32 [rows, k]")
+    rows, k = scores.shape
+    flags = torch.empty(rows, dtype=torch.uint8, device=scores.device)
+    call("mme_tie_rows", scores.data_ptr(), rows, k, flags.data_ptr(), _stream())
+    return flags
+
+
+def sim_scores(q: torch.Tensor, d: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """fp32 [nq, nd] = q @ d.T through mme_sim_topk's own main loop (scores bit-identical to the ones
+    sim_topk ranks)."""
+    _dev(q, d, out)
+    nq, D = q.shape
+    nd = d.shape[0]
+    if d.shape[1] != D:
+        raise ValueError("sim_scores: width mismatch")
+    if D % 64:
+        Dp = -(-D // 64) * 64
+        q = torch.nn.functional.pad(q, (0, Dp - D))
+        d = torch.nn.functional.pad(d, (0, Dp - D))
+        D = Dp
+    if out is None:
+        out = torch.empty(nq, nd, dtype=torch.float32, device=q.device)
+    if out.dtype != torch.float32 or tuple(out.shape) != (nq, nd):
+        raise ValueError("sim_scores: out must be fp32 [nq, nd]")
+    call("mme_sim_scores", q.data_ptr(), _rowmajor(q, "q"), d.data_ptr(), _rowmajor(d, "d"), nq, nd, D,
+         out.data_ptr(), _rowmajor(out, "out"), _stream())
+    return out
 
 
 def maxsim(Q: torch.Tensor, q_lens: torch.Tensor, D: torch.Tensor, d_lens: torch.Tensor,

@@ -342,6 +342,72 @@ def make_full_retrieval(main):
     print("full_retrieval.npz:", dict(zip(keys, out["metric_values"].round(2))))
 
 
+DENSE_TIE_CASES = (  # (tag, n images, D, noise, seed): both sides of torch.topk's k * 64 <= n switch
+    ("wide", 1000, 256, 1.3, 31),    # T2I / Sym 1 000 columns: partial_sort at k = 1, 5, 10
+    ("narrow", 300, 256, 1.3, 32),   # 300 columns: partial_sort at k = 1, nth_element at k = 5, 10
+    ("tiny", 40, 128, 1.0, 33),      # 40 columns: nth_element at every k; I2T 200: partial_sort at k = 1
+)
+
+
+def make_dense_ties(main):
+    """Exact fp32 score ties on the dense path: planted embeddings with exact
+    duplicates (tests/golden/planted.py planted_ties: repeated images, caption rows repeated across
+    images of one base), scored by the reference's own compute_similarity_scores and ranked by its
+    compute_metrics_detailed (main.py:305-383, 440-475; v28 I2T orientation). Stored per case: seed /
+    checksums, the duplicate groups, per row the reference's torch.topk(row, 10) indices, top-11 scores
+    and the hit flags of compute_metrics_detailed's own per-k calls, and the 9 metrics. The GPU test
+    regenerates the embeddings and checks the checksums first."""
+    from planted import bf16_sha, planted_ties
+    out, caps = {}, 5
+    for tag, n, D, noise, seed in DENSE_TIE_CASES:
+        img, all_txt, groups = planted_ties(n, caps, D, noise, seed)
+        t2i = all_txt[::caps].contiguous()
+        m_info = {"type": "dense"}
+        main.DEVICE = "cpu"
+        s_t2i = main.compute_similarity_scores(img, t2i, m_info, None)           # [n, n]  = t2i @ img.T
+        s_i2t = main.compute_similarity_scores(all_txt, img, m_info, None)       # [n, 5n] = img @ all.T (v28)
+        s_sym = s_t2i.t().contiguous()
+        metrics = main.compute_metrics_detailed(s_t2i, s_i2t, s_sym, list(range(n)),
+                                                {i: list(range(caps * i, caps * i + caps)) for i in range(n)},
+                                                {i: i for i in range(n)}, [""] * n)
+        hits = np.zeros((3, n, 3), bool)
+        tied = np.zeros((3, n), bool)
+        for p, (ptag, s, tgt) in enumerate((("t2i", s_t2i, lambda i: [i]),
+                                            ("i2t", s_i2t, lambda i: range(caps * i, caps * i + caps)),
+                                            ("sym", s_sym, lambda i: [i]))):
+            for i in range(n):
+                for j, k in enumerate((1, 5, 10)):
+                    top = torch.topk(s[i], k=min(k, s.shape[1])).indices.tolist()
+                    hits[p, i, j] = any(c in top for c in tgt(i))
+            kk = min(11, s.shape[1])
+            v11, _ = torch.topk(s, kk, dim=1)
+            k10 = min(10, s.shape[1])
+            ix10 = torch.stack([torch.topk(s[i], k10).indices for i in range(n)])
+            tied[p] = (v11[:, 1:] == v11[:, :-1]).any(1).numpy()
+            cols = np.broadcast_to(np.arange(s.shape[1]), s.shape)
+            lex = np.lexsort((cols, -s.numpy()), axis=1)[:, :k10]
+            out[f"{tag}_{ptag}_idx"] = ix10.numpy().astype(np.int32)
+            out[f"{tag}_{ptag}_score"] = v11.numpy().astype(np.float32)
+            print(f"dense_ties {tag} {ptag}: {int(tied[p].sum())}/{n} rows with an exact tie in the top {kk}; "
+                  f"torch order != (score desc, column asc) on {int((lex != ix10.numpy()).any(1).sum())} rows")
+        keys = [k for k in metrics if not k.startswith("_")]
+        vals = np.array([metrics[k] for k in keys], np.float64)
+        assert np.allclose(vals.reshape(3, 3), 100.0 * hits.sum(1) / n)
+        # the duplicated columns score exactly equal in the reference's own fp32 matmul
+        for mode, size, *mem in groups.tolist():
+            mem = mem[:size]
+            if mode in (0, 3):
+                assert (s_t2i[:, mem] == s_t2i[:, mem[:1]]).all()
+        out.update({f"{tag}_params": np.array([n, caps, D, seed], np.int64), f"{tag}_noise": np.float64(noise),
+                    f"{tag}_img_sha": np.array(bf16_sha(img)), f"{tag}_txt_sha": np.array(bf16_sha(all_txt)),
+                    f"{tag}_groups": groups, f"{tag}_hits": hits, f"{tag}_tied": tied,
+                    f"{tag}_metric_values": vals})
+        out["metric_names"] = np.array(keys)
+        print(f"dense_ties {tag}:", dict(zip(keys, vals.round(2))))
+    out["cases"] = np.array([c[0] for c in DENSE_TIE_CASES])
+    np.savez_compressed(os.path.join(HERE, "dense_ties.npz"), **out)
+
+
 # ------------------------------------------------------------------ maxsim + l2norm
 def make_maxsim(main):
     from transformers.models.colpali.processing_colpali import ColPaliProcessor
@@ -772,7 +838,8 @@ if __name__ == "__main__":
              "encoders": lambda: make_encoders(main), "colpali": lambda: make_colpali(main),
              "config0": lambda: make_config0(main), "edge": lambda: make_edge(main),
              "winoground": make_winoground, "bootstrap": lambda: make_bootstrap(main),
-             "colpali_full": lambda: make_colpali_full(main), "torch_topk": make_torch_topk}
+             "colpali_full": lambda: make_colpali_full(main), "torch_topk": make_torch_topk,
+             "dense_ties": lambda: make_dense_ties(main)}
     for name, fn in steps.items():
         if not only or name in only:
             fn()

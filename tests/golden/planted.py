@@ -29,6 +29,48 @@ def planted_np(n: int, caps: int, D: int, noise: float, seed: int = 0):
     return _unit_bf16(img), _unit_bf16(cap)
 
 
+def planted_ties(n: int, caps: int, D: int, noise: float, seed: int = 0):
+    """planted_np with EXACT duplicates, so exact fp32 score ties decide top-k places.
+
+    Disjoint groups of 2, 3 or 4 images share one base (each member's captions describe the
+    others too, so the tied columns rank high). Per group, by mode (cycled):
+      0 'img'  every member's image is the lead's image (T2I rows tie member images);
+      1 'cap0' every member's caption 0 is the lead's caption 0 (Sym rows tie T2I captions,
+               I2T rows tie captions 5m);
+      2 'capj' caption j = 1 + (group % 4) duplicated (I2T only);
+      3 'both' images and caption 0.
+    About 35 % of the images belong to a group. Returns (img [n, D] bf16, all_txt [caps·n, D]
+    bf16, groups int32 [n_groups, 6] = (mode, size, lead, member, member, member; -1 padded))."""
+    rng = np.random.default_rng(seed)
+    base = rng.standard_normal((n, D), dtype=np.float32)
+    perm = rng.permutation(n)
+    groups, pos = [], 0
+    for size, count in ((2, int(0.10 * n)), (3, int(0.03 * n)), (4, int(0.015 * n))):
+        for _ in range(count):
+            if pos + size > n:
+                break
+            groups.append(perm[pos:pos + size].copy())
+            pos += size
+    for m in groups:
+        base[m] = base[m[0]]
+    img = base + np.float32(noise) * rng.standard_normal((n, D), dtype=np.float32)
+    cap = np.repeat(base, caps, 0) + np.float32(noise) * rng.standard_normal((n * caps, D), dtype=np.float32)
+    table = np.full((len(groups), 6), -1, np.int32)
+    for g, m in enumerate(groups):
+        mode = g % 4
+        lead = m[0]
+        if mode in (0, 3):
+            img[m] = img[lead]
+        if mode in (1, 3):
+            cap[caps * m] = cap[caps * lead]
+        if mode == 2:
+            j = 1 + (g // 4) % (caps - 1)
+            cap[caps * m + j] = cap[caps * lead + j]
+        table[g, 0], table[g, 1] = mode, len(m)
+        table[g, 2:2 + len(m)] = m
+    return _unit_bf16(img), _unit_bf16(cap), table
+
+
 def planted_multivec(n: int, caps: int, Ld: int, qlens: tuple, noise: float, batch: int = 4, seed: int = 0):
     """ColPali-shaped planted multi-vectors (SURVEY §8d config 4 geometry, scaled down in n).
 

@@ -1,5 +1,5 @@
-"""Edge cases of the hot path on the MI355X against the reference (tests/golden/edge.npz):
-fewer candidates than k, ragged / tiny job sizes, empty inputs, exact score ties."""
+"""Edge cases of the hot path on the MI355X against the reference (tests/golden/edge.npz,
+dense_ties.npz): fewer candidates than k, ragged / tiny job sizes, empty inputs, exact score ties."""
 import numpy as np
 import pytest
 import torch
@@ -41,21 +41,76 @@ def test_empty_inputs_match_reference(cuda, golden):
     assert model.encode_texts(torch.zeros(0, 16, dtype=torch.int64, device="cuda")).shape == (0, spec.proj_dim)
 
 
-def test_exact_ties_break_by_lowest_column(cuda):
-    """Duplicated documents give exactly equal scores; the device order is (score desc, column asc),
-    the rule oracle/retrieval.py states (torch.topk's CPU order on exact ties is implementation
-    defined), for the fused sim/top-k and the row top-k of a score matrix alike."""
+def test_exact_ties_kernel_order_and_torch_order(cuda):
+    """Duplicated documents give exactly equal scores. The fused kernels' own table is ordered (score
+    desc, column asc) (mme_sim_topk, mme_topk_rows); the ranking the job uses (retrieval.rank_rows)
+    flags exactly tied rows and re-selects them in torch.topk's CPU order, which must equal the
+    oracle's torch-order selection (oracle/torch_topk.cpp, pinned to torch.topk itself)."""
     from oracle import retrieval as R
     g = torch.Generator().manual_seed(3)
     base = torch.nn.functional.normalize(torch.randn(40, 128, generator=g), dim=-1).to(torch.bfloat16)
     docs = base.repeat(3, 1)[torch.randperm(120, generator=g)]      # every document three times
     q = torch.nn.functional.normalize(torch.randn(25, 128, generator=g), dim=-1).to(torch.bfloat16)
+    s = R.scores(q.float().numpy(), docs.float().numpy())
     idx, sc = ops.sim_topk(q.cuda(), docs.cuda(), 10)
-    ridx, rsc = R.topk(R.scores(q.float().numpy(), docs.float().numpy()), 10)
-    assert np.array_equal(idx.cpu().numpy(), ridx)
-    s = (q.float() @ docs.float().T).cuda()
-    idx2, _ = ops.topk_rows(s.contiguous(), 10)
-    assert np.array_equal(idx2.cpu().numpy(), ridx)
+    lidx, _ = R._lex_topk(s, 10)
+    assert np.array_equal(idx.cpu().numpy(), lidx)
+    idx2, _ = ops.topk_rows(torch.from_numpy(s).cuda(), 10)
+    assert np.array_equal(idx2.cpu().numpy(), lidx)
+    ranked = retrieval.rank_rows(q.cuda(), docs.cuda(), 3)
+    tidx, _ = R.topk(s, 10)
+    assert ranked.tie_rows.numel() == 25                            # every row's top 11 holds a tie
+    assert np.array_equal(ranked.idx.cpu().numpy(), tidx)
+    assert not np.array_equal(tidx, lidx)                           # torch's order is not column order here
+    assert ranked.hits.tolist() == R.hits(s, 3).sum(0).tolist()
+
+
+def _device_hit_flags(ranked, tgt_count, n_cols, row_offset=0, ks=(1, 5, 10)):
+    """[rows, len(ks)] bool from rank_rows' tables: rows without a tie from the torch-order top-10
+    table, re-selected rows from their per-k selections."""
+    idx = ranked.idx.cpu().numpy()
+    rows = np.arange(idx.shape[0]) + row_offset
+    out = np.stack([((idx[:, :min(k, n_cols)] // tgt_count) == rows[:, None]).any(1) for k in ks], 1)
+    tie = ranked.tie_rows.cpu().numpy()
+    for j, k in enumerate(ks):
+        if tie.size:
+            ik = ranked.tie_idx[min(k, n_cols)].cpu().numpy()
+            out[tie, j] = ((ik // tgt_count) == rows[tie, None]).any(1)
+    return out
+
+
+@pytest.mark.parametrize("case", ["wide", "narrow", "tiny"])
+def test_dense_exact_ties_vs_reference(cuda, golden, case):
+    """Exact fp32 ties on the dense path, pinned to the reference (dense_ties.npz: duplicated images /
+    captions scored by main.compute_similarity_scores, ranked by compute_metrics_detailed's per-k
+    torch.topk calls; T2I / Sym at 1 000, 300 and 40 columns cover both of torch's branches). Device:
+    every row's hit / miss at k = 1, 5, 10 and its top-10 IN torch.topk's ORDER identical to the
+    reference's (fp32 near-ties between unequal scores excepted and counted), the 9 metrics identical."""
+    from planted import bf16_sha, planted_ties
+    from oracle import retrieval as R
+    g = golden("dense_ties")
+    n, caps, D, seed = (int(x) for x in g[case + "_params"])
+    img_b, allt_b, _ = planted_ties(n, caps, D, float(g[case + "_noise"]), seed)
+    assert bf16_sha(img_b) == str(g[case + "_img_sha"]) and bf16_sha(allt_b) == str(g[case + "_txt_sha"])
+    img, allt = img_b.cuda(), allt_b.cuda()
+    t2i = allt[::caps].contiguous()
+    for p, (tag, q, d, tc) in enumerate((("t2i", t2i, img, 1), ("i2t", img, allt, caps), ("sym", img, t2i, 1))):
+        ranked = retrieval.rank_rows(q, d, tc)
+        same, near = R.compare_topk(ranked.idx.cpu().numpy(), g[f"{case}_{tag}_idx"], g[f"{case}_{tag}_score"])
+        flags = _device_hit_flags(ranked, tc, d.shape[0])
+        hit_same = (flags == g[case + "_hits"][p]).all(1)
+        tied = g[case + "_tied"][p]
+        dev_tied = np.zeros(n, bool)
+        dev_tied[ranked.tie_rows.cpu().numpy()] = True
+        print(f"{case} {tag}: {int(tied.sum())} reference rows with an exact tie in the top 11, "
+              f"{int(dev_tied.sum())} re-ranked on the device; top-10 identical {int(same.sum())}/{n}, "
+              f"hit rows identical {int(hit_same.sum())}/{n}, near-tie rows {int(near.sum())}")
+        assert (same | near).all(), f"{tag}: top-10 differs on decisive rows {np.nonzero(~same & ~near)[0][:5]}"
+        assert (hit_same | near).all(), f"{tag}: hit flags differ on rows {np.nonzero(~hit_same & ~near)[0][:5]}"
+        assert ((dev_tied == tied) | near).all()
+        assert tied.sum() > 0
+    got = retrieval.compute_metrics(img, t2i, allt)
+    assert list(got.values()) == list(g[case + "_metric_values"])
 
 
 @pytest.mark.parametrize("D", [8, 96, 200])

@@ -44,6 +44,21 @@ def test_similarity_matrix(cuda, golden):
     torch.testing.assert_close(s, ref, atol=1e-5, rtol=1e-5)
 
 
+@pytest.mark.parametrize("nq,nd,D", [(300, 3000, 256), (37, 301, 1152), (5, 130, 64)])
+def test_sim_scores_bit_identical_to_sim_topk(cuda, nq, nd, D):
+    """mme_sim_scores runs mme_sim_topk's own main loop: the full rows hold exactly the scores sim_topk
+    ranked (the exact-tie rows of rank_rows are re-selected from them)."""
+    gen = torch.Generator(device="cuda").manual_seed(nd)
+    q = torch.randn(nq, D, device="cuda", generator=gen).to(torch.bfloat16)
+    d = torch.randn(nd, D, device="cuda", generator=gen).to(torch.bfloat16)
+    idx, sc = ops.sim_topk(q, d, 11)
+    S = ops.sim_scores(q, d)
+    assert torch.equal(S.gather(1, idx.long()), sc)
+    torch.testing.assert_close(S, q.float() @ d.float().T, atol=1e-4, rtol=1e-5)
+    flags = ops.tie_rows(sc)
+    assert torch.equal(flags.bool(), (sc[:, 1:] == sc[:, :-1]).any(1))
+
+
 def test_topk_merge_and_offsets(cuda):
     gen = torch.Generator(device="cuda").manual_seed(4)
     q = torch.randn(300, 256, device="cuda", generator=gen).to(torch.bfloat16)

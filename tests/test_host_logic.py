@@ -180,3 +180,21 @@ def test_exec_batches_per_family():
     assert tail_aware_batch(5000, 512, sig.vision.num_patches, sig.vision) == 417
     for name in ("OpenAI-CLIP-L", "LAION-CLIP-H", "Apple-DFN5B-H"):
         assert exec_batches(REGISTRY[name]) == (512, 4096)
+
+
+@pytest.mark.parametrize("n", [7711, 8192, 16384, 40000])
+def test_exec_batch_keeps_gemm_operands_under_4gib(n):
+    """A SigLIP caption batch whose fc2 operand ([rows, max(3d, I_pad)] bf16) would reach 4 GiB is split
+    (pipe9 addresses operands with 32-bit offsets, so 8 192 captions at L = 64 would drop
+    fc2 to the generic kernel); the vision towers' 512-image batches stay under it too."""
+    from mme.config import REGISTRY, exec_batches
+    sig = REGISTRY["SigLIP-400M"]
+    t = sig.text
+    widest = t.max_pos * max(3 * t.hidden, t.inter_pad) * 2
+    b = tail_aware_batch(n, exec_batches(sig)[1], t.max_pos, t)
+    assert b * widest < 1 << 32 and b <= 7710
+    for name in ("SigLIP-400M", "LAION-CLIP-H", "Apple-DFN5B-H", "OpenAI-CLIP-L"):
+        v = REGISTRY[name].vision
+        rows = v.num_patches + 1
+        bv = tail_aware_batch(5000, exec_batches(REGISTRY[name])[0], rows, v)
+        assert bv * rows * max(3 * v.hidden, v.inter_pad) * 2 < 1 << 32
