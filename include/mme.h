@@ -36,7 +36,9 @@ extern "C" {
 #define MME_ERR_UNSUPPORTED 3 /* valid request this build does not handle  */
 
 #define MME_ABI_VERSION 8  /* 6: mme_gemm_res_stats row_part is [M][N / 64][2]; 7: mme_build_flags, mme_topk_rows_torch;
-                              8: mme_recall_hits skip mask, mme_sim_scores, mme_tie_rows */
+                              8: mme_recall_hits skip mask, mme_sim_scores, mme_tie_rows; per-call kernel
+                                 forms (mme_*_form) replace the process-global *_variant switches, which
+                                 remain in the development build only */
 
 /* mme_build_flags() bits */
 #define MME_BUILD_DEV 1 /* development / diagnostic kernel forms compiled in (libmme_dev.so) */
@@ -141,6 +143,26 @@ int mme_layernorm(const void* x, int ldx, const void* gamma, const void* beta, v
  * hd in {64, 72, 80}. Replaces eager/SDPA attention (TF:…siglip.py:228-247). */
 int mme_attention(const void* qkv, int ld_qkv, void* out, int ld_out, int B, int T, int H, int hd,
                   const int32_t* seq_lens, int causal, float scale, void* stream);
+
+/* Per-call kernel forms (ABI 8; bit-identity tests and A/B measurements). Each takes the
+ * arguments of its plain entry point after an int `form`; the library holds no switch
+ * (the plain entry points always run the production dispatch):
+ *   mme_gemm_form / mme_gemm_lnfold_form / mme_gemm_res_stats_form: -1 = production,
+ *     47 = pipe6 (the bit-identity reference of pipe8 / pipe9), 48 = the per-row statistics
+ *     combine (res_stats); other forms exist in the development build (libmme_dev.so) only;
+ *   mme_attention_form: 0 = production, 30 + kind = kernel kind `kind`;
+ *   mme_gemm_mx_form (below): -1 = production (mx10), 0 / 2 / 3 = earlier forms. */
+int mme_gemm_form(int form, const void* A, int lda, const void* B, int ldb, void* C, int ldc, int M, int N, int K,
+                  const void* bias, const void* residual, int ldr, int res_period, int act, int out_f32,
+                  void* stream);
+int mme_gemm_lnfold_form(int form, const void* A, int lda, const void* B, int ldb, void* C, int ldc, int M, int N,
+                         int K, const float* row_stats, const float* col_sum, const float* bias_f32, int act,
+                         void* stream);
+int mme_gemm_res_stats_form(int form, const void* A, int lda, const void* B, int ldb, void* C, int ldc, int M, int N,
+                            int K, const void* bias, const void* residual, int ldr, float eps, float* row_part,
+                            float* row_stats, void* stream);
+int mme_attention_form(int form, const void* qkv, int ld_qkv, void* out, int ld_out, int B, int T, int H, int hd,
+                       const int32_t* seq_lens, int causal, float scale, void* stream);
 
 /* SigLIP MAP pooling-head attention: one probe query per head against the
  * T keys/values of each image. q: bf16 [H*hd] (already projected);
@@ -293,6 +315,10 @@ int mme_layernorm_mx(const void* x, int ldx, const void* gamma, const void* beta
 int mme_gemm_mx(const void* A, int lda, const void* sa, int sa_rows, const void* B, int ldb, const void* sb,
                 int sb_rows, void* C, int ldc, void* c_scales, int c_rows_pad, int M, int N, int K, const void* bias,
                 const void* residual, int ldr, int res_period, int act, int out_mx, void* stream);
+int mme_gemm_mx_form(int form, const void* A, int lda, const void* sa, int sa_rows, const void* B, int ldb,
+                     const void* sb, int sb_rows, void* C, int ldc, void* c_scales, int c_rows_pad, int M, int N,
+                     int K, const void* bias, const void* residual, int ldr, int res_period, int act, int out_mx,
+                     void* stream);
 
 /* ------------------------------------------------ §8f-1: ColPali encoder ----
  * ColPali-v1.3 = PaliGemma-3B (SigLIP-448 vision tower + Gemma-2B) + 128-d head,

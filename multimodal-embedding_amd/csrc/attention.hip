@@ -2660,17 +2660,42 @@ bool launch_attn_dev(int, const AttnArgs&, int, int, int, hipStream_t) {
 }
 #endif
 
-int g_attn_variant = 0;  // dev-only override (tools/attn_bench.py)
+// Kernel form per call (mme_attention_form): 0 = the production dispatch, 30 + kind = force kernel
+// kind `kind` (the kinds compiled into this library; the bit-identity references of the tests).
+// The development build keeps a process-wide default for the plain entry points
+// (mme_attention_variant: tools/attn_bench.py, plus its diagnostic forms 1-4, 21-26, 200).
+#ifdef MME_DEV
+int g_attn_variant = 0;
+inline int attn_default_form() { return g_attn_variant; }
+#else
+inline int attn_default_form() { return 0; }
+#endif
 
+int attention_entry(int form, const void* qkv, int ld_qkv, void* out, int ld_out, int B, int T, int H, int hd,
+                    const int32_t* seq_lens, int causal, float scale, void* stream);
 }  // namespace
 
-extern "C" int mme_attention_variant(int v) {
+#ifdef MME_DEV
+extern "C" int mme_attention_variant(int v) {  // development build only
     g_attn_variant = v;
     return MME_OK;
 }
+#endif
 
 extern "C" int mme_attention(const void* qkv, int ld_qkv, void* out, int ld_out, int B, int T, int H, int hd,
                              const int32_t* seq_lens, int causal, float scale, void* stream) {
+    return attention_entry(attn_default_form(), qkv, ld_qkv, out, ld_out, B, T, H, hd, seq_lens, causal, scale, stream);
+}
+
+extern "C" int mme_attention_form(int form, const void* qkv, int ld_qkv, void* out, int ld_out, int B, int T, int H,
+                                  int hd, const int32_t* seq_lens, int causal, float scale, void* stream) {
+    MME_REQUIRE(form == 0 || (form >= 30 && form <= 199), "mme_attention_form: form %d (0 or 30 + kind)", form);
+    return attention_entry(form, qkv, ld_qkv, out, ld_out, B, T, H, hd, seq_lens, causal, scale, stream);
+}
+
+namespace {
+int attention_entry(int form, const void* qkv, int ld_qkv, void* out, int ld_out, int B, int T, int H, int hd,
+                    const int32_t* seq_lens, int causal, float scale, void* stream) {
     MME_REQUIRE(qkv && out, "mme_attention: null pointer");
     MME_REQUIRE(B >= 0 && T > 0 && H > 0, "mme_attention: bad shape");
     MME_REQUIRE(hd == 64 || hd == 72 || hd == 80, "mme_attention: head_dim %d unsupported (64/72/80)", hd);
@@ -2720,9 +2745,9 @@ extern "C" int mme_attention(const void* qkv, int ld_qkv, void* out, int ld_out,
                : (hd == 80 && pad12 <= pad8 && pad12 * 10 <= pad4 * 11) ? 23
                : (pad8 * 10 <= pad4 * 11 ? (hd == 72 ? 62 : 11) : 14);
 #ifdef MME_DEV
-    if (g_attn_variant >= 1 && g_attn_variant <= 4 && hd == 72) {  // dev-only diagnostic builds
+    if (form >= 1 && form <= 4 && hd == 72) {  // dev-only diagnostic builds
         const dim3 grid(cdiv(T, 128) * H * B);
-        switch (g_attn_variant) {
+        switch (form) {
             case 1: hipLaunchKernelGGL((attn_fwd_kernel<72, 1>), grid, dim3(256), 0, as_stream(stream), a); break;
             case 2: hipLaunchKernelGGL((attn_fwd_kernel<72, 2>), grid, dim3(256), 0, as_stream(stream), a); break;
             case 3: hipLaunchKernelGGL((attn_fwd_kernel<72, 3>), grid, dim3(256), 0, as_stream(stream), a); break;
@@ -2731,14 +2756,14 @@ extern "C" int mme_attention(const void* qkv, int ld_qkv, void* out, int ld_out,
         return mme_check_launch("mme_attention");
     }
 #endif
-    if (g_attn_variant >= 9 && g_attn_variant <= 16) kind = g_attn_variant - 9;  // dev: force a kernel
-    if (g_attn_variant >= 30 && g_attn_variant <= 199) kind = g_attn_variant - 30;  // dev: force a kernel
+    if (form >= 9 && form <= 16) kind = form - 9;  // dev: force a kernel
+    if (form >= 30 && form <= 199) kind = form - 30;  // dev: force a kernel
     if ((kind == 16 || kind == 19 || kind == 66) && T > 64) kind = 0;  // the short kernels hold one 64-key tile
 #ifdef MME_DEV
-    if (g_attn_variant >= 21 && g_attn_variant <= 26 && hd == 72) {  // dev: attn_dma_kernel<72,8,2> diagnostics
+    if (form >= 21 && form <= 26 && hd == 72) {  // dev: attn_dma_kernel<72,8,2> diagnostics
         const dim3 grid(cdiv(T, 256) * H * B), blk(512);
         hipStream_t st = as_stream(stream);
-        switch (g_attn_variant) {
+        switch (form) {
             case 21: hipLaunchKernelGGL((attn_dma_kernel<72, 8, 2, 1>), grid, blk, 0, st, a); break;
             case 22: hipLaunchKernelGGL((attn_dma_kernel<72, 8, 2, 2>), grid, blk, 0, st, a); break;
             case 23: hipLaunchKernelGGL((attn_dma_kernel<72, 8, 2, 3>), grid, blk, 0, st, a); break;
@@ -2755,6 +2780,7 @@ extern "C" int mme_attention(const void* qkv, int ld_qkv, void* out, int ld_out,
     MME_REQUIRE(ok, "mme_attention: kernel kind %d is a development form (build libmme_dev.so: make dev)", kind);
     return mme_check_launch("mme_attention");
 }
+}  // namespace
 
 namespace {
 // map_pool_kernel: the MAP head's attention with the probe query absorbed into the key
@@ -2870,7 +2896,7 @@ extern "C" int mme_probe_attention(const void* q, const void* kv, int ld_kv, voi
     if (B == 0) return MME_OK;
     const int D = H * hd, TR = H <= 16 && 256 % H == 0 ? 256 / H : 0;
     if (TR && D <= PROBE2_D && D % 8 == 0 && (TR * D / 8) % 64 == 0 && hd % 8 == 0 && ld_kv % 8 == 0 &&
-        ld_out % 8 == 0 && ((uintptr_t)out & 15) == 0 && ((uintptr_t)kv & 15) == 0 && g_attn_variant != 200)
+        ld_out % 8 == 0 && ((uintptr_t)out & 15) == 0 && ((uintptr_t)kv & 15) == 0 && attn_default_form() != 200)
         hipLaunchKernelGGL(probe_attn_img_kernel, dim3(B), dim3(256), 0, as_stream(stream), (const bf16*)q,
                            (const bf16*)kv, ld_kv, (bf16*)out, ld_out, T, H, hd, scale);
     else  // other geometries (and dev variant 200: the per-(image, head) form for A/B)

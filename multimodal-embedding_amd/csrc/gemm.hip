@@ -1984,8 +1984,20 @@ using BigCfg = Cfg<256, 128, 4, 2>;
 using SqCfg = Cfg<256, 256, 2, 4>;
 using SmallCfg = Cfg<128, 128, 2, 2>;
 
-int g_variant = -1;  // dev-only override (tools/gemm_bench.py)
-int gemm_dispatch(GemmArgs a, hipStream_t s);
+// Kernel form of a call: -1 = the production dispatch; otherwise a named form, chosen PER CALL
+// through the mme_*_form entry points (the production library takes the bit-identity references
+// 47 = pipe6 and 48 = the per-row statistics combine; the development build every form). No
+// process-global switch exists in the production library; the development build keeps one
+// (mme_gemm_variant, tools/gemm_bench.py) as the form of the plain entry points.
+#ifdef MME_DEV
+int g_variant = -1;
+inline int default_form() { return g_variant; }
+inline bool form_ok(int) { return true; }
+#else
+inline int default_form() { return -1; }
+inline bool form_ok(int v) { return v == -1 || v == 47 || v == 48; }
+#endif
+int gemm_dispatch(GemmArgs a, int variant, hipStream_t s);
 
 }  // namespace
 
@@ -1993,20 +2005,16 @@ extern "C" int mme_gemm_debug_buffer(void* p) {  // dev: device buffer for varia
     return hipMemcpyToSymbol(HIP_SYMBOL(g_gemm_dbg), &p, sizeof(p)) == hipSuccess ? MME_OK : MME_ERR_HIP;
 }
 
-extern "C" int mme_gemm_variant(int v) {
-#ifndef MME_DEV
-    // the production library holds the dispatched kernels and pipe6 (variant 47, the
-    // bit-identity reference of pipe8) / the per-row statistics combine (48) only
-    MME_REQUIRE(v == -1 || v == 47 || v == 48, "mme_gemm_variant: variant %d is a development form "
-                "(build libmme_dev.so: make dev)", v);
-#endif
+#ifdef MME_DEV
+extern "C" int mme_gemm_variant(int v) {  // development build only: the form of the plain entry points
     g_variant = v;
     return MME_OK;
 }
+#endif
 
-extern "C" int mme_gemm(const void* A, int lda, const void* B, int ldb, void* Cp, int ldc, int M, int N, int K,
-                        const void* bias, const void* residual, int ldr, int res_period, int act, int out_f32,
-                        void* stream) {
+namespace {
+int gemm_entry(int form, const void* A, int lda, const void* B, int ldb, void* Cp, int ldc, int M, int N, int K,
+               const void* bias, const void* residual, int ldr, int res_period, int act, int out_f32, void* stream) {
     MME_REQUIRE(A && B && Cp, "mme_gemm: null operand");
     MME_REQUIRE(M > 0 && N > 0 && K > 0, "mme_gemm: empty shape M=%d N=%d K=%d", M, N, K);
     MME_REQUIRE(K % BK == 0, "mme_gemm: K=%d must be a multiple of %d (pad weights/activations)", K, BK);
@@ -2019,7 +2027,22 @@ extern "C" int mme_gemm(const void* A, int lda, const void* B, int ldb, void* Cp
     MME_REQUIRE(res_period >= 0, "mme_gemm: res_period < 0");
     GemmArgs a{(const bf16*)A, (const bf16*)B, Cp, (const bf16*)bias, (const bf16*)residual,
                lda, ldb, ldc, ldr, M, N, K, res_period, act, out_f32, 0, nullptr, nullptr, nullptr, nullptr};
-    return gemm_dispatch(a, as_stream(stream));
+    return gemm_dispatch(a, form, as_stream(stream));
+}
+}  // namespace
+
+extern "C" int mme_gemm(const void* A, int lda, const void* B, int ldb, void* Cp, int ldc, int M, int N, int K,
+                        const void* bias, const void* residual, int ldr, int res_period, int act, int out_f32,
+                        void* stream) {
+    return gemm_entry(default_form(), A, lda, B, ldb, Cp, ldc, M, N, K, bias, residual, ldr, res_period, act, out_f32,
+                      stream);
+}
+
+extern "C" int mme_gemm_form(int form, const void* A, int lda, const void* B, int ldb, void* Cp, int ldc, int M, int N,
+                             int K, const void* bias, const void* residual, int ldr, int res_period, int act,
+                             int out_f32, void* stream) {
+    MME_REQUIRE(form_ok(form), "mme_gemm_form: form %d is a development form (build libmme_dev.so: make dev)", form);
+    return gemm_entry(form, A, lda, B, ldb, Cp, ldc, M, N, K, bias, residual, ldr, res_period, act, out_f32, stream);
 }
 
 namespace {
@@ -2076,9 +2099,10 @@ __global__ __launch_bounds__(256) void row_part_combine_lds_kernel(const float* 
 }
 }  // namespace
 
-extern "C" int mme_gemm_res_stats(const void* A, int lda, const void* B, int ldb, void* Cp, int ldc, int M, int N,
-                                  int K, const void* bias, const void* residual, int ldr, float eps, float* row_part,
-                                  float* row_stats, void* stream) {
+namespace {
+int res_stats_entry(int variant, const void* A, int lda, const void* B, int ldb, void* Cp, int ldc, int M, int N,
+                    int K, const void* bias, const void* residual, int ldr, float eps, float* row_part,
+                    float* row_stats, void* stream) {
     MME_REQUIRE(A && B && Cp && residual && row_part && row_stats, "mme_gemm_res_stats: null operand");
     MME_REQUIRE(M > 0 && N > 0 && K > 0, "mme_gemm_res_stats: empty shape M=%d N=%d K=%d", M, N, K);
     MME_REQUIRE(K % BK == 0, "mme_gemm_res_stats: K=%d must be a multiple of %d", K, BK);
@@ -2091,22 +2115,22 @@ extern "C" int mme_gemm_res_stats(const void* A, int lda, const void* B, int ldb
     hipStream_t s = as_stream(stream);
     GemmArgs a{(const bf16*)A, (const bf16*)B, Cp, (const bf16*)bias, (const bf16*)residual,
                lda, ldb, ldc, ldr, M, N, K, 0, MME_ACT_NONE, 0, 0, nullptr, nullptr, nullptr, row_part};
-    const bool fused = (g_variant < 0 || g_variant == 47 || g_variant == 48) && ldc % 8 == 0 && ((uintptr_t)Cp & 15) == 0 && ldr % 8 == 0 &&
+    const bool fused = (variant < 0 || variant == 47 || variant == 48) && ldc % 8 == 0 && ((uintptr_t)Cp & 15) == 0 && ldr % 8 == 0 &&
                        ((uintptr_t)residual & 15) == 0 && (long)M * N >= 1024L * 1024;
     if (!fused) {  // shapes the pipelined kernel does not take: GEMM, then the row statistics pass
         a.row_part = nullptr;
-        const int rc = gemm_dispatch(a, s);
+        const int rc = gemm_dispatch(a, variant, s);
         if (rc != MME_OK) return rc;
         return mme_rowstats(Cp, ldc, M, N, eps, row_stats, stream);
     }
-    if (pipe8_ok(a) && g_variant != 47)  // variant 47: pipe6 (tests: pipe9 / pipe8 are bit-identical to it)
+    if (pipe8_ok(a) && variant != 47)  // variant 47: pipe6 (tests: pipe9 / pipe8 are bit-identical to it)
         N % 256 == 128 ? launch_pipe9<Pipe256, 4, true>(a, s) : launch_pipe9<Pipe256, 4, false>(a, s);
     else
         N % 256 == 128 ? launch_pipe6<Pipe256, 4, 1, 0, true>(a, s) : launch_pipe6<Pipe256, 4, 1>(a, s);
     const int rc = mme_check_launch("mme_gemm_res_stats");
     if (rc != MME_OK) return rc;
     const int np = N / 64;
-    if (np % 2 == 0 && np <= COMBINE_MAXP && ((uintptr_t)row_part & 15) == 0 && g_variant != 48)
+    if (np % 2 == 0 && np <= COMBINE_MAXP && ((uintptr_t)row_part & 15) == 0 && variant != 48)
         hipLaunchKernelGGL(row_part_combine_lds_kernel, dim3(cdiv(M, 256)), dim3(256), 0, s, row_part, row_stats, M, np,
                            eps);
     else  // variant 48: the per-row form (A/B)
@@ -2114,10 +2138,26 @@ extern "C" int mme_gemm_res_stats(const void* A, int lda, const void* B, int ldb
                            eps);
     return mme_check_launch("mme_gemm_res_stats");
 }
+}  // namespace
 
-extern "C" int mme_gemm_lnfold(const void* A, int lda, const void* B, int ldb, void* Cp, int ldc, int M, int N,
-                               int K, const float* row_stats, const float* col_sum, const float* bias_f32, int act,
-                               void* stream) {
+extern "C" int mme_gemm_res_stats(const void* A, int lda, const void* B, int ldb, void* Cp, int ldc, int M, int N,
+                                  int K, const void* bias, const void* residual, int ldr, float eps, float* row_part,
+                                  float* row_stats, void* stream) {
+    return res_stats_entry(default_form(), A, lda, B, ldb, Cp, ldc, M, N, K, bias, residual, ldr, eps, row_part,
+                           row_stats, stream);
+}
+
+extern "C" int mme_gemm_res_stats_form(int form, const void* A, int lda, const void* B, int ldb, void* Cp, int ldc,
+                                       int M, int N, int K, const void* bias, const void* residual, int ldr, float eps,
+                                       float* row_part, float* row_stats, void* stream) {
+    MME_REQUIRE(form_ok(form), "mme_gemm_res_stats_form: form %d is a development form (make dev)", form);
+    return res_stats_entry(form, A, lda, B, ldb, Cp, ldc, M, N, K, bias, residual, ldr, eps, row_part, row_stats,
+                           stream);
+}
+
+namespace {
+int lnfold_entry(int form, const void* A, int lda, const void* B, int ldb, void* Cp, int ldc, int M, int N, int K,
+                 const float* row_stats, const float* col_sum, const float* bias_f32, int act, void* stream) {
     MME_REQUIRE(A && B && Cp && row_stats && col_sum && bias_f32, "mme_gemm_lnfold: null operand");
     MME_REQUIRE(M > 0 && N > 0 && K > 0, "mme_gemm_lnfold: empty shape M=%d N=%d K=%d", M, N, K);
     MME_REQUIRE(K % BK == 0, "mme_gemm_lnfold: K=%d must be a multiple of %d", K, BK);
@@ -2128,29 +2168,43 @@ extern "C" int mme_gemm_lnfold(const void* A, int lda, const void* B, int ldb, v
                 "mme_gemm_lnfold: col_sum / bias_f32 must be 16-byte and row_stats 8-byte aligned");
     GemmArgs a{(const bf16*)A, (const bf16*)B, Cp, nullptr, nullptr, lda, ldb, ldc, 0, M, N, K, 0, act, 0, 0,
                row_stats, col_sum, bias_f32, nullptr};
-    return gemm_dispatch(a, as_stream(stream));
+    return gemm_dispatch(a, form, as_stream(stream));
+}
+}  // namespace
+
+extern "C" int mme_gemm_lnfold(const void* A, int lda, const void* B, int ldb, void* Cp, int ldc, int M, int N,
+                               int K, const float* row_stats, const float* col_sum, const float* bias_f32, int act,
+                               void* stream) {
+    return lnfold_entry(default_form(), A, lda, B, ldb, Cp, ldc, M, N, K, row_stats, col_sum, bias_f32, act, stream);
+}
+
+extern "C" int mme_gemm_lnfold_form(int form, const void* A, int lda, const void* B, int ldb, void* Cp, int ldc, int M,
+                                    int N, int K, const float* row_stats, const float* col_sum, const float* bias_f32,
+                                    int act, void* stream) {
+    MME_REQUIRE(form_ok(form), "mme_gemm_lnfold_form: form %d is a development form (make dev)", form);
+    return lnfold_entry(form, A, lda, B, ldb, Cp, ldc, M, N, K, row_stats, col_sum, bias_f32, act, stream);
 }
 
 namespace {
-int gemm_dispatch(GemmArgs a, hipStream_t s) {
+int gemm_dispatch(GemmArgs a, int variant, hipStream_t s) {
     const int M = a.M, N = a.N, K = a.K, ldc = a.ldc, ldr = a.ldr, act = a.act, out_f32 = a.out_f32;
     const void* Cp = a.C;
     const void* residual = a.res;
     (void)K;
     const bool glu = act == MME_ACT_GEGLU_TANH;
 #ifdef MME_DEV
-    if (g_variant >= 40 && g_variant <= 43) {  // dev: pipe6 with the first block wave de-phased by
-        a.stagger = (g_variant - 39) * (K / 32) / 12;  // (variant-39)/4 of a tile per phase step
+    if (variant >= 40 && variant <= 43) {  // dev: pipe6 with the first block wave de-phased by
+        a.stagger = (variant - 39) * (K / 32) / 12;  // (variant-39)/4 of a tile per phase step
         return launch_pipe6<Pipe256, 4, 1>(a, s);
     }
 #endif
     if (glu) {  // gated epilogue: the pipelined kernel only (its LDS-staged 16-B tile rows pair gate/up)
         MME_REQUIRE(N % 8 == 0 && ldc % 4 == 0 && !out_f32 && !residual && ((uintptr_t)Cp & 7) == 0,
                     "mme_gemm: GeGLU needs N %% 8 == 0, ldc %% 4 == 0, 8-B aligned bf16 C, no residual");
-        if (pipe8_ok(a) && g_variant != 47) return launch_pipe9<Pipe256, 4, false>(a, s);
+        if (pipe8_ok(a) && variant != 47) return launch_pipe9<Pipe256, 4, false>(a, s);
         return launch_pipe6<Pipe256, 4, 1>(a, s);
     }
-    switch (g_variant) {
+    switch (variant) {
         case 47:  // pipe6 as dispatched before pipe8: split grid (512 x 128 tiles for the last 128 columns) where N = 256 k + 128
             if (a.N % 256 == 128) return launch_pipe6<Pipe256, 4, 1, 0, true>(a, s);
             return launch_pipe6<Pipe256, 4, 1>(a, s);
@@ -2243,7 +2297,7 @@ int gemm_dispatch(GemmArgs a, hipStream_t s) {
         case 81:  // dev: pipe9, static priority 1 for the late wave row, no per-phase setprio
         case 82:  // dev: pipe9 without any setprio
             if (!pipe8_ok(a)) break;
-            if (g_variant == 81)
+            if (variant == 81)
                 return N % 256 == 128 ? launch_pipe9<Pipe256, 4, true, 1>(a, s) : launch_pipe9<Pipe256, 4, false, 1>(a, s);
             return N % 256 == 128 ? launch_pipe9<Pipe256, 4, true, 2>(a, s) : launch_pipe9<Pipe256, 4, false, 2>(a, s);
         case 83:  // dev: pipe9 with 8-row tile bands

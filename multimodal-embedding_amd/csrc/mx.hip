@@ -891,7 +891,22 @@ int launch_mx9(const MxArgs& a, hipStream_t s) {
 
 #endif  // MME_DEV
 
-int g_mx_variant = -1;  // dev: 9 = mx9 where its geometry holds
+// Kernel form per call (mme_gemm_mx_form): -1 = production (mx10 where its geometry holds), 0 = the
+// round-2 kernel, 2 = its per-wave epilogue alone, 3 = + the scale wave (mx10's fallback), 9 = mx9
+// (development build). The development build keeps a process-wide default (mme_gemm_mx_variant).
+#ifdef MME_DEV
+int g_mx_variant = -1;
+inline int mx_default_form() { return g_mx_variant; }
+#else
+inline int mx_default_form() { return -1; }
+#endif
+inline bool mx_form_ok(int v) {
+#ifdef MME_DEV
+    return v == -1 || v == 0 || v == 2 || v == 3 || v == 9;
+#else
+    return v == -1 || v == 0 || v == 2 || v == 3;
+#endif
+}
 
 template <int GROUP_M, bool WEPI = false, bool SC1 = false>
 int launch_mx(const MxArgs& a, hipStream_t s) {
@@ -943,20 +958,41 @@ extern "C" int mme_layernorm_mx(const void* x, int ldx, const void* gamma, const
     return mme_check_launch("mme_layernorm_mx");
 }
 
-extern "C" int mme_gemm_mx_variant(int v) {  // A/B and tests: -1 = production (mx10), 0 = round-2 form,
-                                             // 2 = + per-wave epilogue, 3 = + scale wave, 9 = mx9 (MME_DEV)
-    MME_REQUIRE(v == -1 || v == 0 || v == 2 || v == 3 || v == 9, "mme_gemm_mx_variant: unknown variant %d", v);
-#ifndef MME_DEV
-    MME_REQUIRE(v != 9, "mme_gemm_mx_variant: variant 9 (mx9) is a development form (build libmme_dev.so: make dev)");
-#endif
+#ifdef MME_DEV
+extern "C" int mme_gemm_mx_variant(int v) {  // development build only: the form of mme_gemm_mx
+    MME_REQUIRE(mx_form_ok(v), "mme_gemm_mx_variant: unknown variant %d", v);
     g_mx_variant = v;
     return MME_OK;
+}
+#endif
+
+namespace {
+int gemm_mx_entry(int form, const void* A, int lda, const void* sa, int sa_rows, const void* B, int ldb, const void* sb,
+                  int sb_rows, void* Cp, int ldc, void* c_scales, int c_rows_pad, int M, int N, int K, const void* bias,
+                  const void* residual, int ldr, int res_period, int act, int out_mx, void* stream);
+}  // namespace
+
+extern "C" int mme_gemm_mx_form(int form, const void* A, int lda, const void* sa, int sa_rows, const void* B, int ldb,
+                                const void* sb, int sb_rows, void* Cp, int ldc, void* c_scales, int c_rows_pad, int M,
+                                int N, int K, const void* bias, const void* residual, int ldr, int res_period, int act,
+                                int out_mx, void* stream) {
+    MME_REQUIRE(mx_form_ok(form), "mme_gemm_mx_form: form %d is unknown or a development form (make dev)", form);
+    return gemm_mx_entry(form, A, lda, sa, sa_rows, B, ldb, sb, sb_rows, Cp, ldc, c_scales, c_rows_pad, M, N, K, bias,
+                         residual, ldr, res_period, act, out_mx, stream);
 }
 
 extern "C" int mme_gemm_mx(const void* A, int lda, const void* sa, int sa_rows, const void* B, int ldb,
                            const void* sb, int sb_rows, void* Cp, int ldc, void* c_scales, int c_rows_pad, int M,
                            int N, int K, const void* bias, const void* residual, int ldr, int res_period, int act,
                            int out_mx, void* stream) {
+    return gemm_mx_entry(mx_default_form(), A, lda, sa, sa_rows, B, ldb, sb, sb_rows, Cp, ldc, c_scales, c_rows_pad, M,
+                         N, K, bias, residual, ldr, res_period, act, out_mx, stream);
+}
+
+namespace {
+int gemm_mx_entry(int form, const void* A, int lda, const void* sa, int sa_rows, const void* B, int ldb, const void* sb,
+                  int sb_rows, void* Cp, int ldc, void* c_scales, int c_rows_pad, int M, int N, int K, const void* bias,
+                  const void* residual, int ldr, int res_period, int act, int out_mx, void* stream) {
     MME_REQUIRE(A && B && sa && sb && Cp, "mme_gemm_mx: null operand");
     MME_REQUIRE(M >= 0 && N > 0 && K > 0 && K % 64 == 0, "mme_gemm_mx: K=%d must be a positive multiple of 64", K);
     MME_REQUIRE(lda % 16 == 0 && ldb % 16 == 0 && lda >= K && ldb >= K, "mme_gemm_mx: lda/ldb must be >= K, % 16");
@@ -980,7 +1016,7 @@ extern "C" int mme_gemm_mx(const void* A, int lda, const void* sa, int sa_rows, 
              res_period, act, out_mx};
 #ifdef MME_DEV
     // dev variant 9: mx9 where its geometry holds (every DFN5B-H encoder shape); 32-bit DMA offsets
-    if (g_mx_variant == 9 && K % 128 == 0 && K >= 256 && N % 256 == 0 && (size_t)M * lda < (1ull << 32) &&
+    if (form == 9 && K % 128 == 0 && K >= 256 && N % 256 == 0 && (size_t)M * lda < (1ull << 32) &&
         (size_t)N * ldb < (1ull << 32) && (size_t)(K / 32) * (sa_rows > sb_rows ? sa_rows : sb_rows) < (1ull << 32))
         return launch_mx9<4>(a, as_stream(stream));
 #endif
@@ -990,8 +1026,9 @@ extern "C" int mme_gemm_mx(const void* A, int lda, const void* sa, int sa_rows, 
     // gemm_mx_kernel form with the same epilogue and scale wave. A/B forms: variant 0 = the round-2
     // kernel, 2 = its per-wave epilogue alone, 3 = + the scale wave (mx10's fallback).
     const bool mx10_ok = K >= 256 && (size_t)M * lda < (1ull << 32) && (size_t)N * ldb < (1ull << 32);
-    if (g_mx_variant == 0) return launch_mx<4>(a, as_stream(stream));
-    if (g_mx_variant == 2) return launch_mx<4, true>(a, as_stream(stream));
-    if (g_mx_variant == 3 || !mx10_ok) return launch_mx<4, true, true>(a, as_stream(stream));
+    if (form == 0) return launch_mx<4>(a, as_stream(stream));
+    if (form == 2) return launch_mx<4, true>(a, as_stream(stream));
+    if (form == 3 || !mx10_ok) return launch_mx<4, true, true>(a, as_stream(stream));
     return launch_mx10<4>(a, as_stream(stream));
 }
+}  // namespace

@@ -69,6 +69,9 @@ SIGNATURES = {
     "mme_l2norm_masked": (c_int, [_P, c_int, _P, c_int, c_int, c_int, _P, _P]),
     "mme_attention_mqa": (c_int, [_P, c_int, _P, c_int, c_int, c_int, c_int, c_int, _P, _P, c_float, _P]),
 }
+# per-call kernel forms (ABI 8; mme.ops.kernel_forms): the entry point's arguments after an int form
+for _name in ("mme_gemm", "mme_gemm_lnfold", "mme_gemm_res_stats", "mme_attention", "mme_gemm_mx"):
+    SIGNATURES[_name + "_form"] = (c_int, [c_int] + SIGNATURES[_name][1])
 
 
 class MMEError(RuntimeError):

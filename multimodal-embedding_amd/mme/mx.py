@@ -80,28 +80,17 @@ def layernorm(x: torch.Tensor, g: torch.Tensor, b: torch.Tensor, eps: float, out
     return MXTensor(out.q, out.scales, rows, d)
 
 
-_variant_set = False
-
-
-def _apply_variant_env():
-    """MME_MX_VARIANT=<v>: mme_gemm_mx_variant(v) for every later mx GEMM (job-level A/B of kernel forms)."""
-    global _variant_set
-    _variant_set = True
+def _env_form() -> Optional[int]:
+    """MME_MX_VARIANT=<v>: every mx GEMM of this process runs form v (job-level A/B of kernel forms),
+    passed per call (mme_gemm_mx_form)."""
     v = os.environ.get("MME_MX_VARIANT")
-    if v is not None:
-        import ctypes
-        from . import _lib
-        lib = _lib.load()
-        lib.mme_gemm_mx_variant.argtypes = [ctypes.c_int]
-        lib.mme_gemm_mx_variant(int(v))
+    return None if v is None else int(v)
 
 
 def gemm(a: MXTensor, w: MXTensor, bias: Optional[torch.Tensor] = None, *, residual: Optional[torch.Tensor] = None,
          res_period: int = 0, act: int = ACT_NONE, out: Optional[torch.Tensor] = None,
          out_mx: Optional[MXTensor] = None, algo_flops: Optional[float] = None):
     """act(a @ w.T + bias) (+ residual): bf16 [M, N] into `out`, or mx8 into `out_mx`."""
-    if not _variant_set:
-        _apply_variant_env()
     if a.k != w.k:
         raise ValueError(f"gemm_mx: K mismatch {a.k} vs {w.k}")
     M, N, K = a.rows, w.rows, a.k
@@ -116,7 +105,10 @@ def gemm(a: MXTensor, w: MXTensor, bias: Optional[torch.Tensor] = None, *, resid
         cptr, ldc, csc, crows = out.data_ptr(), ops._rowmajor(out, "out"), None, 0
     ldr = ops._rowmajor(residual, "residual") if residual is not None else 0
     ev = ops.KernelTimer.begin()
-    call("mme_gemm_mx", a.q.data_ptr(), a.q.stride(0), a.scales.data_ptr(), a.rows_pad, w.q.data_ptr(),
+    form = ops._form("mx")
+    form = _env_form() if form is None else form
+    entry, pre = ("mme_gemm_mx", ()) if form is None else ("mme_gemm_mx_form", (form,))
+    call(entry, *pre, a.q.data_ptr(), a.q.stride(0), a.scales.data_ptr(), a.rows_pad, w.q.data_ptr(),
          w.q.stride(0), w.scales.data_ptr(), w.rows_pad, cptr, ldc, csc, crows, M, N, K, ops._ptr(bias),
          ops._ptr(residual), ldr, int(res_period), int(act), int(out_mx is not None), ops._stream())
     ops.KernelTimer.end(ev, "gemm_mx", algo_flops if algo_flops is not None else 2.0 * M * N * K,

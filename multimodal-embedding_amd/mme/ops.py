@@ -7,7 +7,9 @@ host or falls back to torch ops: a missing library or a CPU tensor raises.
 """
 from __future__ import annotations
 
+import contextlib
 import math
+import threading
 from typing import Optional, Sequence
 
 import torch
@@ -16,6 +18,35 @@ from . import _lib
 from ._lib import call, query
 
 BF16 = torch.bfloat16
+
+_forms = threading.local()
+
+
+@contextlib.contextmanager
+def kernel_forms(**forms: int):
+    """Kernel forms for the calls this thread makes inside the block (bit-identity tests, A/B):
+    gemm=47 (pipe6) / 48 (per-row statistics combine), mx=0 / 2 / 3 (earlier mx GEMM forms),
+    attention=30 + kind (force an attention kernel kind). Each call passes its form to the library
+    through the mme_*_form entry points; the library itself holds no switch."""
+    old = dict(getattr(_forms, "d", {}))
+    _forms.d = {**old, **forms}
+    try:
+        yield
+    finally:
+        _forms.d = old
+
+
+def _form(name: str) -> Optional[int]:
+    return getattr(_forms, "d", {}).get(name)
+
+
+def _call_form(entry: str, family: str, *args) -> None:
+    """call(entry, *args), or call(entry + "_form", form, *args) when this thread set a form."""
+    f = _form(family)
+    if f is None:
+        call(entry, *args)
+    else:
+        call(entry + "_form", int(f), *args)
 
 
 def _stream() -> int:
@@ -151,7 +182,7 @@ def gemm(a: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None, 
     if bias is not None and bias.numel() < N:
         raise ValueError("gemm: bias shorter than N")
     ev = KernelTimer.begin()
-    call("mme_gemm", a.data_ptr(), lda, w.data_ptr(), ldb, out.data_ptr(), ldc, M, N, K, _ptr(bias),
+    _call_form("mme_gemm", "gemm", a.data_ptr(), lda, w.data_ptr(), ldb, out.data_ptr(), ldc, M, N, K, _ptr(bias),
          _ptr(residual), ldr, res_period, act, int(out_f32), _stream())
     res_bytes = 2.0 * M * N if residual is not None else 0.0
     KernelTimer.end(ev, "gemm", algo_flops if algo_flops is not None else 2.0 * M * N * K,
@@ -178,7 +209,7 @@ def gemm_res_stats(a: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor
     if out is None:
         out = torch.empty(M, N, dtype=BF16, device=a.device)
     ev = KernelTimer.begin()
-    call("mme_gemm_res_stats", a.data_ptr(), _rowmajor(a, "a"), w.data_ptr(), _rowmajor(w, "w"), out.data_ptr(),
+    _call_form("mme_gemm_res_stats", "gemm", a.data_ptr(), _rowmajor(a, "a"), w.data_ptr(), _rowmajor(w, "w"), out.data_ptr(),
          _rowmajor(out, "out"), M, N, K, _ptr(bias), residual.data_ptr(), _rowmajor(residual, "residual"),
          float(eps), part.data_ptr(), stats.data_ptr(), _stream())
     # the "gemm" family's time includes the statistics combine pass (row_part_combine_kernel, one
@@ -215,7 +246,7 @@ def gemm_lnfold(x: torch.Tensor, folded: "LNFolded", stats: torch.Tensor, *, act
     if out is None:
         out = torch.empty(M, N, dtype=BF16, device=x.device)
     ev = KernelTimer.begin()
-    call("mme_gemm_lnfold", x.data_ptr(), _rowmajor(x, "x"), folded.w.data_ptr(), _rowmajor(folded.w, "w"),
+    _call_form("mme_gemm_lnfold", "gemm", x.data_ptr(), _rowmajor(x, "x"), folded.w.data_ptr(), _rowmajor(folded.w, "w"),
          out.data_ptr(), _rowmajor(out, "out"), M, N, K, stats.data_ptr(), folded.cs.data_ptr(),
          folded.b.data_ptr(), act, _stream())
     KernelTimer.end(ev, "gemm", algo_flops if algo_flops is not None else 2.0 * M * N * K,
@@ -280,7 +311,7 @@ def attention(qkv: torch.Tensor, B: int, T: int, H: int, hd: int, *, seq_lens: O
         raise ValueError("attention: seq_lens must be int32 [B]")
     scale = hd ** -0.5 if scale is None else scale
     ev = KernelTimer.begin()
-    call("mme_attention", qkv.data_ptr(), _rowmajor(qkv, "qkv"), out.data_ptr(), _rowmajor(out, "out"), B, T, H, hd,
+    _call_form("mme_attention", "attention", qkv.data_ptr(), _rowmajor(qkv, "qkv"), out.data_ptr(), _rowmajor(out, "out"), B, T, H, hd,
          _ptr(seq_lens), int(causal), float(scale), _stream())
     KernelTimer.end(ev, "attention", 4.0 * B * H * T * T * hd * (0.5 if causal else 1.0))
     return out

@@ -65,14 +65,17 @@ def test_workspace_queries():
 
 
 def test_production_library_holds_no_dev_forms():
-    """The default libmme.so is the production build: dev / diagnostic kernel forms are
-    refused loudly (they live in libmme_dev.so, `make dev`, MME_DEV=1)."""
+    """The default libmme.so is the production build: no process-global kernel switch is exported
+    (ABI 8: forms are chosen per call, mme_*_form), and dev / diagnostic kernel forms are refused
+    loudly (they live in libmme_dev.so, `make dev`, MME_DEV=1). Argument checks run before any
+    launch, so no GPU is needed."""
     lib = _lib.load()
     if _lib.is_dev():
         pytest.skip("the development library is loaded (MME_DEV=1)")
-    lib.mme_gemm_variant.argtypes = [ctypes.c_int]
-    assert lib.mme_gemm_variant(64) != 0 and b"development form" in lib.mme_last_error()
-    assert lib.mme_gemm_variant(47) == 0 and lib.mme_gemm_variant(-1) == 0
-    lib.mme_gemm_mx_variant.argtypes = [ctypes.c_int]
-    assert lib.mme_gemm_mx_variant(9) != 0 and b"development form" in lib.mme_last_error()
-    assert lib.mme_gemm_mx_variant(-1) == 0
+    for name in ("mme_gemm_variant", "mme_gemm_mx_variant", "mme_attention_variant"):
+        assert getattr(lib, name, None) is None or not hasattr(lib, name), name
+    args = [None, 64, None, 64, None, 64, 16, 16, 64, None, None, 0, 0, 0, 0, None]
+    assert lib.mme_gemm_form(64, *args) != 0 and b"development form" in lib.mme_last_error()
+    mx_args = [None, 64, None, 256, None, 64, None, 256, None, 64, None, 0, 16, 16, 64, None, None, 0, 0, 0, 0, None]
+    assert lib.mme_gemm_mx_form(9, *mx_args) != 0 and b"development form" in lib.mme_last_error()
+    assert lib.mme_attention_form(7, None, 8, None, 8, 1, 1, 1, 64, None, 0, 1.0, None) != 0

@@ -146,17 +146,12 @@ PROD_ATTN_KINDS = (38, 41, 62, 65)  # in the production library; the rest are de
 ])
 def test_attention_m32(cuda, kind, B, T, H, hd, causal, lens):
     """attn_m32_kernel (v_mfma_f32_32x32x16_bf16 flash loop) forced through the dev switch."""
-    from mme import _lib
-    lib = _lib.load()
     g = torch.Generator(device="cuda").manual_seed(B * T + hd + kind)
     qkv = rnd(B * T, 3 * H * hd, scale=1.5, gen=g)
     sl = None if lens is None else torch.tensor(lens, dtype=torch.int32, device="cuda")
-    lib.mme_attention_variant(30 + kind)
-    try:
+    with ops.kernel_forms(attention=30 + kind):
         out = ops.attention(qkv, B, T, H, hd, seq_lens=sl, causal=causal)
-        torch.cuda.synchronize()
-    finally:
-        lib.mme_attention_variant(0)
+    torch.cuda.synchronize()
     ref = attn_ref(qkv, B, T, H, hd, sl, causal, hd ** -0.5)
     torch.testing.assert_close(out.float(), ref, atol=2e-2, rtol=2e-2)
 
@@ -173,19 +168,14 @@ def test_attention_m32_skip(cuda, B, T, H, causal, lens):
     block's P is 0, but an MFMA with an all-zero operand still re-rounds its accumulator in rare cases:
     both kernels deterministic, a few bf16 ulps apart on < 1e-4 of the outputs (measured 1 / 0.70 M
     and 15 / 1.32 M, max 0.00195)."""
-    from mme import _lib
-    lib = _lib.load()
     g = torch.Generator(device="cuda").manual_seed(B * T)
     qkv = rnd(B * T, 3 * H * 80, scale=1.5, gen=g)
     sl = None if lens is None else torch.tensor(lens, dtype=torch.int32, device="cuda")
     outs = []
     for kind in (41, 41, 65, 65):
-        lib.mme_attention_variant(30 + kind)
-        try:
+        with ops.kernel_forms(attention=30 + kind):
             outs.append(ops.attention(qkv, B, T, H, 80, seq_lens=sl, causal=causal))
-            torch.cuda.synchronize()
-        finally:
-            lib.mme_attention_variant(0)
+        torch.cuda.synchronize()
     assert torch.equal(outs[0], outs[1]) and torch.equal(outs[2], outs[3]), "attention is not deterministic"
     a, b = outs[0].float(), outs[2].float()
     d = (a - b).abs()
@@ -223,15 +213,11 @@ def test_attention_hd72_production_grid_vs_kind30(cuda):
     B, T, H, hd = 239, 729, 16, 72
     g = torch.Generator(device="cuda").manual_seed(729)
     qkv = rnd(B * T, 3 * H * hd, scale=1.5, gen=g)
-    lib = _lib.load()
     outs = {}
     for kind in (0, 30):
-        lib.mme_attention_variant(0 if kind == 0 else 30 + kind)
-        try:
+        with ops.kernel_forms(attention=0 if kind == 0 else 30 + kind):
             outs[kind] = ops.attention(qkv, B, T, H, hd).float()
-            torch.cuda.synchronize()
-        finally:
-            lib.mme_attention_variant(0)
+        torch.cuda.synchronize()
     diff = (outs[0] - outs[30]).abs()
     print(f"hd-72 production grid: max |diff| {diff.max().item():.3g}, mean {diff.mean().item():.3g}")
     assert torch.isfinite(outs[0]).all()
@@ -380,9 +366,6 @@ def test_gemm_res_stats(cuda, M, N, K, shift):
 # including a ragged last block of rows.
 @pytest.mark.parametrize("M,N,K", [(4096, 1152, 1152), (3001, 1280, 512), (2000, 1024, 256)])
 def test_row_part_combine_lds_bit_identical(cuda, M, N, K):
-    import ctypes
-    lib = _lib.load()
-    lib.mme_gemm_variant.argtypes = [ctypes.c_int]
     g = torch.Generator(device="cuda").manual_seed(M + 3 * N + K)
     a = rnd(M, K, gen=g)
     w = rnd(N, K, scale=1 / math.sqrt(K), gen=g)
@@ -392,12 +375,9 @@ def test_row_part_combine_lds_bit_identical(cuda, M, N, K):
     for v in (-1, 48):
         st = torch.full((M, 2), float("nan"), dtype=torch.float32, device="cuda")
         part = torch.empty(M, N // 64, 2, dtype=torch.float32, device="cuda")
-        lib.mme_gemm_variant(v)
-        try:
+        with ops.kernel_forms(gemm=v):
             out = ops.gemm_res_stats(a, w, b, x.clone(), 1e-6, st, part)
-            torch.cuda.synchronize()
-        finally:
-            lib.mme_gemm_variant(-1)
+        torch.cuda.synchronize()
         res.append((out, st))
     assert torch.equal(res[0][0], res[1][0])
     assert torch.isfinite(res[0][1]).all()
@@ -415,9 +395,6 @@ def test_row_part_combine_lds_bit_identical(cuda, M, N, K):
                                        (3000, 1152, 1152, "resstats"), (3000, 576, 320, "resstats"),
                                        (2048, 704, 256, "resstats"), (3000, 448, 320, "resstats")])
 def test_gemm_pipe8_bit_identical_to_pipe6(cuda, M, N, K, epi):
-    import ctypes
-    lib = _lib.load()
-    lib.mme_gemm_variant.argtypes = [ctypes.c_int]
     g = torch.Generator(device="cuda").manual_seed(M + N + K)
     a = rnd(M, K, scale=2.0, gen=g) + 0.5
     w = rnd(N, K, scale=1 / math.sqrt(K), gen=g)
@@ -444,13 +421,9 @@ def test_gemm_pipe8_bit_identical_to_pipe6(cuda, M, N, K, epi):
         out = ops.gemm_res_stats(a, w, b, x.clone(), 1e-6, st, part)
         return out, st
 
-    try:
-        lib.mme_gemm_variant(-1)
-        new = run()
-        lib.mme_gemm_variant(47)
+    new = run()
+    with ops.kernel_forms(gemm=47):
         old = run()
-    finally:
-        lib.mme_gemm_variant(-1)
     torch.cuda.synchronize()
     for n_, o_ in zip(new, old):
         assert torch.equal(n_, o_), f"pipe8 differs from pipe6 ({epi}, {M}x{N}x{K})"
@@ -512,9 +485,6 @@ def test_im2col(cuda):
                                        (4096, 1152, 1152, "res"), (1000, 3456, 1152, "lnfold"),
                                        (1024, 1152, 4352, "bias"), (3000, 4352, 1152, "gelu")])
 def test_gemm_pipe9_bit_identical_to_pipe8(cuda, M, N, K, epi):
-    import ctypes
-    lib = _lib.load()
-    lib.mme_gemm_variant.argtypes = [ctypes.c_int]
     g = torch.Generator(device="cuda").manual_seed(M + 2 * N + K)
     a = rnd(M, K, scale=2.0, gen=g) + 0.5
     w = rnd(N, K, scale=1 / math.sqrt(K), gen=g)
@@ -534,12 +504,8 @@ def test_gemm_pipe9_bit_identical_to_pipe8(cuda, M, N, K, epi):
             return ops.gemm(a, w, b, residual=x)
         return ops.gemm_lnfold(a, fold, stats, act=_lib.ACT_GELU_TANH)
 
-    try:
-        lib.mme_gemm_variant(71)
+    with ops.kernel_forms(gemm=71):
         ref = run()
-        lib.mme_gemm_variant(-1)
-        new = run()
-    finally:
-        lib.mme_gemm_variant(-1)
+    new = run()
     torch.cuda.synchronize()
     assert torch.equal(new, ref), f"pipe9 differs from pipe8 ({epi}, {M}x{N}x{K})"

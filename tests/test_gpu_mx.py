@@ -201,9 +201,6 @@ def test_fp8_dfn5b_full_size_vs_oracle(cuda, monkeypatch):
 @pytest.mark.dev
 @pytest.mark.parametrize("M,N,K", [(1000, 3840, 1280), (777, 1280, 5120), (513, 256, 256), (300, 512, 384)])
 def test_gemm_mx9_bit_identical_to_mx(cuda, M, N, K):
-    import ctypes
-    lib = _lib.load()
-    lib.mme_gemm_mx_variant.argtypes = [ctypes.c_int]
     g = torch.Generator(device="cuda").manual_seed(M + N + 7 * K)
     a = mx.quantize(rnd(M, K, gen=g))
     w = mx.quantize(rnd(N, K, scale=1 / math.sqrt(K), gen=g))
@@ -218,12 +215,9 @@ def test_gemm_mx9_bit_identical_to_mx(cuda, M, N, K):
         t = mx.gemm(a, w, b, act=_lib.ACT_QUICK_GELU, out_mx=o)
         return y, x, t.q.clone(), t.scales.clone()
 
-    try:
-        old = run()
-        assert lib.mme_gemm_mx_variant(9) == 0
+    old = run()
+    with ops.kernel_forms(mx=9):
         new = run()
-    finally:
-        lib.mme_gemm_mx_variant(-1)
     torch.cuda.synchronize()
     for o_, n_, what in zip(old, new, ("bf16 + act", "residual", "mx8 values", "mx8 scales")):
         assert torch.equal(o_, n_), f"mx9 differs from the half-line kernel ({what}, {M}x{N}x{K})"
@@ -238,9 +232,6 @@ def test_gemm_mx9_bit_identical_to_mx(cuda, M, N, K):
                                          (129, 96, 192, "res"), (513, 256, 256, "bias"), (300, 512, 320, "res"),
                                          (257, 768, 448, "mx_out"), (600, 1024, 512, "bias"), (64, 256, 576, "bias")])
 def test_gemm_mx_wave_epilogue_bit_identical(cuda, M, N, K, kind):
-    import ctypes
-    lib = _lib.load()
-    lib.mme_gemm_mx_variant.argtypes = [ctypes.c_int]
     g = torch.Generator(device="cuda").manual_seed(M + N + K)
     a = mx.quantize(rnd(M, K, gen=g))
     w = mx.quantize(rnd(N, K, scale=1 / math.sqrt(K), gen=g))
@@ -248,8 +239,7 @@ def test_gemm_mx_wave_epilogue_bit_identical(cuda, M, N, K, kind):
     res0 = rnd(M, N, gen=g)
     outs = []
     for v in (0, 2, 3, -1):  # round-2 form, + per-wave epilogue, + single-wave scale DMA, production (mx10)
-        assert lib.mme_gemm_mx_variant(v) == 0
-        try:
+        with ops.kernel_forms(mx=v):
             if kind == "mx_out":
                 o = mx.MXTensor.empty(M, N, "cuda")
                 mx.gemm(a, w, bias, act=_lib.ACT_QUICK_GELU, out_mx=o)
@@ -258,9 +248,7 @@ def test_gemm_mx_wave_epilogue_bit_identical(cuda, M, N, K, kind):
                 x = res0.clone()
                 y = mx.gemm(a, w, bias, residual=x if kind == "res" else None, out=x)
                 outs.append((y.clone(),))
-            torch.cuda.synchronize()
-        finally:
-            lib.mme_gemm_mx_variant(-1)
+        torch.cuda.synchronize()
     for o in outs[1:]:
         for p, q in zip(outs[0], o):
             assert torch.equal(p, q), f"per-wave mx epilogue / single-wave scale DMA differs ({kind}, {M}x{N}x{K})"
