@@ -197,7 +197,42 @@ def encoder_parity(spec, imgs_u8, cap_ids, dev_img, dev_txt, bar: float = 0.999)
             "seconds": round(time.time() - t0, 2)}
 
 
-def colpali_parity(tables, scores, caps_per_image: int = 5, n_t2i: int = 50, n_i2t: int = 10, n_sym: int = 50):
+def colpali_encoder_parity(imgs_u8, t2i_caps, tables, img_batch: int = 32, bar_min: float = 0.995,
+                           bar_mean: float = 0.999):
+    """ColPali encoder parity of the job (checker; after the timed region): the job's own images at the
+    first and last rows of its first execution batch and the job's last image, and its first and last
+    T2I queries (each in its reference batch of 4, left-padded as process_queries, main.py:420-425),
+    encoded by the fp32 oracle (oracle/colpali_encoder.py) with the job's weights, against the
+    device's multi-vectors: per-token cosine (mean >= 0.999; min >= 0.995)."""
+    sys.path.insert(0, ROOT)
+    from oracle import colpali_encoder as oc
+    from mme.colpali_encoder import random_state_dict
+    from mme.config import COLPALI
+    t0 = time.time()
+    spec = COLPALI["ColPali-v1.3"]
+    sd = {k: v.float().cpu() for k, v in random_state_dict(spec, seed=0, device="cuda").items()}
+    n = imgs_u8.shape[0]
+    img_rows = sorted({0, min(img_batch, n) - 1, n - 1})
+    D, dl, Qt, qtl = (tables[k] for k in ("D", "dl", "Qt", "qtl"))
+    cos = lambda a, b: torch.nn.functional.cosine_similarity(a.float().cpu(), b.float(), dim=-1)
+    res = {"image_rows": img_rows, "query_rows": sorted({0, len(t2i_caps) - 1})}
+    ci = [cos(D[i, : int(dl[i])], oc.encode_image(spec, sd, imgs_u8[i].cpu().numpy())) for i in img_rows]
+    cq = []
+    for i in res["query_rows"]:
+        lo = i // spec.batch_size * spec.batch_size
+        ref = oc.encode_query_batch(spec, sd, t2i_caps[lo:lo + spec.batch_size])[i - lo]
+        cq.append(cos(Qt[i, : int(qtl[i])], ref))
+    c = torch.cat(ci + cq)
+    res.update(img_cos_min=round(float(torch.cat(ci).min()), 6), query_cos_min=round(float(torch.cat(cq).min()), 6),
+               cos_mean=round(float(c.mean()), 6), bar_min=bar_min, bar_mean=bar_mean,
+               ok=bool(c.min() >= bar_min and c.mean() >= bar_mean),
+               checker="oracle/colpali_encoder.py fp32 on the job's own images / T2I queries and weights",
+               seconds=round(time.time() - t0, 2))
+    return res
+
+
+def colpali_parity(tables, scores, caps_per_image: int = 5, n_t2i: int = 50, n_i2t: int = 10, n_sym: int = 50,
+                   imgs_u8=None, t2i_caps=None):
     """MaxSim parity of the ColPali job (checker; runs after the timed region): sampled query rows
     of the job's own multi-vector tables re-scored on the host by the oracle's restatement of the
     reference's colpali chunk loop (oracle/maxsim.py: pad_sequence + bf16 einsum / max / sum per
@@ -262,6 +297,7 @@ def colpali_parity(tables, scores, caps_per_image: int = 5, n_t2i: int = 50, n_i
         ok &= r["scores_max_ulp"] <= 1 and bool((same_idx | ~same_top).all()) and bool((same_hit | ~same_top).all())
         out[name] = r
     return {"parity_ok": bool(ok), "rows": out,
+            "encoders": colpali_encoder_parity(imgs_u8, t2i_caps, tables) if imgs_u8 is not None else None,
             "rule": "scores <= 1 bf16 ulp apart; rows whose top-11 agree: top-10 in torch.topk's CPU order and "
                     "hit/miss at k = 1, 5, 10 identical",
             "checker": "oracle/maxsim.py chunk loop (reference main.py:451-470) on the job's own multi-vectors, host",
@@ -443,7 +479,7 @@ def main_colpali(args, rank, world, dev):
     out["process_group"] = ({"backend": dist.get_backend(), "ranks": dist.get_world_size(),
                              "same_device": bool(args.same_device)} if world > 1 else None)
     if rank == 0 and world == 1 and not args.no_parity:
-        out["parity"] = colpali_parity(last["tables"], last["scores"], caps)
+        out["parity"] = colpali_parity(last["tables"], last["scores"], caps, imgs_u8=my_imgs, t2i_caps=my_t2i)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         sys.path.insert(0, ROOT)
         out["cpu_baseline"] = cpu_baseline_colpali(spec, args.cpu_seconds, n, caps)

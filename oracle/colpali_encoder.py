@@ -111,6 +111,35 @@ def forward(spec, sd: Dict[str, torch.Tensor], input_ids: torch.Tensor, attentio
     return e
 
 
+@torch.no_grad()
+def encode_query_batch(spec, sd: Dict[str, torch.Tensor], captions) -> list:
+    """One reference batch of ColPali queries, as encode_data's colpali branch runs it
+    (main.py:420-425): processor.process_queries(batch) left-pads the batch to its longest
+    query (TF:models/gemma/tokenization_gemma.py:55, padding_side left), model(**inputs)
+    returns [B, L_b, 128] with the padded rows zeroed; each item's valid rows are its last
+    len rows. Returns per item the valid [len, 128] rows."""
+    rows = [list(spec.query_tokens(c)) for c in captions]
+    L = max(len(r) for r in rows)
+    ids = torch.full((len(rows), L), spec.pad_id, dtype=torch.int64)
+    mask = torch.zeros((len(rows), L), dtype=torch.int64)
+    for i, r in enumerate(rows):
+        ids[i, L - len(r):] = torch.tensor(r)
+        mask[i, L - len(r):] = 1
+    e = forward(spec, sd, ids, mask)
+    return [e[i, L - len(r):] for i, r in enumerate(rows)]
+
+
+@torch.no_grad()
+def encode_image(spec, sd: Dict[str, torch.Tensor], image_u8) -> torch.Tensor:
+    """One image through processor.process_images + model (main.py:402-405): the PIL-exact
+    resize / normalise (oracle/pil_bicubic.py), then [L_img, 128]."""
+    from . import pil_bicubic
+    ip = spec.image_proc
+    pv = torch.from_numpy(pil_bicubic.normalize(pil_bicubic.preprocess_u8(image_u8, ip.size, ip.mode),
+                                                ip.mean, ip.std))[None]
+    return forward(spec, sd, torch.tensor([spec.image_tokens]), None, pv)[0]
+
+
 def flops_per_token(spec, L: int) -> float:
     """Algorithmic FLOPs of one decoder token (GEMMs + attention over L keys)."""
     t = spec.text
