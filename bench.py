@@ -95,6 +95,48 @@ def synth_inputs(spec, n, caps, device):
     return imgs, ids.to(torch.int64)
 
 
+HBM_FAMILIES = {  # KernelTimer family -> the kernel(s) behind it (rocprof names)
+    "preprocess": "resample_patch_p_kernel", "rowstats": "rowstats_kernel", "layernorm": "layernorm_kernel",
+    "l2norm": "l2norm_kernel", "attention_short": "attn_short_kernel"}
+
+
+def load_traffic(model, n, img_batch, txt_batch, fp8):
+    """profiles/hbm_traffic.json (tools/pmc_job.sh: rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE over one job,
+    tools/pmc_summary.py) when it was measured on this configuration, else None."""
+    path = os.path.join(ROOT, "profiles", "hbm_traffic.json")
+    try:
+        d = json.load(open(path))
+    except (OSError, ValueError):
+        return None
+    want = {"model": model, "n_images": n, "img_batch": img_batch, "txt_batch": txt_batch, "fp8": bool(fp8)}
+    for entry in d.get("configs", []):
+        if all(entry.get("config", {}).get(k) == v for k, v in want.items()):
+            return dict(entry["families"], _source=f"profiles/hbm_traffic.json ({entry.get('build', '?')})")
+    return None
+
+
+def hbm_rooflines(kt, dt, pmc, steps):
+    """HBM-bound kernels of the job: algorithmic bytes per launch / HIP-event time of the
+    timed launches vs the 8 TB/s peak, and the PMC-measured bytes per launch where the pass matches."""
+    out = {}
+    for fam, kname in HBM_FAMILIES.items():
+        if fam not in kt:
+            continue
+        k = kt[fam]
+        gbs = k["bytes"] / (k["ms"] / 1e3) / 1e9
+        r = {"kernel": kname, "launches_per_job": k["launches"] // max(steps, 1),
+             "avg_launch_ms": round(k["ms"] / k["launches"], 4),
+             "algorithmic_bytes_per_launch": round(k["bytes"] / k["launches"]),
+             "achieved_GBs": round(gbs, 1), "peak_GBs": HBM_PEAK_GBS, "frac": round(gbs / HBM_PEAK_GBS, 4),
+             "share_of_step_time": round(k["ms"] / 1e3 / dt, 4)}
+        m = (pmc or {}).get(kname)
+        if m and m.get("launches") == r["launches_per_job"]:
+            r["traffic"] = round(m["hbm_bytes_per_launch"])
+            r["traffic_GBs"] = round(m["hbm_bytes_per_launch"] / (r["avg_launch_ms"] / 1e3) / 1e9, 1)
+        out[fam] = r
+    return out
+
+
 def cpu_baseline(spec, seconds: float, tables=None, caps_per_image: int = 5):
     """The oracle's bf16 PyTorch-CPU restatement of the reference encoders (validated against the
     reference's own main.encode_data in profiles/r02_cpu_baseline_check.json) at the reference's
@@ -626,17 +668,21 @@ def main():
             roofline["bf16_gemm_tflops"] = round(b["flops"] / (b["ms"] / 1e3) / 1e12, 1)
             roofline["bf16_gemm_share"] = round(b["ms"] / 1e3 / dt, 3)
         # HBM bytes per launch from the rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes (tools/pmc_gemm.sh,
-        # gfx950-corrected by tools/pmc_summary.py) of the same launch shapes
-        pmc = os.path.join(ROOT, "profiles", "gemm_traffic.json")
-        if os.path.exists(pmc) and not args.fp8 and args.model == "SigLIP-400M":  # measured on SigLIP's shapes
-            try:
-                roofline["traffic"] = round(json.load(open(pmc))["mme_gemm"]["hbm_bytes_per_launch"])
-            except (KeyError, ValueError, TypeError):
-                pass
+        # gfx950-corrected by tools/pmc_summary.py) over one job of THIS geometry: used only when the pass
+        # saw the same GEMM launch count per job as this run's timed steps (same batches, same mix)
+        pmc = load_traffic(args.model, n, args.img_batch, args.txt_batch, args.fp8)
+        per_job = g["launches"] // max(args.steps, 1)
+        if pmc and pmc.get(fam, {}).get("launches") == per_job:
+            roofline["traffic"] = round(pmc[fam]["hbm_bytes_per_launch"])
+            roofline["traffic_source"] = pmc["_source"]
+        elif pmc:
+            roofline["traffic_note"] = (f"{pmc['_source']} holds {pmc.get(fam, {}).get('launches')} {fam} launches "
+                                        f"per job, this run {per_job}: not the same launch mix, not reported")
         if "attention" in kt:
             a = kt["attention"]
             roofline["attention_tflops"] = round(a["flops"] / (a["ms"] / 1e3) / 1e12, 1)
             roofline["attention_share"] = round(a["ms"] / 1e3 / dt, 3)
+        roofline["hbm_kernels"] = hbm_rooflines(kt, dt, pmc, args.steps)
 
     value = n * args.steps / dt
     out = {

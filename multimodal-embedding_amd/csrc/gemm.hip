@@ -902,18 +902,26 @@ int launch_pipe6(const GemmArgs& a, hipStream_t s) {
 }
 
 // Per-wave epilogue (pipe8 WEPI): each wave stages ONLY its own 128 x 64 sub-tile in its
-// own 18 KiB LDS region (row pitch 144 B), reads it back as 16-B row chunks (8 rows x 128 B
-// per store instruction) and stores it -- no workgroup barrier, so the early wave row's
-// epilogue runs beside the late row's last MFMAs and each wave leaves as soon as it is done.
-// Same arithmetic as gemm_epilogue_lds step for step (bit-identical outputs and row
-// statistics: a wave's 64 columns of a row are one 64-column slice).
-template <class C, int ACT>
+// own LDS region, reads it back as 16-B row chunks (8 rows x 128 B per store instruction) and
+// stores it -- no workgroup barrier, so the early wave row's epilogue runs beside the late row's
+// last MFMAs and each wave leaves as soon as it is done. Same arithmetic as gemm_epilogue_lds
+// step for step (bit-identical outputs and row statistics: a wave's 64 columns of a row are one
+// 64-column slice).
+// Staging layout (round 4, SWZ): 128-B rows (16 KiB per wave), 16-B chunk c of row r stored at
+// chunk c ^ (r & 7) with its two 8-B halves swapped when bit 3 of r is set. The 8-B staging
+// writes (ds_write_b64: 16 contiguous lanes = rows li = 0..15 of one column quad per LDS cycle,
+// banks (a/4) mod 32) then cover all 32 banks once, and the 16-B read-back (ds_read_b128, the
+// gfx950 lane groups {0-3,12-15,20-27}, ..., banks (a/4) mod 64) hits 16 distinct slots per
+// group: conflict-free both ways. The round-2/3 layout (pitch 144 B, 18 KiB) was 2-way on both
+// (rows li and li + 8 share banks for the writes; rows r and r + 1 for the reads): 19 M
+// SQ_LDS_BANK_CONFLICT cycles per fc1 launch (profiles/r03_v12_pmc_gemm_util_fc1.json).
+template <class C, int ACT, bool SWZ = true>
 __device__ __forceinline__ void gemm_epilogue_wave(const GemmArgs& p, char* lds, f32x4 (&acc)[C::FM][C::FN], int m0,
                                                    int n0, int wave, int wm, int wn, int g, int li, int lane) {
     static_assert(C::TM == 128 && C::TN == 64 && C::FM == 8 && C::FN == 4, "per-wave epilogue: 128 x 64 wave tiles");
     constexpr bool GLU = ACT == MME_ACT_GEGLU_TANH;
     constexpr int RACT = GLU ? MME_ACT_NONE : ACT;
-    constexpr int PITCH = 144, REGION = 128 * PITCH;
+    constexpr int PITCH = SWZ ? 128 : 144, REGION = 128 * PITCH;
     char* reg = lds + wave * REGION;
     const int rm0 = m0 + wm * C::TM, cn0 = n0 + wn * C::TN;  // this wave's sub-tile origin
     const int rr = lane >> 3, cc = lane & 7;                 // store phase: row rr of 8, 16-B chunk cc
@@ -972,7 +980,11 @@ __device__ __forceinline__ void gemm_epilogue_wave(const GemmArgs& p, char* lds,
                     o[r + 1] = f2bf(y.y);
                 }
             }
-            *reinterpret_cast<bf16x4*>(reg + (i * 16 + li) * PITCH + nl * 2) = o;
+            if constexpr (SWZ)  // chunk 2 j + g / 2 ^ (row & 7), half (g & 1) ^ (row >> 3 & 1); row & 15 = li
+                *reinterpret_cast<bf16x4*>(reg + (i * 16 + li) * PITCH + (((2 * j + (g >> 1)) ^ (li & 7)) << 4) +
+                                           (((g & 1) ^ (li >> 3)) << 3)) = o;
+            else
+                *reinterpret_cast<bf16x4*>(reg + (i * 16 + li) * PITCH + nl * 2) = o;
         }
     }
     // the wave's own LDS writes precede its reads (LDS executes one wave's instructions in order)
@@ -981,7 +993,13 @@ __device__ __forceinline__ void gemm_epilogue_wave(const GemmArgs& p, char* lds,
     for (int q = 0; q < 16; ++q) {
         const int row = q * 8 + rr;
         const int gr = rm0 + row, gc = cn0 + cc * 8;
-        const u16x8 v = *reinterpret_cast<const u16x8*>(reg + row * PITCH + cc * 16);
+        u16x8 v;
+        if constexpr (SWZ) {  // row & 7 = rr; bit 3 of the row = q & 1 (a static half swap)
+            const u16x8 w = *reinterpret_cast<const u16x8*>(reg + row * PITCH + ((cc ^ rr) << 4));
+            v = (q & 1) ? u16x8{w[4], w[5], w[6], w[7], w[0], w[1], w[2], w[3]} : w;
+        } else {
+            v = *reinterpret_cast<const u16x8*>(reg + row * PITCH + cc * 16);
+        }
         if (gr >= p.M || gc >= p.N) continue;
         if (GLU) {
             u16x4 o;
@@ -1201,7 +1219,7 @@ __device__ __forceinline__ void dma4(unsigned m0base, const unsigned (&voff)[4],
 // PRIO (dev variants 81 / 82): 0 = s_setprio 1 around every compute phase (production);
 // 1 = static priority 1 for the late wave row, no per-phase flips (MI355X_MICROARCH.md, two waves
 // per SIMD, item 4); 2 = no priority changes.
-template <class C, int ACT, bool LATE, int PRIO = 0>
+template <class C, int ACT, bool LATE, int PRIO = 0, bool ESWZ = true>
 __device__ __forceinline__ void pipe9_tile(const GemmArgs& p, char* lds, const int m0, const int n0, const int wave) {
     static_assert(C::BM == 256 && C::BN == 256 && C::FN == 4 && C::FM == 8 && C::NW == 8, "pipe9: 256 x 256, 8 waves");
     constexpr int UNIT = 32768;
@@ -1321,10 +1339,11 @@ __device__ __forceinline__ void pipe9_tile(const GemmArgs& p, char* lds, const i
     stage(sa2, true, false, 0, false);
     stage(sa1, false, false, -1, true);
     vm_wait<0>();
-    gemm_epilogue_wave<C, ACT>(p, lds, acc, m0, n0, wave, wm, wn, g, li, lane);
+    gemm_epilogue_wave<C, ACT, ESWZ>(p, lds, acc, m0, n0, wave, wm, wn, g, li, lane);
 }
 
-template <class C, int GROUP_M, int ACT, bool SPLIT, int PRIO = 0>
+// ESWZ: the conflict-free staging layout of gemm_epilogue_wave (round 4); false = pitch 144 (dev form 84)
+template <class C, int GROUP_M, int ACT, bool SPLIT, int PRIO = 0, bool ESWZ = true>
 __global__ __launch_bounds__(C::NT, 2) void gemm_pipe9_kernel(GemmArgs p) {
     __shared__ __attribute__((aligned(16))) char lds[5 * 32768];
     const int nbm = (p.M + C::BM - 1) / C::BM;
@@ -1344,9 +1363,9 @@ __global__ __launch_bounds__(C::NT, 2) void gemm_pipe9_kernel(GemmArgs p) {
     }
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     if (wave >= C::NW / 2)
-        pipe9_tile<C, ACT, true, PRIO>(p, lds, m0, n0, wave);
+        pipe9_tile<C, ACT, true, PRIO, ESWZ>(p, lds, m0, n0, wave);
     else
-        pipe9_tile<C, ACT, false, PRIO>(p, lds, m0, n0, wave);
+        pipe9_tile<C, ACT, false, PRIO, ESWZ>(p, lds, m0, n0, wave);
 }
 
 template <class C, int GROUP_M, int ACT, int DIAG = 0, bool SPLIT = false, bool WEPI = false>
@@ -1434,25 +1453,25 @@ int launch_pipe8(const GemmArgs& a, hipStream_t s) {
     return mme_check_launch("mme_gemm");
 }
 
-template <class C, int GROUP_M, bool SPLIT, int PRIO = 0>
+template <class C, int GROUP_M, bool SPLIT, int PRIO = 0, bool ESWZ = true>
 int launch_pipe9(const GemmArgs& a, hipStream_t s) {
     const int nbm = (a.M + C::BM - 1) / C::BM, nbn = (a.N + C::BN - 1) / C::BN;
     const dim3 grid(SPLIT ? split_tiles(nbm, a.N / C::BN) : nbm * nbn), block(C::NT);
     switch (a.act) {
         case MME_ACT_GELU_TANH:
-            hipLaunchKernelGGL((gemm_pipe9_kernel<C, GROUP_M, MME_ACT_GELU_TANH, SPLIT, PRIO>), grid, block, 0, s, a);
+            hipLaunchKernelGGL((gemm_pipe9_kernel<C, GROUP_M, MME_ACT_GELU_TANH, SPLIT, PRIO, ESWZ>), grid, block, 0, s, a);
             break;
         case MME_ACT_QUICK_GELU:
-            hipLaunchKernelGGL((gemm_pipe9_kernel<C, GROUP_M, MME_ACT_QUICK_GELU, SPLIT, PRIO>), grid, block, 0, s, a);
+            hipLaunchKernelGGL((gemm_pipe9_kernel<C, GROUP_M, MME_ACT_QUICK_GELU, SPLIT, PRIO, ESWZ>), grid, block, 0, s, a);
             break;
         case MME_ACT_GELU_ERF:
-            hipLaunchKernelGGL((gemm_pipe9_kernel<C, GROUP_M, MME_ACT_GELU_ERF, SPLIT, PRIO>), grid, block, 0, s, a);
+            hipLaunchKernelGGL((gemm_pipe9_kernel<C, GROUP_M, MME_ACT_GELU_ERF, SPLIT, PRIO, ESWZ>), grid, block, 0, s, a);
             break;
         case MME_ACT_GEGLU_TANH:
-            hipLaunchKernelGGL((gemm_pipe9_kernel<C, GROUP_M, MME_ACT_GEGLU_TANH, SPLIT, PRIO>), grid, block, 0, s, a);
+            hipLaunchKernelGGL((gemm_pipe9_kernel<C, GROUP_M, MME_ACT_GEGLU_TANH, SPLIT, PRIO, ESWZ>), grid, block, 0, s, a);
             break;
         default:
-            hipLaunchKernelGGL((gemm_pipe9_kernel<C, GROUP_M, MME_ACT_NONE, SPLIT, PRIO>), grid, block, 0, s, a);
+            hipLaunchKernelGGL((gemm_pipe9_kernel<C, GROUP_M, MME_ACT_NONE, SPLIT, PRIO, ESWZ>), grid, block, 0, s, a);
             break;
     }
     return mme_check_launch("mme_gemm");
@@ -2300,6 +2319,10 @@ int gemm_dispatch(GemmArgs a, int variant, hipStream_t s) {
             if (variant == 81)
                 return N % 256 == 128 ? launch_pipe9<Pipe256, 4, true, 1>(a, s) : launch_pipe9<Pipe256, 4, false, 1>(a, s);
             return N % 256 == 128 ? launch_pipe9<Pipe256, 4, true, 2>(a, s) : launch_pipe9<Pipe256, 4, false, 2>(a, s);
+        case 84:  // dev: pipe9 with the round-2/3 epilogue staging (pitch 144 B: 2-way LDS bank conflicts)
+            if (!pipe8_ok(a)) break;
+            if (N % 256 == 128) return launch_pipe9<Pipe256, 4, true, 0, false>(a, s);
+            return launch_pipe9<Pipe256, 4, false, 0, false>(a, s);
         case 83:  // dev: pipe9 with 8-row tile bands
             if (!pipe8_ok(a)) break;
             if (N % 256 == 128) return launch_pipe9<Pipe256, 8, true>(a, s);

@@ -247,11 +247,15 @@ __device__ __forceinline__ void mx_dma1(unsigned m0base, unsigned voff, i32x4v r
 // 16-B row chunks and stores it (bf16, + residual) or re-quantises it to mx8 -- no workgroup barrier,
 // so the early wave row's epilogue runs beside the late row's last MFMAs. Same arithmetic as the
 // whole-tile epilogue of gemm_mx_kernel (bit-identical outputs).
+// Staging layout (round 4, SWZ; the bf16 kernels' gemm_epilogue_wave has the reasoning): 128-B rows,
+// 16-B chunk c of row r at chunk c ^ (r & 7), its 8-B halves swapped when bit 3 of r is set --
+// conflict-free ds_write_b64 staging (16 contiguous lanes = rows r32 0..15) and ds_read_b128
+// read-back; SWZ = false: the round-3 pitch-144 layout (2-way on both; dev form 4).
 constexpr int MXW_PITCH = 144, MXW_LDS = 8 * 128 * MXW_PITCH;
-template <int ACT>
+template <int ACT, bool SWZ = true>
 __device__ __forceinline__ void mx_epilogue_wave(const MxArgs& p, char* lds, f32x16 (&acc)[4][2], int m0, int n0,
                                                  int wave, int lane) {
-    constexpr int TM = 128, TN = 64, MX9_PITCH = MXW_PITCH;
+    constexpr int TM = 128, TN = 64, MX9_PITCH = SWZ ? 128 : MXW_PITCH;
     const int wm = wave / 4, wn = wave % 4;
     const int h = lane >> 5, r32 = lane & 31;
     // lane (r32, h) holds row i*32 + r32, columns j*32 + 8q + 4h + (0..3)
@@ -272,17 +276,29 @@ __device__ __forceinline__ void mx_epilogue_wave(const MxArgs& p, char* lds, f32
                 bf16x4 o;
 #pragma unroll
                 for (int r = 0; r < 4; ++r) o[r] = f2bf(apply_act(acc[i][j][4 * qd + r] + bv[r], ACT));
-                *reinterpret_cast<bf16x4*>(reg + (i * 32 + r32) * MX9_PITCH + nl * 2) = o;
+                if constexpr (SWZ)  // chunk 4 j + qd ^ (row & 7), half h ^ (row >> 3 & 1); row & 31 = r32
+                    *reinterpret_cast<bf16x4*>(reg + (i * 32 + r32) * MX9_PITCH + (((4 * j + qd) ^ (r32 & 7)) << 4) +
+                                               ((h ^ ((r32 >> 3) & 1)) << 3)) = o;
+                else
+                    *reinterpret_cast<bf16x4*>(reg + (i * 32 + r32) * MX9_PITCH + nl * 2) = o;
             }
         }
     // the wave's own LDS writes precede its reads
     const int rr = lane >> 3, cc = lane & 7;
+    auto rd = [&](int q, int row) __attribute__((always_inline)) -> u16x8 {
+        if constexpr (SWZ) {  // row & 7 = rr, bit 3 of the row = q & 1
+            const u16x8 w = *reinterpret_cast<const u16x8*>(reg + row * MX9_PITCH + ((cc ^ rr) << 4));
+            return (q & 1) ? u16x8{w[4], w[5], w[6], w[7], w[0], w[1], w[2], w[3]} : w;
+        } else {
+            return *reinterpret_cast<const u16x8*>(reg + row * MX9_PITCH + cc * 16);
+        }
+    };
     if (!p.out_mx) {
         bf16* Cout = reinterpret_cast<bf16*>(p.C);
 #pragma unroll 4
         for (int q = 0; q < 16; ++q) {
             const int row = q * 8 + rr, gr = rm0 + row, gc = cn0 + cc * 8;
-            const u16x8 v = *reinterpret_cast<const u16x8*>(reg + row * MX9_PITCH + cc * 16);
+            const u16x8 v = rd(q, row);
             if (gr >= p.M || gc >= p.N) continue;
             if (p.res) {
                 const int r2 = p.res_period ? gr % p.res_period : gr;
@@ -301,7 +317,7 @@ __device__ __forceinline__ void mx_epilogue_wave(const MxArgs& p, char* lds, f32
 #pragma unroll 4
         for (int q = 0; q < 16; ++q) {  // same trip count for every lane (shuffles)
             const int row = q * 8 + rr, gr = rm0 + row, gc = cn0 + cc * 8;
-            const u16x8 v = *reinterpret_cast<const u16x8*>(reg + row * MX9_PITCH + cc * 16);
+            const u16x8 v = rd(q, row);
             float f[8];
             float a = 0.f;
 #pragma unroll
@@ -539,7 +555,7 @@ __global__ __launch_bounds__(512, 2) void gemm_mx_kernel(MxArgs p) {
 //     and the K offset in soffset (one SGPR add per stage) instead of a 64-bit address per piece.
 // Needs K % 64 == 0, K >= 256 (4 stages) and operands < 4 GiB (32-bit offsets).
 // ---------------------------------------------------------------------------
-template <int ACT, bool LATE, bool SCW>
+template <int ACT, bool LATE, bool SCW, bool ESWZ = true>
 __device__ __forceinline__ void mx10_tile(const MxArgs& p, char* lds, const int m0, const int n0, const int wave) {
     using C = MxCfg;
     static_assert(C::PPW == 4 && C::NSTAGE == 4, "mx10: 4 data pieces per wave, 4-slot ring");
@@ -667,10 +683,10 @@ __device__ __forceinline__ void mx10_tile(const MxArgs& p, char* lds, const int 
     }
     // no LDS hazard: every wave's last fragment reads and DMA waits precede the barrier closing the
     // late row's last memory phase, which the early row passes before it writes its region
-    mx_epilogue_wave<ACT>(p, lds, acc, m0, n0, wave, lane);
+    mx_epilogue_wave<ACT, ESWZ>(p, lds, acc, m0, n0, wave, lane);
 }
 
-template <int GROUP_M, int ACT>
+template <int GROUP_M, int ACT, bool ESWZ = true>
 __global__ __launch_bounds__(512, 2) void gemm_mx10_kernel(MxArgs p) {
     using C = MxCfg;
     __shared__ __attribute__((aligned(16))) char lds[MXW_LDS > C::LDS ? MXW_LDS : C::LDS];
@@ -680,28 +696,28 @@ __global__ __launch_bounds__(512, 2) void gemm_mx10_kernel(MxArgs p) {
     tile_coords<GROUP_M>(tile, nbm, nbn, bm, bn);
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     if (wave == 0)
-        mx10_tile<ACT, false, true>(p, lds, bm * C::BM, bn * C::BN, wave);
+        mx10_tile<ACT, false, true, ESWZ>(p, lds, bm * C::BM, bn * C::BN, wave);
     else if (wave < 4)
-        mx10_tile<ACT, false, false>(p, lds, bm * C::BM, bn * C::BN, wave);
+        mx10_tile<ACT, false, false, ESWZ>(p, lds, bm * C::BM, bn * C::BN, wave);
     else
-        mx10_tile<ACT, true, false>(p, lds, bm * C::BM, bn * C::BN, wave);
+        mx10_tile<ACT, true, false, ESWZ>(p, lds, bm * C::BM, bn * C::BN, wave);
 }
 
-template <int GROUP_M>
+template <int GROUP_M, bool ESWZ = true>
 int launch_mx10(const MxArgs& a, hipStream_t s) {
     const dim3 grid(((a.M + 255) / 256) * ((a.N + 255) / 256)), block(512);
     switch (a.act) {
         case MME_ACT_GELU_TANH:
-            hipLaunchKernelGGL((gemm_mx10_kernel<GROUP_M, MME_ACT_GELU_TANH>), grid, block, 0, s, a);
+            hipLaunchKernelGGL((gemm_mx10_kernel<GROUP_M, MME_ACT_GELU_TANH, ESWZ>), grid, block, 0, s, a);
             break;
         case MME_ACT_QUICK_GELU:
-            hipLaunchKernelGGL((gemm_mx10_kernel<GROUP_M, MME_ACT_QUICK_GELU>), grid, block, 0, s, a);
+            hipLaunchKernelGGL((gemm_mx10_kernel<GROUP_M, MME_ACT_QUICK_GELU, ESWZ>), grid, block, 0, s, a);
             break;
         case MME_ACT_GELU_ERF:
-            hipLaunchKernelGGL((gemm_mx10_kernel<GROUP_M, MME_ACT_GELU_ERF>), grid, block, 0, s, a);
+            hipLaunchKernelGGL((gemm_mx10_kernel<GROUP_M, MME_ACT_GELU_ERF, ESWZ>), grid, block, 0, s, a);
             break;
         default:
-            hipLaunchKernelGGL((gemm_mx10_kernel<GROUP_M, MME_ACT_NONE>), grid, block, 0, s, a);
+            hipLaunchKernelGGL((gemm_mx10_kernel<GROUP_M, MME_ACT_NONE, ESWZ>), grid, block, 0, s, a);
             break;
     }
     return mme_check_launch("mme_gemm_mx");
@@ -902,7 +918,7 @@ inline int mx_default_form() { return -1; }
 #endif
 inline bool mx_form_ok(int v) {
 #ifdef MME_DEV
-    return v == -1 || v == 0 || v == 2 || v == 3 || v == 9;
+    return v == -1 || v == 0 || v == 2 || v == 3 || v == 4 || v == 9;
 #else
     return v == -1 || v == 0 || v == 2 || v == 3;
 #endif
@@ -1026,6 +1042,9 @@ int gemm_mx_entry(int form, const void* A, int lda, const void* sa, int sa_rows,
     // gemm_mx_kernel form with the same epilogue and scale wave. A/B forms: variant 0 = the round-2
     // kernel, 2 = its per-wave epilogue alone, 3 = + the scale wave (mx10's fallback).
     const bool mx10_ok = K >= 256 && (size_t)M * lda < (1ull << 32) && (size_t)N * ldb < (1ull << 32);
+#ifdef MME_DEV
+    if (form == 4 && mx10_ok) return launch_mx10<4, false>(a, as_stream(stream));  // dev: round-3 epilogue staging
+#endif
     if (form == 0) return launch_mx<4>(a, as_stream(stream));
     if (form == 2) return launch_mx<4, true>(a, as_stream(stream));
     if (form == 3 || !mx10_ok) return launch_mx<4, true, true>(a, as_stream(stream));

@@ -230,7 +230,9 @@ def rowstats(x: torch.Tensor, eps: float, *, d: Optional[int] = None,
         out = torch.empty(rows, 2, dtype=torch.float32, device=x.device)
     if out.dtype != torch.float32 or not out.is_contiguous() or out.numel() < 2 * rows:
         raise ValueError("rowstats: out must be contiguous fp32 [rows, 2]")
+    ev = KernelTimer.begin()
     call("mme_rowstats", x.data_ptr(), _rowmajor(x, "x"), rows, d, float(eps), out.data_ptr(), _stream())
+    KernelTimer.end(ev, "rowstats", 0.0, 2.0 * rows * d + 8.0 * rows)  # HBM-bound: rows read, 8 B per row out
     return out
 
 
@@ -284,8 +286,10 @@ def layernorm(x: torch.Tensor, gamma: torch.Tensor, beta: torch.Tensor, eps: flo
         out = torch.empty(rows, d, dtype=BF16, device=x.device)
     if rows_idx is not None and rows_idx.dtype != torch.int32:
         raise ValueError("layernorm: rows_idx must be int32")
+    ev = KernelTimer.begin()
     call("mme_layernorm", x.data_ptr(), _rowmajor(x, "x"), gamma.data_ptr(), beta.data_ptr(), out.data_ptr(),
          _rowmajor(out, "out"), rows, d, float(eps), _ptr(rows_idx), _stream())
+    KernelTimer.end(ev, "layernorm", 0.0, 4.0 * rows * d + 4.0 * d)  # rows in + out bf16, gamma / beta
     return out
 
 
@@ -295,7 +299,9 @@ def l2norm(x: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
     rows, d = x.shape
     if out is None:
         out = torch.empty(rows, d, dtype=BF16, device=x.device)
+    ev = KernelTimer.begin()
     call("mme_l2norm", x.data_ptr(), _rowmajor(x, "x"), out.data_ptr(), _rowmajor(out, "out"), rows, d, _stream())
+    KernelTimer.end(ev, "l2norm", 0.0, 4.0 * rows * d)
     return out
 
 
@@ -311,9 +317,11 @@ def attention(qkv: torch.Tensor, B: int, T: int, H: int, hd: int, *, seq_lens: O
         raise ValueError("attention: seq_lens must be int32 [B]")
     scale = hd ** -0.5 if scale is None else scale
     ev = KernelTimer.begin()
-    _call_form("mme_attention", "attention", qkv.data_ptr(), _rowmajor(qkv, "qkv"), out.data_ptr(), _rowmajor(out, "out"), B, T, H, hd,
-         _ptr(seq_lens), int(causal), float(scale), _stream())
-    KernelTimer.end(ev, "attention", 4.0 * B * H * T * T * hd * (0.5 if causal else 1.0))
+    _call_form("mme_attention", "attention", qkv.data_ptr(), _rowmajor(qkv, "qkv"), out.data_ptr(),
+               _rowmajor(out, "out"), B, T, H, hd, _ptr(seq_lens), int(causal), float(scale), _stream())
+    # T <= 64 (SigLIP text) runs attn_short_kernel: one key tile per (batch, head), HBM-bound (Q, K, V in, O out)
+    KernelTimer.end(ev, "attention_short" if T <= 64 else "attention",
+                    4.0 * B * H * T * T * hd * (0.5 if causal else 1.0), 8.0 * B * T * H * hd)
     return out
 
 
@@ -482,8 +490,12 @@ def preprocess_u8(imgs: torch.Tensor, *, resize: Sequence[int], crop: Sequence[i
     # mean/std are HOST float[3] (copied by value into the kernel arguments)
     mean_h = torch.tensor(list(mean), dtype=torch.float32)
     std_h = torch.tensor(list(std), dtype=torch.float32)
+    ev = KernelTimer.begin()
     call("mme_preprocess_u8", imgs.data_ptr(), n, H, W, rh, rw, top, left, S, mean_h.data_ptr(), std_h.data_ptr(),
          kind, patch, kpad, out.data_ptr(), ws.data_ptr(), wsb, _stream())
+    # algorithmic bytes: the u8 images in, the bf16 patches (3 p^2 of each kpad-wide row) / fp32 pixels out
+    out_b = n * (S // patch) ** 2 * 3 * patch * patch * 2.0 if patch else n * 3 * S * S * 4.0
+    KernelTimer.end(ev, "preprocess", 0.0, float(n * H * W * 3) + out_b)
     return out
 
 
