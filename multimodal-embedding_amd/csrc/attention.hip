@@ -2500,7 +2500,13 @@ bool launch_attn(int kind, const AttnArgs& a, int B, int T, int H, hipStream_t s
                           // for hd 80 in 9-wave blocks (ViT-H T 257: +2-4 %, profiles/r03_v11_attn_vith_ab.log)
         hipLaunchKernelGGL((attn_m32_kernel<HD, 9, 1, true, false, false, true>), dim3(cdiv(T, 288) * H * B),
                            dim3(576), 0, st, a);
-    else if (kind == 62) {  // attn_hyb_kernel skipping a tile's second key block when it lies past the keys,
+    else if (kind == 58) {  // attn_hyb_kernel without the skip (round 2's production form): the bit-identity
+                            // reference of kind 62 (tests/test_gpu_kernels.py::test_attention_skip_bit_identical)
+        if constexpr (HD != 64)
+            hipLaunchKernelGGL((attn_hyb_kernel<HD, 8, 4, true>), dim3(cdiv(T, 256) * H * B), dim3(512), 0, st, a);
+        else
+            hipLaunchKernelGGL((attn_m32_kernel<HD, 8, 1, true>), dim3(cdiv(T, 256) * H * B), dim3(512), 0, st, a);
+    } else if (kind == 62) {  // attn_hyb_kernel skipping a tile's second key block when it lies past the keys,
                             // literal-zero QK^T starts (since round 3: +0.5-0.7 %, bit-identical,
                             // profiles/r03_v18_attn_bufdma_literal_zero_ab.log): production for hd 72
         if constexpr (HD != 64)
@@ -2625,12 +2631,10 @@ bool launch_attn_dev(int kind, const AttnArgs& a, int B, int T, int H, hipStream
         hipLaunchKernelGGL((attn_m32_kernel<HD, 8, 4, true, false, true>), dim3(cdiv(T, 256) * H * B), dim3(512), 0, st, a);
     else if (kind == 57)  // dev: PF, 9 waves, 3 waves / SIMD
         hipLaunchKernelGGL((attn_m32_kernel<HD, 9, 3, true, false, true>), dim3(cdiv(T, 288) * H * B), dim3(576), 0, st, a);
-    else if (kind == 58 || kind == 59 || kind == 60 || kind == 61) {  // attn_hyb_kernel (hd 72 / 80; hd 64: kind 38);
-                                                                      // kind 58 is production for hd 72
+    else if (kind == 59 || kind == 60 || kind == 61) {  // attn_hyb_kernel (hd 72 / 80; hd 64: kind 38);
+                                                        // kind 58 (production launch_attn) is the 8-wave, 4 waves / SIMD form
         if constexpr (HD != 64) {
-            if (kind == 58)  // 4 waves / SIMD (<= 128 VGPRs)
-                hipLaunchKernelGGL((attn_hyb_kernel<HD, 8, 4, true>), dim3(cdiv(T, 256) * H * B), dim3(512), 0, st, a);
-            else if (kind == 59)  // 12 waves, 3 waves / SIMD
+            if (kind == 59)  // 12 waves, 3 waves / SIMD
                 hipLaunchKernelGGL((attn_hyb_kernel<HD, 12, 1, true>), dim3(cdiv(T, 384) * H * B), dim3(768), 0, st, a);
             else if (kind == 60)  // 8 waves, no register cap (129 VGPRs: 3 waves / SIMD)
                 hipLaunchKernelGGL((attn_hyb_kernel<HD, 8, 1, true>), dim3(cdiv(T, 256) * H * B), dim3(512), 0, st, a);
@@ -2639,6 +2643,10 @@ bool launch_attn_dev(int kind, const AttnArgs& a, int B, int T, int H, hipStream
         } else {
             hipLaunchKernelGGL((attn_m32_kernel<HD, 8, 1, true>), dim3(cdiv(T, 256) * H * B), dim3(512), 0, st, a);
         }
+    } else if (kind == 64) {  // dev: kind 38 (8-wave attn_m32_kernel) with the last-tile skip (round 3: 18 % slower
+                              // at DFN5B T 730; the pair whose rare 1-ulp difference round 3 recorded)
+        hipLaunchKernelGGL((attn_m32_kernel<HD, 8, 1, true, false, false, true>), dim3(cdiv(T, 256) * H * B), dim3(512),
+                           0, st, a);
     } else if (kind == 63) {  // dev: kind 62 as in round 2 (the skipped block's fill and the accumulator
                               // init as per-tile register moves)
         if constexpr (HD != 64)
