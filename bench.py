@@ -189,6 +189,7 @@ def retrieval_parity(tables, metrics, caps_per_image: int = 5):
     re-selected in torch.topk's CPU order) vs the oracle (numpy fp32 matmul + torch.topk's order,
     oracle/retrieval.py restating main.py:471-473 and 331-378), row by row; the job's device recall
     vs the oracle's recall of the same tables (one selection per k, as compute_metrics_detailed)."""
+    import numpy as np
     sys.path.insert(0, ROOT)
     from oracle import retrieval as R
     from mme.retrieval import rank_rows
@@ -204,7 +205,9 @@ def retrieval_parity(tables, metrics, caps_per_image: int = 5):
         s = R.scores(host[qk], host[dk])
         ridx, _ = R.topk(s, k)
         _, rsc = R.topk(s, k + 1)
-        same, near = R.compare_topk(ranked.idx.cpu().numpy(), ridx, rsc)
+        tied = np.zeros(len(ridx), bool)
+        tied[ranked.tie_rows.cpu().numpy()] = True
+        same, near = R.compare_topk(ranked.idx.cpu().numpy(), ridx, rsc, exact_rows=tied)
         rows[name] = {"rows_identical": f"{int(same.sum())}/{len(same)}", "near_tie_rows": int(near.sum()),
                       "decisive_rows_differing": int((~same & ~near).sum()),
                       "exact_tie_rows_torch_order": int(ranked.tie_rows.numel())}
@@ -212,8 +215,9 @@ def retrieval_parity(tables, metrics, caps_per_image: int = 5):
             ref_metrics[f"{name}_R@{kr}"] = 100.0 * h / n
     return {"recall_identical": all(ref_metrics[k] == metrics[k] for k in ref_metrics),
             "oracle_recall": {k: round(v, 2) for k, v in ref_metrics.items()}, "rows": rows,
-            "near_tie_rule": "unequal neighbouring oracle scores among the top 11 within 1e-5*|s1|; exact ties "
-                             "are not exempt (torch.topk's order, replayed on both sides)",
+            "near_tie_rule": "neighbouring oracle scores among the top 11 within 1e-5*|s1|; exact ties are not "
+                             "exempt on rows the device finds tied too (torch.topk's order, replayed on both "
+                             "sides), an oracle-only exact tie is a near tie",
             "checker": "oracle/retrieval.py on the job's own embeddings (numpy fp32 + torch.topk order, host)",
             "seconds": round(time.time() - t0, 2)}
 

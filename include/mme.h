@@ -295,8 +295,10 @@ int mme_maxsim(const void* Q, const int32_t* q_lens, int nq, int Lq, const void*
  * BASELINE.json configs[4]; the reference runs the same CLIP layers in bf16,
  * TF:models/clip/modeling_clip.py CLIPAttention q/k/v + CLIPMLP fc1/fc2).
  * mx8 tensor: values u8 [rows][k] e4m3fn (row stride ld bytes) + E8M0 scale
- * bytes [k/32][rows_pad] (block-major planes, rows_pad % 256 == 0);
- * element (r,c) = e4m3(q[r][c]) * 2^(S[c/32][r] - 127). Block rule: absmax a,
+ * bytes [k/32][rows_pad] (block-major planes, rows_pad % 256 == 0); since ABI 8 row r's
+ * byte of plane b sits at column srow(r) = (r & ~127) | (r & 31) << 2 | (r >> 5) & 3 (the
+ * four rows i*32 + r of one MFMA lane in one aligned dword, loaded by one buffer_load_dword);
+ * element (r,c) = e4m3(q[r][c]) * 2^(S[c/32][srow(r)] - 127). Block rule: absmax a,
  * S = clamp(expfield(a) - 8 + (mantissa(a) > 0x600000), 1, 254) (127 when a == 0),
  * q = RNE_e4m3(clamp(x * 2^(127-S), +-448)).  */
 

@@ -2309,6 +2309,266 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(MINW)))
     }
 }
 
+// ---------------------------------------------------------------------------
+// attn_pp_kernel (round 4, head dim 72): attn_hyb_kernel's arithmetic (kind 62: 32x32x16 QK^T
+// 80 deep from literal-zero starts, 16x16x32 PV with the ones row, lazy rescale, last-tile
+// skip) in a matrix / vector ping-pong. Every 64-key tile is two phases per wave:
+//   M(t): PV(t - 1) (20 MFMAs + 20 transposed V reads) and QK^T(t) (10 MFMAs + 10 K reads);
+//   V(t): mask, row max, lazy rescale of O, 32 exp2, bf16 packing into P(t) (VALU only).
+// The block's two wave rows (waves 0-3 and 4-7, one of each per SIMD) run one phase apart
+// between raw barriers, so on every SIMD one wave's MFMAs meet the other's softmax VALU
+// instead of both waves needing the same pipe at once (attn_hyb_kernel's waves all reach
+// their QK^T and their softmax together; its counters put MFMA-busy + VALU-busy at the
+// kernel time: the pipes take turns). Same per-accumulator MFMA order and the same VALU
+// sequence as kind 62, so the outputs are bit-identical to it.
+// Ring: 3 slots of K / V chunk planes (tile t in slot t % 3): V(t) is read one phase pair
+// after K(t), so tile t + 1, issued when the early row opens M(t), may only overwrite the
+// tile read last by the late row's M(t - 1).
+// Intervals between barriers: the early row runs M(t) in interval 2t and V(t) in 2t + 1, the
+// late row one interval later; each wave issues its pieces of tile t + 1 at the start of
+// interval 2t and retires them (vmcnt 0) before the barrier that closes interval 2t + 1.
+// PRIO: 0 none, 1 = s_setprio 1 for the late row (static), 2 = s_setprio 1 in every M phase.
+// ---------------------------------------------------------------------------
+template <int HD, int PRIO, int MINW>
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(MINW))) void attn_pp_kernel(AttnArgs a) {
+    static_assert(HD == 72, "the ones-row weight sums need V^T row 72 inside the 80-row PV");
+    constexpr int NW = 8, QB = NW * 32;
+    constexpr int NCHL = HD / 8, NKS = 5, NDT = 5, NVP = 2 * NDT;
+    constexpr int TILE = (NCHL + NVP) * 1024, NSLOT = 3;
+    constexpr int NINS = 2 * NCHL, MAXI = (NINS + NW - 1) / NW;
+    typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
+    __shared__ __attribute__((aligned(16))) char lds[NSLOT * TILE];
+
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const bool late = wave >= NW / 2;
+    const int r = lane & 31, hh = lane >> 5;
+    const int g = lane >> 4, li = lane & 15;
+    const int nqb = (a.T + QB - 1) / QB;
+    int id;
+    {
+        const int bid = blockIdx.x, nwg = gridDim.x;
+        const int xcd = bid & 7, loc = bid >> 3, q8 = nwg >> 3, r8 = nwg & 7;
+        id = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + loc;
+    }
+    const int qb = id % nqb, h = (id / nqb) % a.H, b = id / (nqb * a.H);
+    const int T = a.T, D = a.H * HD;
+    const bf16* base = a.qkv + (long)b * T * a.ld;
+    const int qw0 = qb * QB + wave * 32;
+    const int Tk = a.seq_lens ? a.seq_lens[b] : T;
+    const float c = a.scale_log2;
+
+    for (int i = tid; i < NSLOT * 64; i += NW * 64)  // the ones plane in every ring slot
+        *reinterpret_cast<u16x8*>(lds + (i >> 6) * TILE + (2 * NCHL) * 1024 + (i & 63) * 16) =
+            u16x8{0x3F80, 0x3F80, 0x3F80, 0x3F80, 0x3F80, 0x3F80, 0x3F80, 0x3F80};
+
+    bf16x8 qf[NKS];
+    {
+        const bf16* qrow = base + (long)min(qw0 + r, T - 1) * a.ld + h * HD;
+#pragma unroll
+        for (int ks = 0; ks < NKS; ++ks) {
+            const int col = ks * 16 + 8 * hh;
+            qf[ks] = col < HD ? *reinterpret_cast<const bf16x8*>(qrow + col) : bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
+        }
+    }
+    int nkt = (Tk + 63) / 64;
+    if (a.causal) nkt = min(nkt, (min(T, qb * QB + QB) + 63) / 64);
+
+    auto vslot = [](int key, int plane) { return key ^ (4 * ((key >> 4) & 1) + 8 * (plane & 1)); };
+    auto issue = [&](int t) __attribute__((always_inline)) {
+        char* tb = lds + (t % NSLOT) * TILE;
+#pragma unroll
+        for (int i = 0; i < MAXI; ++i) {
+            const int idx = wave + NW * i;
+            if (i < MAXI - 1 || idx < NINS) {
+                const bool isV = idx >= NCHL;
+                const int plane = isV ? idx - NCHL : idx;
+                const int key = isV ? vslot(lane, plane) : lane;
+                const bf16* src = base + (long)min(t * 64 + key, T - 1) * a.ld + (isV ? 2 : 1) * D + h * HD + plane * 8;
+                glds16(src, tb + idx * 1024);
+            }
+        }
+    };
+
+    const unsigned lds0 = (unsigned)(uintptr_t)(LDS_AS char*)lds;
+    const unsigned kb0 = lds0 + hh * 1024 + r * 16;
+    unsigned vbj[2];
+    {
+        const int q = li >> 2, p = li & 3, pc = p >> 1;
+        const int bg = 16 * (g & 1) + 4 * (g >> 1);
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+            vbj[j] = lds0 + (NCHL + pc) * 1024 + vslot(bg + 8 * j + q, pc) * 16 + (p & 1) * 8;
+    }
+
+    f32x4 o[2][NDT];
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+#pragma unroll
+        for (int i = 0; i < NDT; ++i) o[u][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+    float m = -1e30f;
+    f32x16 sc[2];       // S^T of the tile between its M and V phases
+    bf16x8 pb[2][2];    // P of the tile between its V phase and the next M phase: [key block][query half]
+    bool phalf = false;  // that tile's second key block skipped
+
+    auto barrier = [&]() __attribute__((always_inline)) {
+        __builtin_amdgcn_sched_barrier(0);
+        __builtin_amdgcn_s_barrier();
+        __builtin_amdgcn_sched_barrier(0);
+    };
+    // M phase: PV of the previous tile (slot sp, if any), then QK^T of tile t (slot sk, if any)
+    auto mphase = [&](int t, bool pv, bool qk) __attribute__((always_inline)) {
+        if (PRIO == 2) __builtin_amdgcn_s_setprio(1);
+        if (pv) {
+            const unsigned sp = (unsigned)((t - 1) % NSLOT) * TILE;
+#pragma unroll
+            for (int kb = 0; kb < 2; ++kb) {
+                if (kb == 1 && phalf) break;
+#pragma unroll
+                for (int dt = 0; dt < NDT; ++dt) {
+                    const unsigned off = sp + kb * 512 + dt * 2048;
+                    const s16x4 v0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS_AS s16x4*)(uintptr_t)(vbj[0] + off));
+                    const s16x4 v1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS_AS s16x4*)(uintptr_t)(vbj[1] + off));
+                    const bf16x8 vv = __builtin_bit_cast(bf16x8, __builtin_shufflevector(v0, v1, 0, 1, 2, 3, 4, 5, 6, 7));
+                    o[0][dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vv, pb[kb][0], o[0][dt], 0, 0, 0);
+                    o[1][dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vv, pb[kb][1], o[1][dt], 0, 0, 0);
+                }
+            }
+        }
+        if (qk) {
+            const unsigned so = (unsigned)(t % NSLOT) * TILE;
+            const bool half = t * 64 + 32 >= Tk;
+#pragma unroll
+            for (int kb = 0; kb < 2; ++kb) {
+                if (kb == 1 && half) {
+#pragma unroll
+                    for (int e = 0; e < 16; ++e) {
+                        float f;
+                        asm volatile("v_mov_b32 %0, 0xff800000" : "=v"(f));
+                        sc[1][e] = f;
+                    }
+                } else {
+                    f32x16 z = {};
+#pragma unroll
+                    for (int ks = 0; ks < NKS; ++ks) {
+                        const bf16x8 kf =
+                            *reinterpret_cast<const LDS_AS bf16x8*>((uintptr_t)(kb0 + so + kb * 512 + ks * 2048));
+                        z = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[ks], z, 0, 0, 0);
+                    }
+                    sc[kb] = z;
+                }
+            }
+        }
+        if (PRIO == 2) __builtin_amdgcn_s_setprio(0);
+    };
+    // V phase of tile t: mask, max, lazy rescale, exp2, P packing
+    auto vphase = [&](int t) __attribute__((always_inline)) {
+        if ((t * 64 + 64 > Tk) || (a.causal && t * 64 + 63 > qw0)) {
+            const int q = qw0 + r;
+            const int lim = a.causal ? min(Tk, q + 1) : Tk;
+#pragma unroll
+            for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+                for (int e = 0; e < 16; ++e)
+                    if (t * 64 + kb * 32 + (e & 3) + 8 * (e >> 2) + 4 * hh >= lim) sc[kb][e] = -INFINITY;
+        }
+        float mloc = fmaxf(sc[0][0], sc[0][1]);
+#pragma unroll
+        for (int e = 2; e < 16; ++e) mloc = fmaxf(mloc, sc[0][e]);
+#pragma unroll
+        for (int e = 0; e < 16; ++e) mloc = fmaxf(mloc, sc[1][e]);
+        mloc = xmax32(mloc);
+        const float mnew = fmaxf(m, mloc);
+        if (__builtin_amdgcn_ballot_w64(mnew != m)) {
+            const float alpha = __builtin_amdgcn_exp2f((m - mnew) * c);
+#pragma unroll
+            for (int u = 0; u < 2; ++u) {
+                const float au = __shfl(alpha, 16 * u + li, 64);
+#pragma unroll
+                for (int i = 0; i < NDT; ++i) o[u][i] *= au;
+            }
+        }
+        m = mnew;
+        const float mc = mnew * c;
+#pragma unroll
+        for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+            for (int e = 0; e < 16; ++e) sc[kb][e] = __builtin_amdgcn_exp2f(sc[kb][e] * c - mc);
+        phalf = t * 64 + 32 >= Tk;
+#pragma unroll
+        for (int kb = 0; kb < 2; ++kb) {
+            unsigned xw[4], yw[4];
+#pragma unroll
+            for (int w = 0; w < 4; ++w) {
+                bf16x2_t px = {f2bf(sc[kb][2 * w]), f2bf(sc[kb][2 * w + 1])};
+                bf16x2_t py = {f2bf(sc[kb][8 + 2 * w]), f2bf(sc[kb][8 + 2 * w + 1])};
+                xw[w] = __builtin_bit_cast(unsigned, px);
+                yw[w] = __builtin_bit_cast(unsigned, py);
+            }
+            unsigned b0w[4], b1w[4];
+#pragma unroll
+            for (int w = 0; w < 4; ++w) {
+                const auto sw = __builtin_amdgcn_permlane16_swap(xw[w], yw[w], false, false);
+                b0w[w] = sw[0];
+                b1w[w] = sw[1];
+            }
+            pb[kb][0] = __builtin_bit_cast(bf16x8, make_uint4(b0w[0], b0w[1], b0w[2], b0w[3]));
+            pb[kb][1] = __builtin_bit_cast(bf16x8, make_uint4(b1w[0], b1w[1], b1w[2], b1w[3]));
+        }
+    };
+
+    if (PRIO == 1 && late) __builtin_amdgcn_s_setprio(1);
+    if (nkt > 0) {
+        issue(0);
+        vm_wait<0>();
+        barrier();
+        if (!late) {
+            for (int t = 0; t < nkt; ++t) {
+                if (t + 1 < nkt) issue(t + 1);  // interval 2t
+                mphase(t, t > 0, true);
+                barrier();
+                vphase(t);  // interval 2t + 1
+                vm_wait<0>();
+                barrier();
+            }
+            mphase(nkt, true, false);  // interval 2 nkt
+            barrier();
+        } else {
+            if (nkt > 1) issue(1);  // interval 0
+            barrier();
+            for (int t = 0; t < nkt; ++t) {
+                mphase(t, t > 0, true);  // interval 2t + 1
+                vm_wait<0>();
+                barrier();
+                if (t + 2 < nkt) issue(t + 2);  // interval 2t + 2
+                vphase(t);
+                barrier();
+            }
+            mphase(nkt, true, false);  // interval 2 nkt + 1
+        }
+    }
+
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+        const float ltot = __shfl(o[u][NDT - 1][0], 32 + li, 64);
+        const float inv = 1.0f / ltot;
+        const int q = qw0 + 16 * u + li;
+        if (q < T) {
+            bf16* orow = a.out + ((long)b * T + q) * a.ldo + h * HD;
+#pragma unroll
+            for (int dt = 0; dt < NDT; ++dt) {
+                const int d0 = dt * 16 + 4 * g;
+                if (d0 < HD) {
+                    bf16x4 v;
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) v[e] = f2bf(o[u][dt][e] * inv);
+                    *reinterpret_cast<bf16x4*>(orow + d0) = v;
+                }
+            }
+        }
+    }
+}
+
 // SigLIP MAP head: one probe query per head, keys = the T tokens of image b.
 constexpr int PROBE_MAXT = 1024;
 __global__ __launch_bounds__(256) void probe_attn_kernel(const bf16* __restrict__ qv, const bf16* __restrict__ kv,
@@ -2653,6 +2913,19 @@ bool launch_attn_dev(int kind, const AttnArgs& a, int B, int T, int H, hipStream
             hipLaunchKernelGGL((attn_hyb_kernel<HD, 8, 4, true, 1>), dim3(cdiv(T, 256) * H * B), dim3(512), 0, st, a);
         else
             hipLaunchKernelGGL((attn_m32_kernel<HD, 8, 1, true>), dim3(cdiv(T, 256) * H * B), dim3(512), 0, st, a);
+    } else if (kind >= 70 && kind <= 72) {  // dev: attn_pp_kernel (hd 72), PRIO = kind - 70, 2 waves per SIMD
+                                            // (155 VGPRs; a 128-VGPR cap spills 16)
+        if constexpr (HD == 72) {
+            const dim3 grid(cdiv(T, 256) * H * B), blk(512);
+            if (kind == 70)
+                hipLaunchKernelGGL((attn_pp_kernel<HD, 0, 2>), grid, blk, 0, st, a);
+            else if (kind == 71)
+                hipLaunchKernelGGL((attn_pp_kernel<HD, 1, 2>), grid, blk, 0, st, a);
+            else
+                hipLaunchKernelGGL((attn_pp_kernel<HD, 2, 2>), grid, blk, 0, st, a);
+        } else {
+            return false;
+        }
     } else if (kind == 12)  // dev: pipelined + lazy + ones
         hipLaunchKernelGGL((attn_pipe_kernel<HD, 8, 3, true, HD == 72, true>), dim3(cdiv(T, 256) * H * B), dim3(512), 0, st, a);
     else if (kind == 2)

@@ -47,6 +47,11 @@ __device__ __forceinline__ uint2 mx_pack8(const float (&v)[8], int sb) {
     return make_uint2(lo, hi);
 }
 
+// Scale-plane row order (round 4): inside each 128-row group of a plane, row r is stored at
+// (r % 32) * 4 + (r % 128) / 32, so the 4 scale bytes a 32x32x64 MFMA lane needs for the rows
+// i * 32 + r (i = 0..3) of one block are one aligned dword (gemm_mx11: one 4-byte load per block).
+__device__ __forceinline__ int mx_srow(int r) { return (r & ~127) | ((r & 31) << 2) | ((r >> 5) & 3); }
+
 // absmax over the 4 consecutive lanes holding one 32-element block
 __device__ __forceinline__ float block_amax(float a) {
     a = fmaxf(a, __shfl_xor(a, 1, 64));
@@ -82,7 +87,7 @@ __global__ __launch_bounds__(256) void mx_quant_kernel(const bf16* __restrict__ 
         const int sb = mx_scale_byte(block_amax(a));
         if (ch < nch) {
             *reinterpret_cast<uint2*>(q + (long)row * ldq + ch * 8) = mx_pack8(v, sb);
-            if ((ch & 3) == 0) sc[(long)(ch >> 2) * rows_pad + row] = (uint8_t)sb;
+            if ((ch & 3) == 0) sc[(long)(ch >> 2) * rows_pad + mx_srow(row)] = (uint8_t)sb;
         }
     }
 }
@@ -158,7 +163,7 @@ __global__ __launch_bounds__(256) void layernorm_mx_kernel(const bf16* __restric
         const int sb = mx_scale_byte(block_amax(a));
         if (ch < nch) {
             *reinterpret_cast<uint2*>(q + (long)row * ldq + ch * 8) = mx_pack8(o, sb);
-            if ((ch & 3) == 0) sc[(long)(ch >> 2) * rows_pad + row] = (uint8_t)sb;
+            if ((ch & 3) == 0) sc[(long)(ch >> 2) * rows_pad + mx_srow(row)] = (uint8_t)sb;
         }
     }
 }
@@ -252,7 +257,9 @@ __device__ __forceinline__ void mx_dma1(unsigned m0base, unsigned voff, i32x4v r
 // conflict-free ds_write_b64 staging (16 contiguous lanes = rows r32 0..15) and ds_read_b128
 // read-back; SWZ = false: the round-3 pitch-144 layout (2-way on both; dev form 4).
 constexpr int MXW_PITCH = 144, MXW_LDS = 8 * 128 * MXW_PITCH;
-template <int ACT, bool SWZ = true>
+// SB (mx11): a scheduling barrier after each staged column quad keeps the unrolled staging loop
+// from interleaving (and holding live) all 32 quads' activations at once.
+template <int ACT, bool SWZ = true, bool SB = false>
 __device__ __forceinline__ void mx_epilogue_wave(const MxArgs& p, char* lds, f32x16 (&acc)[4][2], int m0, int n0,
                                                  int wave, int lane) {
     constexpr int TM = 128, TN = 64, MX9_PITCH = SWZ ? 128 : MXW_PITCH;
@@ -282,6 +289,7 @@ __device__ __forceinline__ void mx_epilogue_wave(const MxArgs& p, char* lds, f32
                 else
                     *reinterpret_cast<bf16x4*>(reg + (i * 32 + r32) * MX9_PITCH + nl * 2) = o;
             }
+            if (SB) __builtin_amdgcn_sched_barrier(0);
         }
     // the wave's own LDS writes precede its reads
     const int rr = lane >> 3, cc = lane & 7;
@@ -328,7 +336,7 @@ __device__ __forceinline__ void mx_epilogue_wave(const MxArgs& p, char* lds, f32
             const int sbyte = mx_scale_byte(block_amax(a));
             if (gr < p.M && gc < p.N) {
                 *reinterpret_cast<uint2*>(Cq + (size_t)gr * p.ldc + gc) = mx_pack8(f, sbyte);
-                if ((cc & 3) == 0) p.sc[(size_t)(gc >> 5) * p.sc_rows + gr] = (uint8_t)sbyte;
+                if ((cc & 3) == 0) p.sc[(size_t)(gc >> 5) * p.sc_rows + mx_srow(gr)] = (uint8_t)sbyte;
             }
         }
     }
@@ -390,8 +398,8 @@ __global__ __launch_bounds__(512, 2) void gemm_mx_kernel(MxArgs p) {
     const unsigned c0 = (unsigned)((h ^ sw) << 4), c1 = (unsigned)(((2 + h) ^ sw) << 4);
     const unsigned a_row = lds0 + (wm * C::TM + r32) * 64;
     const unsigned b_row = lds0 + C::A_ST + (wn * C::TN + r32) * 64;
-    const unsigned sa_l = lds0 + C::A_ST + C::B_ST + h * 256 + wm * C::TM + r32;
-    const unsigned sb_l = lds0 + C::A_ST + C::B_ST + 512 + h * 256 + wn * C::TN + r32;
+    const unsigned sa_l = lds0 + C::A_ST + C::B_ST + h * 256 + wm * C::TM + r32 * 4;  // mx_srow order
+    const unsigned sb_l = lds0 + C::A_ST + C::B_ST + 512 + h * 256 + (wn >> 1) * 128 + r32 * 4 + (wn & 1) * 2;
 
     f32x16 acc[C::FM][C::FN];
 #pragma unroll
@@ -434,14 +442,14 @@ __global__ __launch_bounds__(512, 2) void gemm_mx_kernel(MxArgs p) {
             ds_read16<0>(a[i][1], a_row + so + i * 32 * 64 + c1);
         }
         asm volatile("ds_read_u8 %0, %1 offset:0" : "=v"(sbv[0]) : "v"(sb_l + so) : "memory");
-        asm volatile("ds_read_u8 %0, %1 offset:32" : "=v"(sbv[1]) : "v"(sb_l + so) : "memory");
+        asm volatile("ds_read_u8 %0, %1 offset:1" : "=v"(sbv[1]) : "v"(sb_l + so) : "memory");
 #pragma unroll
         for (int i = 0; i < C::FM; ++i) {
             // offsets i*32 (A) / j*32 (B) as immediates
             if (i == 0) asm volatile("ds_read_u8 %0, %1 offset:0" : "=v"(sa[0]) : "v"(sa_l + so) : "memory");
-            if (i == 1) asm volatile("ds_read_u8 %0, %1 offset:32" : "=v"(sa[1]) : "v"(sa_l + so) : "memory");
-            if (i == 2) asm volatile("ds_read_u8 %0, %1 offset:64" : "=v"(sa[2]) : "v"(sa_l + so) : "memory");
-            if (i == 3) asm volatile("ds_read_u8 %0, %1 offset:96" : "=v"(sa[3]) : "v"(sa_l + so) : "memory");
+            if (i == 1) asm volatile("ds_read_u8 %0, %1 offset:1" : "=v"(sa[1]) : "v"(sa_l + so) : "memory");
+            if (i == 2) asm volatile("ds_read_u8 %0, %1 offset:2" : "=v"(sa[2]) : "v"(sa_l + so) : "memory");
+            if (i == 3) asm volatile("ds_read_u8 %0, %1 offset:3" : "=v"(sa[3]) : "v"(sa_l + so) : "memory");
         }
         if (t + 3 < nk) {
             issue(t + 3);
@@ -536,7 +544,7 @@ __global__ __launch_bounds__(512, 2) void gemm_mx_kernel(MxArgs p) {
             const int sbyte = mx_scale_byte(block_amax(a));
             if (gr < p.M && gc < p.N) {
                 *reinterpret_cast<uint2*>(Cq + (size_t)gr * p.ldc + gc) = mx_pack8(f, sbyte);
-                if ((cc & 3) == 0) p.sc[(size_t)(gc >> 5) * p.sc_rows + gr] = (uint8_t)sbyte;
+                if ((cc & 3) == 0) p.sc[(size_t)(gc >> 5) * p.sc_rows + mx_srow(gr)] = (uint8_t)sbyte;
             }
         }
     }
@@ -587,8 +595,8 @@ __device__ __forceinline__ void mx10_tile(const MxArgs& p, char* lds, const int 
     // two bases per operand: slots 0 / 1 at base + {0, STAGE}, slots 2 / 3 at base2 + {0, STAGE}
     const unsigned a0 = lds0 + (wm * C::TM + r32) * 64 + c0, a1 = lds0 + (wm * C::TM + r32) * 64 + c1;
     const unsigned b0 = lds0 + C::A_ST + (wn * C::TN + r32) * 64 + c0, b1 = lds0 + C::A_ST + (wn * C::TN + r32) * 64 + c1;
-    const unsigned sa_l = lds0 + C::A_ST + C::B_ST + h * 256 + wm * C::TM + r32;
-    const unsigned sb_l = lds0 + C::A_ST + C::B_ST + 512 + h * 256 + wn * C::TN + r32;
+    const unsigned sa_l = lds0 + C::A_ST + C::B_ST + h * 256 + wm * C::TM + r32 * 4;  // mx_srow order
+    const unsigned sb_l = lds0 + C::A_ST + C::B_ST + 512 + h * 256 + (wn >> 1) * 128 + r32 * 4 + (wn & 1) * 2;
     constexpr unsigned HI = 2 * C::STAGE;
 
     f32x16 acc[C::FM][C::FN];
@@ -628,11 +636,11 @@ __device__ __forceinline__ void mx10_tile(const MxArgs& p, char* lds, const int 
             if (i == 3) { ds_read16<OFF + 3 * 2048>(a[3][0], abase0); ds_read16<OFF + 3 * 2048>(a[3][1], abase1); }
         }
         asm volatile("ds_read_u8 %0, %1 offset:%2" : "=v"(sbv[0]) : "v"(sbb), "n"(OFF + 0) : "memory");
-        asm volatile("ds_read_u8 %0, %1 offset:%2" : "=v"(sbv[1]) : "v"(sbb), "n"(OFF + 32) : "memory");
+        asm volatile("ds_read_u8 %0, %1 offset:%2" : "=v"(sbv[1]) : "v"(sbb), "n"(OFF + 1) : "memory");
         asm volatile("ds_read_u8 %0, %1 offset:%2" : "=v"(sa[0]) : "v"(sab), "n"(OFF + 0) : "memory");
-        asm volatile("ds_read_u8 %0, %1 offset:%2" : "=v"(sa[1]) : "v"(sab), "n"(OFF + 32) : "memory");
-        asm volatile("ds_read_u8 %0, %1 offset:%2" : "=v"(sa[2]) : "v"(sab), "n"(OFF + 64) : "memory");
-        asm volatile("ds_read_u8 %0, %1 offset:%2" : "=v"(sa[3]) : "v"(sab), "n"(OFF + 96) : "memory");
+        asm volatile("ds_read_u8 %0, %1 offset:%2" : "=v"(sa[1]) : "v"(sab), "n"(OFF + 1) : "memory");
+        asm volatile("ds_read_u8 %0, %1 offset:%2" : "=v"(sa[2]) : "v"(sab), "n"(OFF + 2) : "memory");
+        asm volatile("ds_read_u8 %0, %1 offset:%2" : "=v"(sa[3]) : "v"(sab), "n"(OFF + 3) : "memory");
         if (dma) issue(ist, isl);
         wait(rem);
         lgkm_wait<0>();
@@ -723,6 +731,256 @@ int launch_mx10(const MxArgs& a, hipStream_t s) {
     return mme_check_launch("mme_gemm_mx");
 }
 
+// ---------------------------------------------------------------------------
+// mx11 (round 4): the block-scaled fp8 GEMM on pipe9's LDS ring and schedule (gemm.hip).
+// fp8 values are one byte, so a 128-deep fp8 stage of 256 rows is one 32 KiB unit of whole
+// 128-B cache-line rows -- exactly pipe9's unit. The ring is pipe9's (five units: A of stage s in
+// slot 2s mod 5, B in 2s + 1 mod 5, all 160 KiB of LDS), with pipe9's DMA pieces (8 rows x 128 B,
+// chunk swizzle c ^ ((row >> 1) & 7): the 32-row fragment reads below hit 16 distinct 16-B bank
+// slots per ds_read_b128 lane group), ping-pong wave rows (LATE), static waits / barriers and
+// soffset-stepped buffer_load ... lds. A stage runs as two 64-deep k-steps, each a memory phase
+// (12 ds_read_b128: lane (r, h) reads logical chunks 4 ks + h and 4 ks + 2 + h of its rows, the
+// v_mfma_scale_f32_32x32x64_f8f6f4 operand layout of mx10) and a compute phase of 8 MFMAs
+// (4 x 2 tiles of 32 x 32): per k-step the same LDS bytes, ds_reads and MFMA cycles as one pipe9
+// step, at twice the FLOPs. The K order and MFMA chains are mx10's, so the outputs are bit-identical
+// to mx10 (tests/test_gpu_mx.py).
+// Scales leave LDS (mx9 kept them there and lost a ring slot: -10 %): the planes' mx_srow row order
+// puts the 4 bytes lane (r, h) needs for rows i * 32 + r of one block in one aligned dword, so a
+// stage costs 4 buffer_load_dword per lane (A and B, blocks 4 s + h and 4 s + 2 + h), issued one
+// stage ahead with the B unit of the next stage and retired by the same counted vmcnt; the MFMA's
+// scale op_sel picks the byte (A: i; B: j after a 16-bit shift for odd wn).
+// Needs K % 128 == 0, K >= 384 (three stages) and operands < 4 GiB (32-bit offsets).
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ unsigned mx_sload(unsigned voff, i32x4v rsrc, unsigned soff) {
+    unsigned v;
+    asm volatile("buffer_load_dword %0, %1, %2, %3 offen" : "=v"(v) : "v"(voff), "s"(rsrc), "s"(soff) : "memory");
+    return v;
+}
+// counted vmcnt that also marks the scale registers loaded by inline asm as written here, so no
+// use of them can be scheduled before the wait that retires their loads
+template <int N>
+__device__ __forceinline__ void vm_wait_sc(unsigned (&sc)[4]) {
+    asm volatile("s_waitcnt vmcnt(%4)" : "+v"(sc[0]), "+v"(sc[1]), "+v"(sc[2]), "+v"(sc[3]) : "n"(N) : "memory");
+}
+template <int I, int J>
+__device__ __forceinline__ void mx11_mfma(f32x16& acc, const bf16x8 (&a)[2], const bf16x8 (&b)[2], unsigned sa,
+                                          unsigned sb) {
+    const i32x8 bo = __builtin_bit_cast(i32x8, __builtin_shufflevector(b[0], b[1], 0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10,
+                                                                       11, 12, 13, 14, 15));
+    const i32x8 ao = __builtin_bit_cast(i32x8, __builtin_shufflevector(a[0], a[1], 0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10,
+                                                                       11, 12, 13, 14, 15));
+    acc = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(bo, ao, acc, 0, 0, J, (int)sb, I, (int)sa);
+}
+
+template <int ACT, bool LATE>
+__device__ __forceinline__ void mx11_tile(const MxArgs& p, char* lds, const int m0, const int n0, const int wave) {
+    constexpr int UNIT = 32768;
+    const int lane = threadIdx.x & 63;
+    const int wm = wave / 4, wn = wave % 4;
+    const int h = lane >> 5, r32 = lane & 31;
+
+    unsigned offA[4], offB[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const int prow = (wave * 4 + q) * 8 + (lane >> 3);
+        const int logical = swz(prow, lane & 7);
+        offA[q] = (unsigned)min(m0 + prow, p.M - 1) * (unsigned)p.lda + logical * 16;
+        offB[q] = (unsigned)min(n0 + prow, p.N - 1) * (unsigned)p.ldb + logical * 16;
+    }
+    const i32x4v rA = mx_rsrc(p.A, (unsigned)((size_t)p.M * p.lda));
+    const i32x4v rB = mx_rsrc(p.B, (unsigned)((size_t)p.N * p.ldb));
+    // scale dwords: A rows m0 + wm 128 + {0, 32, 64, 96} + r32 of block b at plane b, bytes
+    // m0 + wm 128 + 4 r32 + i; B columns n0 + wn 64 + {0, 32} + r32 at n0 + (wn / 2) 128 + 4 r32 + 2 (wn & 1) + j
+    const i32x4v rSA = mx_rsrc(p.sa, (unsigned)((size_t)(p.K / 32) * p.sa_rows));
+    const i32x4v rSB = mx_rsrc(p.sb, (unsigned)((size_t)(p.K / 32) * p.sb_rows));
+    const unsigned vsa = (unsigned)(h * p.sa_rows + m0 + wm * 128 + 4 * r32);
+    const unsigned vsb = (unsigned)(h * p.sb_rows + n0 + (wn >> 1) * 128 + 4 * r32);
+    const unsigned sstepA = 4u * p.sa_rows, sstepB = 4u * p.sb_rows, bshift = (wn & 1) * 16;
+    const unsigned s2A = 2u * p.sa_rows, s2B = 2u * p.sb_rows;  // k-step 1's blocks: two planes further
+
+    const unsigned lds0 = (unsigned)(uintptr_t)(LDS_AS char*)lds;
+    const unsigned lw = __builtin_amdgcn_readfirstlane(lds0 + wave * 4096);
+    const int sw = (r32 >> 1) & 7;  // fragment rows differ by multiples of 32: the swizzle depends on r32
+    // logical chunk c of the lane's row sits at chunk c ^ sw; with x = h ^ sw the k-step ks chunks
+    // 4 ks + h + {0, 2} are at (x ^ (4 ks + {0, 2})), i.e. base_x ^ ((4 ks + {0, 2}) << 4) with
+    // base_x = row base + (x << 4) (128-B aligned rows: no carries), and the XOR commutes with the
+    // fragment (i * 4 KiB) and slot (32 KiB) offsets: two base registers, one v_xor per read address
+    const unsigned a_x = lds0 + (wm * 128 + r32) * 128 + ((h ^ sw) << 4);
+    const unsigned b_x = lds0 + (wn * 64 + r32) * 128 + ((h ^ sw) << 4);
+
+    f32x16 acc[4][2];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
+    const int nk = p.K / 128;
+    unsigned cur[4], nxt[4];  // scale dwords of this / the next stage: A ks 0, A ks 1, B ks 0, B ks 1
+    unsigned kscA = 0, kscB = 0;  // soffsets of the next scales to load (A / B planes)
+
+    auto load_sc = [&](unsigned (&d)[4]) __attribute__((always_inline)) {
+        d[0] = mx_sload(vsa, rSA, kscA);
+        d[1] = mx_sload(vsa, rSA, kscA + s2A);
+        d[2] = mx_sload(vsb, rSB, kscB);
+        d[3] = mx_sload(vsb, rSB, kscB + s2B);
+        kscA += sstepA;
+        kscB += sstepB;
+    };
+    // one 64-deep k-step: memory phase (12 fragment reads, optionally the next stage's scales and
+    // a DMA unit), barrier, compute phase (8 MFMAs), barrier. wm_ / wc_: vmcnt kept after the
+    // memory / compute phase (-1: no wait); the waits that retire a scale load tie nxt.
+    auto step = [&](unsigned aa0, unsigned aa1, unsigned bb0, unsigned bb1, unsigned sa, unsigned sb, bool scl,
+                    bool dma, unsigned m0base, const unsigned (&voff)[4], i32x4v rs, unsigned soff, int wm_, int wc_,
+                    bool end_barrier) __attribute__((always_inline)) {
+        bf16x8 a[4][2], b[2][2];
+        ds_read16<0>(b[0][0], bb0);
+        ds_read16<0>(b[0][1], bb1);
+        ds_read16<4096>(b[1][0], bb0);
+        ds_read16<4096>(b[1][1], bb1);
+        ds_read16<0>(a[0][0], aa0);
+        ds_read16<0>(a[0][1], aa1);
+        ds_read16<4096>(a[1][0], aa0);
+        ds_read16<4096>(a[1][1], aa1);
+        ds_read16<8192>(a[2][0], aa0);
+        ds_read16<8192>(a[2][1], aa1);
+        ds_read16<12288>(a[3][0], aa0);
+        ds_read16<12288>(a[3][1], aa1);
+        if (scl) load_sc(nxt);
+        if (dma) mx_dma4(m0base, voff, rs, soff);
+        if (wm_ == 0) vm_wait_sc<0>(nxt);
+        else if (wm_ == 4) vm_wait_sc<4>(nxt);
+        lgkm_wait<0>();
+        __builtin_amdgcn_s_barrier();
+        __builtin_amdgcn_s_setprio(1);
+        const unsigned sbs = sb >> bshift;
+        mx11_mfma<0, 0>(acc[0][0], a[0], b[0], sa, sbs);
+        mx11_mfma<0, 1>(acc[0][1], a[0], b[1], sa, sbs);
+        mx11_mfma<1, 0>(acc[1][0], a[1], b[0], sa, sbs);
+        mx11_mfma<1, 1>(acc[1][1], a[1], b[1], sa, sbs);
+        mx11_mfma<2, 0>(acc[2][0], a[2], b[0], sa, sbs);
+        mx11_mfma<2, 1>(acc[2][1], a[2], b[1], sa, sbs);
+        mx11_mfma<3, 0>(acc[3][0], a[3], b[0], sa, sbs);
+        mx11_mfma<3, 1>(acc[3][1], a[3], b[1], sa, sbs);
+        __builtin_amdgcn_s_setprio(0);
+        __builtin_amdgcn_sched_barrier(0);
+        if (wc_ == 0) vm_wait_sc<0>(nxt);
+        else if (wc_ == 4) vm_wait_sc<4>(nxt);
+        if (end_barrier) __builtin_amdgcn_s_barrier();
+    };
+    // soffset (bytes along K) of the B unit (stage s + 1) / A unit (s + 2) that stage s issues: from
+    // stage 1 on (stage 0's successors B1 and A2 come from the prologue)
+    unsigned kB = 256, kA = 384;
+    // stage with its A in slot sa (B in sa + 1): issue B(s + 1) (+ its scales) into slot sa + 3, A(s + 2)
+    // into sa + 4 (mod 5); need: this wave's loads kept in flight at the barrier before stage s + 1
+    auto stage = [&](int sa, bool dB, bool scl, bool dA, int need, bool last) __attribute__((always_inline)) {
+        const int sb = sa == 4 ? 0 : sa + 1;
+        const int iB = sa + 3 >= 5 ? sa - 2 : sa + 3, iA = sa + 4 >= 5 ? sa - 1 : sa + 4;
+        const unsigned as = a_x + sa * UNIT, bs = b_x + sb * UNIT;
+        step(as, as ^ (2u << 4), bs, bs ^ (2u << 4), cur[0], cur[2], scl, dB, lw + iB * UNIT, offB, rB, kB, -1, -1,
+             true);
+        step(as ^ (4u << 4), as ^ (6u << 4), bs ^ (4u << 4), bs ^ (6u << 4), cur[1], cur[3], false, dA,
+             lw + iA * UNIT, offA, rA, kA, LATE ? need : -1, LATE ? -1 : need, !(LATE && last));
+        kB += 128;
+        kA += 128;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) cur[q] = nxt[q];
+    };
+
+    // prologue: scales of stage 0, units 0 and 1 (stage 0), scales of stage 1, units 2..4 (A1 B1 A2)
+    load_sc(cur);
+    mx_dma4(lw + 0 * UNIT, offA, rA, 0);
+    mx_dma4(lw + 1 * UNIT, offB, rB, 0);
+    load_sc(nxt);
+    mx_dma4(lw + 2 * UNIT, offA, rA, 128);
+    mx_dma4(lw + 3 * UNIT, offB, rB, 128);
+    mx_dma4(lw + 4 * UNIT, offA, rA, 256);
+    vm_wait_sc<12>(cur);  // stage 0's scales and units landed (and stage 1's scales)
+    vm_wait_sc<12>(nxt);
+    __builtin_amdgcn_s_barrier();
+    if (LATE) __builtin_amdgcn_s_barrier();
+
+    {  // stage 0: its successors' units were issued in the prologue; cur <- stage 1's scales
+        const unsigned c0 = cur[0], c1 = cur[1], c2 = cur[2], c3 = cur[3];
+        const unsigned bs = b_x + UNIT;
+        step(a_x, a_x ^ (2u << 4), bs, bs ^ (2u << 4), c0, c2, false, false, 0, offB, rB, 0, -1, -1, true);
+        step(a_x ^ (4u << 4), a_x ^ (6u << 4), bs ^ (4u << 4), bs ^ (6u << 4), c1, c3, false, false, 0, offA, rA, 0,
+             LATE ? 4 : -1, LATE ? -1 : 4, true);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) cur[q] = nxt[q];
+    }
+    int s = 1;
+    // from here the scales of stage s + 1 are loaded in stage s (kscA / kscB at stage 2's)
+    for (; s + 5 <= nk - 2; s += 5) {  // steady state: s = 1 (mod 5) -> A slots 2, 4, 1, 3, 0
+        stage(2, true, true, true, 4, false);
+        stage(4, true, true, true, 4, false);
+        stage(1, true, true, true, 4, false);
+        stage(3, true, true, true, 4, false);
+        stage(0, true, true, true, 4, false);
+    }
+    if (s < nk - 2) {
+        stage(2, true, true, true, 4, false);
+        if (++s < nk - 2) {
+            stage(4, true, true, true, 4, false);
+            if (++s < nk - 2) {
+                stage(1, true, true, true, 4, false);
+                if (++s < nk - 2) {
+                    stage(3, true, true, true, 4, false);
+                    ++s;
+                }
+            }
+        }
+    }
+    // s = nk - 2: B and the scales of the last stage only; s = nk - 1: nothing (ring slots at run time)
+    const int sa2 = (2 * s) % 5, sa1 = sa2 >= 3 ? sa2 - 3 : sa2 + 2;
+    stage(sa2, true, true, false, 0, false);
+    stage(sa1, false, false, false, -1, true);
+    vm_wait<0>();
+    // the accumulators pass through an empty asm here: without it the last stage's MFMAs are sunk
+    // into the epilogue's branches, holding their fragments live beside the epilogue (VGPR spills)
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) asm volatile("" : "+v"(acc[i][j]));
+    // no LDS hazard: every wave's last fragment reads precede the barrier closing the late row's
+    // last memory phase, which the early row passes before it writes its epilogue region
+    mx_epilogue_wave<ACT, true, true>(p, lds, acc, m0, n0, wave, lane);
+}
+
+template <int GROUP_M, int ACT>
+__global__ __launch_bounds__(512, 2) void gemm_mx11_kernel(MxArgs p) {
+    __shared__ __attribute__((aligned(16))) char lds[5 * 32768];
+    const int nbm = (p.M + 255) / 256, nbn = (p.N + 255) / 256;
+    const int tile = xcd_remap(blockIdx.x, gridDim.x);
+    int bm, bn;
+    tile_coords<GROUP_M>(tile, nbm, nbn, bm, bn);
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    if (wave >= 4)
+        mx11_tile<ACT, true>(p, lds, bm * 256, bn * 256, wave);
+    else
+        mx11_tile<ACT, false>(p, lds, bm * 256, bn * 256, wave);
+}
+
+template <int GROUP_M>
+int launch_mx11(const MxArgs& a, hipStream_t s) {
+    const dim3 grid(((a.M + 255) / 256) * ((a.N + 255) / 256)), block(512);
+    switch (a.act) {
+        case MME_ACT_GELU_TANH:
+            hipLaunchKernelGGL((gemm_mx11_kernel<GROUP_M, MME_ACT_GELU_TANH>), grid, block, 0, s, a);
+            break;
+        case MME_ACT_QUICK_GELU:
+            hipLaunchKernelGGL((gemm_mx11_kernel<GROUP_M, MME_ACT_QUICK_GELU>), grid, block, 0, s, a);
+            break;
+        case MME_ACT_GELU_ERF:
+            hipLaunchKernelGGL((gemm_mx11_kernel<GROUP_M, MME_ACT_GELU_ERF>), grid, block, 0, s, a);
+            break;
+        default:
+            hipLaunchKernelGGL((gemm_mx11_kernel<GROUP_M, MME_ACT_NONE>), grid, block, 0, s, a);
+            break;
+    }
+    return mme_check_launch("mme_gemm_mx");
+}
+
 #ifdef MME_DEV
 // ---------------------------------------------------------------------------
 // mx9 (dev variant 9, round 3; MME_DEV builds only): the block-scaled fp8 GEMM on
@@ -782,8 +1040,8 @@ __device__ __forceinline__ void mx9_tile(const MxArgs& p, char* lds, const int m
     const unsigned a10 = a_row + (((4 + h) ^ sw) << 4), a11 = a_row + (((6 + h) ^ sw) << 4);
     const unsigned b00 = b_row + (((0 + h) ^ sw) << 4), b01 = b_row + (((2 + h) ^ sw) << 4);
     const unsigned b10 = b_row + (((4 + h) ^ sw) << 4), b11 = b_row + (((6 + h) ^ sw) << 4);
-    const unsigned sa_l = lds0 + MX9_SC + h * 256 + wm * TM + r32;
-    const unsigned sb_l = lds0 + MX9_SC + 1024 + h * 256 + wn * TN + r32;
+    const unsigned sa_l = lds0 + MX9_SC + h * 256 + wm * TM + r32 * 4;  // mx_srow order
+    const unsigned sb_l = lds0 + MX9_SC + 1024 + h * 256 + (wn >> 1) * 128 + r32 * 4 + (wn & 1) * 2;
 
     f32x16 acc[4][2];
 #pragma unroll
@@ -815,11 +1073,11 @@ __device__ __forceinline__ void mx9_tile(const MxArgs& p, char* lds, const int m
         ds_read16<12288>(a[3][0], aa0);
         ds_read16<12288>(a[3][1], aa1);
         asm volatile("ds_read_u8 %0, %1 offset:0" : "=v"(sbv[0]) : "v"(scb) : "memory");
-        asm volatile("ds_read_u8 %0, %1 offset:32" : "=v"(sbv[1]) : "v"(scb) : "memory");
+        asm volatile("ds_read_u8 %0, %1 offset:1" : "=v"(sbv[1]) : "v"(scb) : "memory");
         asm volatile("ds_read_u8 %0, %1 offset:0" : "=v"(sa[0]) : "v"(sca) : "memory");
-        asm volatile("ds_read_u8 %0, %1 offset:32" : "=v"(sa[1]) : "v"(sca) : "memory");
-        asm volatile("ds_read_u8 %0, %1 offset:64" : "=v"(sa[2]) : "v"(sca) : "memory");
-        asm volatile("ds_read_u8 %0, %1 offset:96" : "=v"(sa[3]) : "v"(sca) : "memory");
+        asm volatile("ds_read_u8 %0, %1 offset:1" : "=v"(sa[1]) : "v"(sca) : "memory");
+        asm volatile("ds_read_u8 %0, %1 offset:2" : "=v"(sa[2]) : "v"(sca) : "memory");
+        asm volatile("ds_read_u8 %0, %1 offset:3" : "=v"(sa[3]) : "v"(sca) : "memory");
         if (dma) {
             mx_dma4(lw + nslot * 2 * MX9_UNIT, offA, rA, soff);
             mx_dma4(lw + nslot * 2 * MX9_UNIT + MX9_UNIT, offB, rB, soff);
@@ -918,9 +1176,9 @@ inline int mx_default_form() { return -1; }
 #endif
 inline bool mx_form_ok(int v) {
 #ifdef MME_DEV
-    return v == -1 || v == 0 || v == 2 || v == 3 || v == 4 || v == 9;
+    return v == -1 || v == 0 || v == 2 || v == 3 || v == 4 || v == 9 || v == 10;
 #else
-    return v == -1 || v == 0 || v == 2 || v == 3;
+    return v == -1 || v == 0 || v == 2 || v == 3 || v == 10;
 #endif
 }
 
@@ -1048,6 +1306,11 @@ int gemm_mx_entry(int form, const void* A, int lda, const void* sa, int sa_rows,
     if (form == 0) return launch_mx<4>(a, as_stream(stream));
     if (form == 2) return launch_mx<4, true>(a, as_stream(stream));
     if (form == 3 || !mx10_ok) return launch_mx<4, true, true>(a, as_stream(stream));
+    // round 4: mx11 (pipe9's whole-line ring, scales by buffer loads) where its geometry holds;
+    // form 10 = mx10 (the bit-identity reference and A/B baseline)
+    const bool mx11_ok = K % 128 == 0 && K >= 384 &&
+                         (size_t)(K / 32) * (sa_rows > sb_rows ? sa_rows : sb_rows) < (1ull << 32);
+    if (form != 10 && mx11_ok) return launch_mx11<4>(a, as_stream(stream));
     return launch_mx10<4>(a, as_stream(stream));
 }
 }  // namespace

@@ -25,7 +25,7 @@ _forms = threading.local()
 @contextlib.contextmanager
 def kernel_forms(**forms: int):
     """Kernel forms for the calls this thread makes inside the block (bit-identity tests, A/B):
-    gemm=47 (pipe6) / 48 (per-row statistics combine), mx=0 / 2 / 3 (earlier mx GEMM forms),
+    gemm=47 (pipe6) / 48 (per-row statistics combine), mx=0 / 2 / 3 / 10 (earlier mx GEMM forms),
     attention=30 + kind (force an attention kernel kind). Each call passes its form to the library
     through the mme_*_form entry points; the library itself holds no switch."""
     old = dict(getattr(_forms, "d", {}))

@@ -47,8 +47,15 @@ def encode_e4m3(x: np.ndarray) -> np.ndarray:
     return torch.from_numpy(np.ascontiguousarray(xc)).to(torch.float8_e4m3fn).view(torch.uint8).numpy()
 
 
+def srow(r: np.ndarray) -> np.ndarray:
+    """Position of row r in a scale plane (include/mme.h, round 4): inside each 128-row group, row r
+    is stored at (r % 32) * 4 + (r % 128) // 32 (the 4 rows i * 32 + r of an MFMA lane adjacent)."""
+    r = np.asarray(r)
+    return (r & ~127) | ((r & 31) << 2) | ((r >> 5) & 3)
+
+
 def quantize(x: np.ndarray, rows_pad: int = 0):
-    """x: float32 [R, K] (bf16-valued) -> (q u8 [R, K], scales u8 [K/32, rows_pad])."""
+    """x: float32 [R, K] (bf16-valued) -> (q u8 [R, K], scales u8 [K/32, rows_pad], rows in srow order)."""
     x = np.asarray(x, dtype=np.float32)
     R, K = x.shape
     assert K % 32 == 0
@@ -58,7 +65,7 @@ def quantize(x: np.ndarray, rows_pad: int = 0):
     scaled = np.ldexp(blocks, (127 - sb.astype(np.int32))[:, :, None]).astype(np.float32)
     q = encode_e4m3(scaled.reshape(R, K))
     planes = np.zeros((K // 32, rp), dtype=np.uint8)
-    planes[:, :R] = sb.T
+    planes[:, srow(np.arange(R))] = sb.T
     return q, planes
 
 
@@ -67,7 +74,7 @@ def dequantize(q: np.ndarray, planes: np.ndarray, rows: int) -> np.ndarray:
     tab = e4m3_table().astype(np.float64)
     vals = tab[q[:rows]]
     K = vals.shape[1]
-    sc = np.ldexp(1.0, planes[:, :rows].T.astype(np.int64) - 127)   # [rows, K/32]
+    sc = np.ldexp(1.0, planes[:, srow(np.arange(rows))].T.astype(np.int64) - 127)   # [rows, K/32]
     return vals * np.repeat(sc, 32, axis=1)[:, :K]
 
 

@@ -99,21 +99,28 @@ def hits(s: np.ndarray, tgt_count: int, ks: Sequence[int] = KS, row_offset: int 
     return out
 
 
-def compare_topk(idx: np.ndarray, ref_idx: np.ndarray, ref_score: np.ndarray, rel_tol: float = 1e-5):
+def compare_topk(idx: np.ndarray, ref_idx: np.ndarray, ref_score: np.ndarray, rel_tol: float = 1e-5,
+                 exact_rows: np.ndarray = None):
     """Row-wise parity of a top-k index table against the reference's.
 
     ref_idx / ref_score hold the reference's top-(k+1) per row (score desc). A row is a
     near-tie when two neighbouring scores among those k+1 differ by <= rel_tol·|s_1| but are
     not equal: a different fp32 summation order may legitimately swap them (SURVEY §7,
     "exact-index parity"). EXACT ties are not exempt: their order is torch.topk's, which the
-    device replays. Returns (identical [rows] bool, near_tie [rows] bool); every row that is
-    not a near-tie must be identical. With no (k+1)-th reference column (fewer columns than
-    k + 1) only the gaps that exist are compared."""
+    device replays. exact_rows (bool per row, optional): the rows the compared side itself found
+    exactly tied (mme.retrieval.Ranked.tie_rows); a reference exact tie on any OTHER row is one the
+    compared side's own summation order did not produce (its scores differ by rounding), i.e. a
+    near tie. Returns (identical [rows] bool, near_tie [rows] bool); every row that is not a
+    near-tie must be identical. With no (k+1)-th reference column (fewer columns than k + 1)
+    only the gaps that exist are compared."""
     k = idx.shape[1]
     same = (idx == ref_idx[:, :k]).all(1)
     kk = min(k + 1, ref_score.shape[1])
     gaps = ref_score[:, :kk - 1] - ref_score[:, 1:kk]
-    near = ((gaps <= rel_tol * np.abs(ref_score[:, :1])) & (gaps != 0)).any(1)
+    unequal = gaps != 0
+    if exact_rows is not None:
+        unequal = unequal | ~np.asarray(exact_rows, bool)[:, None]
+    near = ((gaps <= rel_tol * np.abs(ref_score[:, :1])) & unequal).any(1)
     return same, near
 
 

@@ -211,6 +211,28 @@ def test_attention_m32_8wave_skip_vs_kind38(cuda, B, T, H, causal, lens):
     assert nd == 0
 
 
+@pytest.mark.dev
+@pytest.mark.parametrize("kind", [70, 71, 72])
+@pytest.mark.parametrize("B,T,H,causal,lens", SKIP_CASES + [(2, 200, 2, True, None), (1, 64, 2, False, None),
+                                                         (1, 65, 1, False, None)])
+def test_attention_pingpong_bit_identical_to_kind62(cuda, kind, B, T, H, causal, lens):
+    """Dev kinds 70-72 (attn_pp_kernel: kind 62's arithmetic with the block's wave rows one matrix /
+    vector phase apart) run kind 62's per-accumulator MFMA order and VALU sequence: bit-identical."""
+    g = torch.Generator(device="cuda").manual_seed(B * T + 72)
+    qkv = rnd(B * T, 3 * H * 72, scale=1.5, gen=g)
+    sl = None if lens is None else torch.tensor(lens, dtype=torch.int32, device="cuda")
+    outs = []
+    for k in (62, kind, kind):
+        with ops.kernel_forms(attention=30 + k):
+            outs.append(ops.attention(qkv, B, T, H, 72, seq_lens=sl, causal=causal))
+        torch.cuda.synchronize()
+    assert torch.equal(outs[1], outs[2]), "attention is not deterministic"
+    d = (outs[0].float() - outs[1].float()).abs()
+    nd = int((d > 0).sum())
+    assert nd == 0, f"kind {kind} differs from kind 62 on {nd} outputs (max {d.max().item():.3g}, " \
+                    f"first {(d > 0).nonzero()[:4].tolist()})"
+
+
 def test_attention_production_full_grid(cuda):
     """The production hd-72 kernel over the bench's full launch grid (417 images x 16 heads x
     3 query blocks of SigLIP vision; 239 before round 3's larger execution batches) against the fp32

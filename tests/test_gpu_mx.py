@@ -37,7 +37,8 @@ def test_mx_quant_bit_exact(cuda, rows, k):
     q, sc = mx_host(t)
     rq, rsc = omx.quantize(x.float().cpu().numpy(), rows_pad=t.rows_pad)
     assert np.array_equal(q, rq)
-    assert np.array_equal(sc[:, :rows], rsc[:, :rows])
+    pos = omx.srow(np.arange(rows))  # the planes' rows in their stored order
+    assert np.array_equal(sc[:, pos], rsc[:, pos])
 
 
 @pytest.mark.parametrize("rows,d,with_idx", [(5, 1280, False), (300, 1024, False), (37, 1152, True)])
@@ -54,7 +55,8 @@ def test_layernorm_mx_bit_exact(cuda, rows, d, with_idx):
     rq, rsc = omx.quantize(y.float().cpu().numpy(), rows_pad=t.rows_pad)
     q, sc = mx_host(t)
     assert np.array_equal(q, rq)
-    assert np.array_equal(sc[:, :rows], rsc[:, :rows])
+    pos = omx.srow(np.arange(rows))  # the planes' rows in their stored order
+    assert np.array_equal(sc[:, pos], rsc[:, pos])
 
 
 @pytest.mark.parametrize("M,N,K", [(1, 64, 64), (300, 256, 128), (1000, 3840, 1280), (777, 1280, 5120),
@@ -94,7 +96,8 @@ def test_gemm_mx_residual_and_mx_output(cuda):
     rq, rsc = omx.quantize(plain.float().cpu().numpy(), rows_pad=t.rows_pad)
     q, sc = mx_host(t)
     assert np.array_equal(q, rq)
-    assert np.array_equal(sc[:, :M], rsc[:, :M])
+    pos = omx.srow(np.arange(M))
+    assert np.array_equal(sc[:, pos], rsc[:, pos])
 
 
 def test_gemm_mx_rejects_bad_args(cuda):
@@ -223,14 +226,18 @@ def test_gemm_mx9_bit_identical_to_mx(cuda, M, N, K):
         assert torch.equal(o_, n_), f"mx9 differs from the half-line kernel ({what}, {M}x{N}x{K})"
 
 
-# Round 3's fp8 GEMM forms against the round-2 kernel (variant 0): its per-wave epilogue (2), + the
-# single-wave scale DMA (3), and mx10 (production: static slots / waits, buffer-load DMA) run the same
-# MFMA sequence and epilogue arithmetic: bit-identical outputs (bf16 + bias, + residual in place,
-# mx8 re-quantised output with an activation), ragged M and N off the 256 grid included.
+# The fp8 GEMM forms against the round-2 kernel (form 0): its per-wave epilogue (2), + the single-wave
+# scale DMA (3), mx10 (10: static slots / waits, buffer-load DMA) and production (-1: mx11, pipe9's
+# whole-line ring with buffer-loaded scales, where K % 128 == 0 and K >= 384; mx10 elsewhere) run the
+# same MFMA sequence and epilogue arithmetic: bit-identical outputs (bf16 + bias, + residual in
+# place, mx8 re-quantised output with an activation), ragged M and N off the 256 grid included. The
+# K values cover mx11's stage counts 3..12 and 40 (every peel length of its 5-stage unrolled loop).
 @pytest.mark.parametrize("M,N,K,kind", [(1000, 3840, 1280, "bias"), (777, 1280, 5120, "res"),
                                          (2048, 5120, 1280, "mx_out"), (300, 544, 192, "mx_out"),
                                          (129, 96, 192, "res"), (513, 256, 256, "bias"), (300, 512, 320, "res"),
-                                         (257, 768, 448, "mx_out"), (600, 1024, 512, "bias"), (64, 256, 576, "bias")])
+                                         (257, 768, 448, "mx_out"), (600, 1024, 512, "bias"), (64, 256, 576, "bias"),
+                                         (300, 512, 384, "res"), (1000, 1024, 640, "mx_out"), (513, 768, 768, "bias"),
+                                         (257, 1280, 896, "res"), (700, 512, 1024, "mx_out"), (1300, 768, 1536, "res")])
 def test_gemm_mx_wave_epilogue_bit_identical(cuda, M, N, K, kind):
     g = torch.Generator(device="cuda").manual_seed(M + N + K)
     a = mx.quantize(rnd(M, K, gen=g))
@@ -238,12 +245,12 @@ def test_gemm_mx_wave_epilogue_bit_identical(cuda, M, N, K, kind):
     bias = rnd(N, scale=0.1, gen=g)
     res0 = rnd(M, N, gen=g)
     outs = []
-    for v in (0, 2, 3, -1):  # round-2 form, + per-wave epilogue, + single-wave scale DMA, production (mx10)
+    for v in (0, 2, 3, 10, -1):  # round-2 form, + per-wave epilogue, + single-wave scale DMA, mx10, production
         with ops.kernel_forms(mx=v):
             if kind == "mx_out":
                 o = mx.MXTensor.empty(M, N, "cuda")
                 mx.gemm(a, w, bias, act=_lib.ACT_QUICK_GELU, out_mx=o)
-                outs.append((o.q[:M, :N].clone(), o.scales[:, :M].clone()))
+                outs.append((o.q[:M, :N].clone(), o.scales[:, torch.from_numpy(omx.srow(np.arange(M))).cuda()].clone()))
             else:
                 x = res0.clone()
                 y = mx.gemm(a, w, bias, residual=x if kind == "res" else None, out=x)
@@ -251,4 +258,4 @@ def test_gemm_mx_wave_epilogue_bit_identical(cuda, M, N, K, kind):
         torch.cuda.synchronize()
     for o in outs[1:]:
         for p, q in zip(outs[0], o):
-            assert torch.equal(p, q), f"per-wave mx epilogue / single-wave scale DMA differs ({kind}, {M}x{N}x{K})"
+            assert torch.equal(p, q), f"mx GEMM form differs from the round-2 kernel ({kind}, {M}x{N}x{K})"

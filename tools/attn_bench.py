@@ -5,17 +5,14 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "multimodal-embedding_amd"))
-import ctypes  # noqa: E402
-
 import torch  # noqa: E402
-from mme import _lib, ops  # noqa: E402
+from mme import ops  # noqa: E402
 
-# --variants 0,1,...: 0 = production dispatch; 1-4 dev diagnostic builds of the hd-72 register-
-# staged kernel (1 no K/V loads, 2 no exp2, 3 no PV MFMA, 4 no QK MFMA; wrong results);
-# 9 / 10 / 11 force the register-staged / LDS-DMA 4-wave / LDS-DMA 8-wave kernel
+# --variants 0,F,...: per-call attention forms (ops.kernel_forms(attention=F)): 0 = production
+# dispatch, 30 + kind = force kernel kind `kind` (dev kinds need MME_DEV=1: libmme_dev.so).
+# --batch B overrides every case's batch (e.g. 417 = the SigLIP job's execution batch).
 VARIANTS = [int(v) for v in sys.argv[sys.argv.index("--variants") + 1].split(",")] if "--variants" in sys.argv else [0]
-lib = _lib.load()
-lib.mme_attention_variant.argtypes = [ctypes.c_int]
+BATCH = int(sys.argv[sys.argv.index("--batch") + 1]) if "--batch" in sys.argv else None
 
 CASES = [  # name, B, T, H, hd, causal
     ("siglip_vision", 256, 729, 16, 72, False),
@@ -30,29 +27,32 @@ CASES = [  # name, B, T, H, hd, causal
 if "--cases" in sys.argv:
     _want = sys.argv[sys.argv.index("--cases") + 1].split(",")
     CASES = [c for c in CASES if c[0] in _want]
+def run(v, *args, **kw):
+    with ops.kernel_forms(**({"attention": v} if v else {})):
+        return ops.attention(*args, **kw)
+
+
 for (name, B, T, H, hd, causal), v in [(c, v) for c in CASES for v in VARIANTS]:
-    if (1 <= v <= 4 or 21 <= v <= 26) and (hd != 72 or (v >= 21 and T < 256)):
-        continue
+    B = BATCH or B
     torch.manual_seed(0)
     qkv = torch.randn(B * T, 3 * H * hd, device="cuda").to(torch.bfloat16)
     out = torch.empty(B * T, H * hd, device="cuda", dtype=torch.bfloat16)
-    lib.mme_attention_variant(0)
-    ref = ops.attention(qkv, B, T, H, hd, causal=causal).float()
-    lib.mme_attention_variant(v)
-    ops.attention(qkv, B, T, H, hd, causal=causal, out=out)
+    ref = run(0, qkv, B, T, H, hd, causal=causal)
+    run(v, qkv, B, T, H, hd, causal=causal, out=out)
     torch.cuda.synchronize()
-    err = (out.float() - ref).abs().max().item()
+    err = (out.float() - ref.float()).abs().max().item()
+    same = bool(torch.equal(out, ref))
     s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     it = 5
     for _ in range(3):  # warm the clocks / caches for this variant
-        ops.attention(qkv, B, T, H, hd, causal=causal, out=out)
+        run(v, qkv, B, T, H, hd, causal=causal, out=out)
     ms = 1e30
     for rep in range(3):  # best of 3 timed groups
         s.record()
         for _ in range(it):
-            ops.attention(qkv, B, T, H, hd, causal=causal, out=out)
+            run(v, qkv, B, T, H, hd, causal=causal, out=out)
         e.record()
         torch.cuda.synchronize()
         ms = min(ms, s.elapsed_time(e) / it)
     fl = 4.0 * B * H * T * T * hd * (0.5 if causal else 1.0)
-    print(f"{name:18s} v{v} B={B} T={T} H={H} hd={hd}: {ms:7.3f} ms {fl / ms / 1e9:7.1f} TFLOP/s  maxdiff vs v0 {err:.3g}", flush=True)
+    print(f"{name:18s} v{v} B={B} T={T} H={H} hd={hd}: {ms:7.3f} ms {fl / ms / 1e9:7.1f} TFLOP/s  maxdiff vs v0 {err:.3g} identical {same}", flush=True)

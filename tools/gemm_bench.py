@@ -1,12 +1,11 @@
 #!/usr/bin/env python3
 """GEMM microbenchmark on the SigLIP-400M encoder shapes (HIP-event timed).
 
-Usage: python tools/gemm_bench.py [--rows 186624] [--iters 10] [--variant V]
-Prints per-shape ms and TFLOP/s; --variant selects a dev kernel variant
-(mme_gemm_variant) when the library exposes one.
+Usage: python tools/gemm_bench.py [--rows 186624] [--iters 10] [--variants V,..] [--mx --mx-variants F,..]
+Prints per-shape ms and TFLOP/s; --variants / --mx-variants are per-call kernel forms
+(ops.kernel_forms; dev-only forms need MME_DEV=1, i.e. libmme_dev.so).
 """
 import argparse
-import ctypes
 import json
 import os
 import sys
@@ -31,19 +30,14 @@ def main():
     p.add_argument("--variants", default="")
     p.add_argument("--shapes", default="qkv,o_proj,fc1,fc2")
     p.add_argument("--mx", action="store_true", help="also time the mx8 (block-scaled fp8) GEMM")
-    p.add_argument("--mx-variants", default="-1", help="mme_gemm_mx_variant values to time with --mx "
-                   "(-1 = production, 0 = round-2 form, 2 = per-wave epilogue alone, 9 = mx9 in libmme_dev.so)")
+    p.add_argument("--mx-variants", default="-1", help="mx GEMM forms to time with --mx (-1 = production, "
+                   "10 = mx10, 0 = round-2 form, 2 = per-wave epilogue alone, 3 = + scale wave; dev: 4, 9)")
     p.add_argument("--mx-epi", default="none", help="mx8 epilogue: none | job (the fp8 job's: QKV bias, fc1 "
                    "bias + quick_gelu to an mx8 output, fc2 bias + residual in place)")
     p.add_argument("--torch", action="store_true", help="also time torch F.linear (hipBLASLt) on each shape")
     p.add_argument("--epi", default="none", help="epilogue: none | bias | res (residual in place) | resstats (res + LayerNorm "
                    "statistics, mme_gemm_res_stats) | gelu (bias+gelu_tanh)")
     a = p.parse_args()
-    lib = _lib.load()
-    has_var = hasattr(lib, "mme_gemm_variant")
-    if has_var:
-        lib.mme_gemm_variant.restype = ctypes.c_int
-        lib.mme_gemm_variant.argtypes = [ctypes.c_int]
     variants = [int(v) for v in a.variants.split(",")] if a.variants else [-1]
     g = torch.Generator(device="cuda").manual_seed(0)
     M = a.rows
@@ -61,15 +55,17 @@ def main():
         st = torch.empty(M, 2, device="cuda")
         part = torch.empty(M, max(1, N // 64), 2, device="cuda")
 
+        form = {"v": None}
+
         def run():
-            if a.epi == "resstats":
-                ops.gemm_res_stats(A, W, bias, C, 1e-6, st, part, out=C)
-            else:
-                ops.gemm(A, W, out=C, **kw)
+            with ops.kernel_forms(**({} if form["v"] is None else {"gemm": form["v"]})):
+                if a.epi == "resstats":
+                    ops.gemm_res_stats(A, W, bias, C, 1e-6, st, part, out=C)
+                else:
+                    ops.gemm(A, W, out=C, **kw)
         ref = None
         for v in variants:
-            if has_var:
-                lib.mme_gemm_variant(v)  # -1 = production dispatch
+            form["v"] = None if v == -1 else v  # -1 = production dispatch
             run()
             err = float("nan")
             if ref is None or a.epi in ("res", "resstats"):
@@ -116,7 +112,6 @@ def main():
             del Ct
         if a.mx:
             from mme import mx
-            lib.mme_gemm_mx_variant.argtypes = [ctypes.c_int]
             Aq, Wq = mx.quantize(A), mx.quantize(W)
             mkw, omx = {}, None
             if a.mx_epi == "job":
@@ -130,11 +125,16 @@ def main():
                 mkw["out"] = C
             first = None
             C0 = C.clone()  # the in-place residual's operand, restored before every variant's check
+            r = torch.arange(M, device="cuda")
+            srow = (r & ~127) | ((r & 31) << 2) | ((r >> 5) & 3)  # scale-plane position of row r (include/mme.h)
+
+            def mrun(mv):
+                with ops.kernel_forms(**({} if mv == -1 else {"mx": mv})):
+                    return mx.gemm(Aq, Wq, **mkw)
             for mv in [int(v) for v in a.mx_variants.split(",")]:
-                lib.mme_gemm_mx_variant(mv)
                 C.copy_(C0)
-                Cm = mx.gemm(Aq, Wq, **mkw)
-                snap = (omx.q.clone(), omx.scales[:, :M].clone()) if omx is not None else (Cm.clone(),)
+                Cm = mrun(mv)
+                snap = (omx.q.clone(), omx.scales[:, srow].clone()) if omx is not None else (Cm.clone(),)
                 if omx is None:
                     err = (Cm.float() - ref.float()).abs().max().item() if ref is not None and not a.mx_epi == "job" else 0.0
                 else:
@@ -143,14 +143,14 @@ def main():
                     first = snap
                 same = all(bool(torch.equal(x, y)) for x, y in zip(snap, first))
                 for _ in range(3):
-                    mx.gemm(Aq, Wq, **mkw)
+                    mrun(mv)
                 torch.cuda.synchronize()
                 s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 ms = 1e30
                 for rep in range(3):  # best of 3 timed groups
                     s.record()
                     for _ in range(a.iters):
-                        mx.gemm(Aq, Wq, **mkw)
+                        mrun(mv)
                     e.record()
                     torch.cuda.synchronize()
                     ms = min(ms, s.elapsed_time(e) / a.iters)
@@ -158,9 +158,6 @@ def main():
                 res[f"{name}/mx{mv}"] = {"ms": round(ms, 4), "tflops": round(tf, 1)}
                 print(f"{name:7s} mx8 v{mv:<2d} M={M} N={N} K={K}: {ms:8.3f} ms  {tf:7.1f} TFLOP/s  "
                       f"(max |mx - bf16| {err:.3g}, identical to first mx variant: {same})", flush=True)
-            lib.mme_gemm_mx_variant(-1)
-    if has_var:
-        lib.mme_gemm_variant(-1)
     print(json.dumps(res))
 
 
