@@ -222,6 +222,38 @@ def retrieval_parity(tables, metrics, caps_per_image: int = 5):
             "seconds": round(time.time() - t0, 2)}
 
 
+def fp8_drift(model_name, dev, imgs, t2i_ids, cap_ids, fp8_tables, img_batch, txt_batch, caps: int = 5):
+    """fp8 against bf16 over the WHOLE job (checker; after the timed region, --fp8 only): the same
+    weights (seed 0) loaded without the mx8 GEMMs encode the job's images and captions, and the
+    job's fp8 tables are compared with them: per-row cosine of the embeddings, and the I2T ranking
+    (every image against all 5n captions, mme_sim_topk) as top-1 agreement and top-10 overlap.
+    tests/test_gpu_mx.py asserts the same quantities (FP8_DRIFT) on a production batch."""
+    from mme import ops
+    from mme.models import load_model
+    t0 = time.time()
+    bf, _ = load_model(model_name, seed=0, device=dev, fp8=False)
+    img = bf.encode_images(imgs, batch=img_batch)
+    t2i = bf.encode_texts(t2i_ids, exec_batch=txt_batch)
+    allc = bf.encode_texts(cap_ids, exec_batch=txt_batch)
+    del bf
+
+    def cos(a, b):
+        a, b = a.float(), b.float()
+        return (a * b).sum(1) / (a.norm(dim=1) * b.norm(dim=1)).clamp_min(1e-30)
+    ci, ct, ca = cos(fp8_tables["img"], img), cos(fp8_tables["t2i"], t2i), cos(fp8_tables["all"], allc)
+    i8, _ = ops.sim_topk(fp8_tables["img"], fp8_tables["all"], 10)
+    i16, _ = ops.sim_topk(img, allc, 10)
+    top1 = (i8[:, 0] == i16[:, 0]).float().mean().item()
+    ov = (i8[:, :, None] == i16[:, None, :]).any(2).float().mean().item()
+    torch.cuda.synchronize()
+    return {"images": int(img.shape[0]), "captions": int(allc.shape[0]),
+            "cos_img_min": round(ci.min().item(), 5), "cos_img_mean": round(ci.mean().item(), 5),
+            "cos_txt_min": round(min(ct.min().item(), ca.min().item()), 5),
+            "cos_txt_mean": round(ca.mean().item(), 5),
+            "i2t_top1_agreement": round(top1, 4), "i2t_top10_overlap": round(ov, 4),
+            "checker": "the same weights in bf16 (mme, no mx8 GEMMs) over the whole job", "seconds": round(time.time() - t0, 2)}
+
+
 def encoder_parity(spec, imgs_u8, cap_ids, dev_img, dev_txt, bar: float = 0.999):
     """Encoder parity of the headline job (checker; after the timed region): the job's own images and
     T2I captions at the first, middle and last rows encoded by the fp32 oracle (oracle/encoders.py: the PIL-exact processor and the
@@ -654,7 +686,7 @@ def main():
     if fam in kt:
         # dominant kernel family: mme_gemm (gemm_pipe9_kernel; gemm_pipe6_kernel where K % 64 != 0;
         # gemm_tn_kernel for the few small shapes),
-        # or with --fp8 mme_gemm_mx (gemm_mx_kernel, block-scaled fp8 MFMA; dense fp8 peak).
+        # or with --fp8 mme_gemm_mx (gemm_mx11_kernel since round 4, block-scaled fp8 MFMA; dense fp8 peak).
         # achieved = algorithmic FLOPs per launch (2*M*N*K, zero-padding excluded) / average launch time
         # from HIP events recorded on the launch stream over the timed region.
         g = kt[fam]
@@ -662,7 +694,7 @@ def main():
         achieved = g["flops"] / (g["ms"] / 1e3) / 1e12
         peak = MFMA_FP8_PEAK_TFLOPS if args.fp8 else MFMA_BF16_PEAK_TFLOPS
         roofline = {"bound": "mfma",
-                    "kernel": "mme_gemm_mx (gemm_mx_kernel)" if args.fp8 else "mme_gemm (gemm_pipe9_kernel)",
+                    "kernel": "mme_gemm_mx (gemm_mx11_kernel)" if args.fp8 else "mme_gemm (gemm_pipe9_kernel)",
                     "achieved": round(achieved, 1), "peak": peak, "unit": "TFLOP/s", "frac": round(achieved / peak, 4),
                     "traffic": None, "launches": g["launches"], "avg_launch_ms": round(avg_ms, 4),
                     "algorithmic_bytes_per_launch": round(g["bytes"] / g["launches"]),
@@ -730,6 +762,9 @@ def main():
             out["parity"]["encoders"] = encoder_parity(spec, my_imgs[ii], my_t2i[ii], last["img"][ii], last["t2i"][ii],
                                                        bar=0.99 if args.fp8 else 0.999)
             out["parity"]["encoders"]["rows"] = enc_idx
+        if args.fp8 and world == 1:
+            out["fp8_drift"] = fp8_drift(args.model, dev, my_imgs, my_t2i, my_caps, last["tables"], args.img_batch,
+                                         args.txt_batch, caps)
     if args.host_inputs:
         host_imgs = my_imgs.cpu().pin_memory()
         barrier()

@@ -1361,10 +1361,12 @@ __global__ __launch_bounds__(256, 2) void attn_short_pf_kernel(AttnArgs a, int u
 // ---------------------------------------------------------------------------
 // SKIP (round 3, kind 65): a tile whose second 32-key block lies wholly past the keys skips
 // that block's QK^T and PV MFMAs, as attn_hyb_kernel's kind 62 does at hd 72 -- ViT-H
-// (T = 257 = 4 x 64 + 1) ends in such a tile (1/10 of the key blocks). Its P is 0, yet the
-// outputs are not bit-identical to the unskipped kernel: an MFMA whose B operand is all zero
-// still changes the accumulator it passes through in rare cases (1-15 of 0.7-1.3 M outputs
-// differ, by one or two bf16 ulps; test_attention_m32_skip). The same skip in 8-wave blocks (DFN5B,
+// (T = 257 = 4 x 64 + 1) ends in such a tile (1/10 of the key blocks). Its P is 0, and an MFMA
+// with an all-zero operand leaves its accumulator bit-identical (tools/mfma_zero_probe.hip, round 4),
+// so the skip is exact; yet 0-18 of 0.1-3.7 M outputs differ from the unskipped kernel by one bf16
+// ulp, a deterministic code-generation effect of these compiled loops (printf instrumentation of the
+// unskipped kernel alone moves outputs the same way; DESIGN.md §4 round 4, test_attention_skip_vs_
+// unskipped). The same skip in 8-wave blocks (DFN5B,
 // T = 730) measured 18 % slower than kind 38 (0.59 vs 0.50 ms, profiles/r03_v11_attn_dfn5b_ab.log)
 // and is not built.
 template <int HD, int NW, int MINW, bool PRIO, bool DPV = false, bool PF = false, bool SKIP = false>
@@ -2061,7 +2063,9 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(2))) vo
 // SKIP: 0 none; 1 = a tile whose second 32-key block lies wholly past the keys skips that
 // block's MFMAs (round 2's kind 62, now dev kind 63); 2 = the same with literal-zero accumulator
 // starts (production kind 62 since round 3).
-template <int HD, int NW, int MINW, bool PRIO, int SKIP = 0>
+// DBG (dev kinds 76 / 77, round 4): printf trace of one (batch 1, head 8, query 334) through the
+// tile loop -- running max, two O^T elements (d 7, d 22) and the weight sum -- per tile.
+template <int HD, int NW, int MINW, bool PRIO, int SKIP = 0, bool DBG = false>
 __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(MINW))) void attn_hyb_kernel(AttnArgs a) {
     static_assert(HD == 72 || HD == 80, "80-deep QK^T, 80 PV rows");
     constexpr bool ONES = HD == 72;  // hd 72: V^T row 72 = ones (weight sums); hd 80: f32 sums
@@ -2153,8 +2157,8 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(MINW)))
 
     auto tile_step = [&](int t, const unsigned so) __attribute__((always_inline)) {
         // SKIP: a tile whose second 32-key block lies wholly past the keys (the last tile at
-        // T = 729) skips that block's QK^T and PV MFMAs; its P is 0 either way (outputs may still
-        // differ from the unskipped kernel by a bf16 ulp in rare cases: see attn_m32_kernel's SKIP)
+        // T = 729) skips that block's QK^T and PV MFMAs; its P is 0 either way (exact: see
+        // attn_m32_kernel's SKIP for the rare 1-ulp code-generation differences)
         const bool half = SKIP && t * 64 + 32 >= Tk;
         f32x16 sc[2];
         if (SKIP == 2) {
@@ -2200,6 +2204,11 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(MINW)))
             sc[kb] = z;
         }
         }
+        if (DBG && b == 1 && h == 8 && qb == 1 && wave == 2 && t == 1 && (lane == 14 || lane == 46))
+            for (int kb = 0; kb < 2; ++kb)
+                printf("K%d S lane %d kb %d: %a %a %a %a %a %a %a %a %a %a %a %a %a %a %a %a\n", SKIP, lane, kb,
+                       sc[kb][0], sc[kb][1], sc[kb][2], sc[kb][3], sc[kb][4], sc[kb][5], sc[kb][6], sc[kb][7],
+                       sc[kb][8], sc[kb][9], sc[kb][10], sc[kb][11], sc[kb][12], sc[kb][13], sc[kb][14], sc[kb][15]);
         if ((t * 64 + 64 > Tk) || (a.causal && t * 64 + 63 > qw0)) {
             const int q = qw0 + r;
             const int lim = a.causal ? min(Tk, q + 1) : Tk;
@@ -2228,6 +2237,8 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(MINW)))
         }
         m = mnew;
         const float mc = mnew * c;
+        if (DBG && b == 1 && h == 8 && qb == 1 && wave == 2 && t == 1 && (lane == 14 || lane == 46))
+            printf("K%d mc lane %d: m %a c %a mc %a\n", SKIP, lane, mnew, c, mc);
         float psum = 0.f;
 #pragma unroll
         for (int kb = 0; kb < 2; ++kb)
@@ -2237,6 +2248,11 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(MINW)))
                 if (!ONES) psum += sc[kb][e];
             }
         if (!ONES) lsum += psum;
+        if (DBG && b == 1 && h == 8 && qb == 1 && wave == 2 && t == 1 && (lane == 14 || lane == 46))
+            for (int kb = 0; kb < 2; ++kb)
+                printf("K%d E lane %d kb %d: %a %a %a %a %a %a %a %a %a %a %a %a %a %a %a %a\n", SKIP, lane, kb,
+                       sc[kb][0], sc[kb][1], sc[kb][2], sc[kb][3], sc[kb][4], sc[kb][5], sc[kb][6], sc[kb][7],
+                       sc[kb][8], sc[kb][9], sc[kb][10], sc[kb][11], sc[kb][12], sc[kb][13], sc[kb][14], sc[kb][15]);
 #pragma unroll
         for (int kb = 0; kb < 2; ++kb) {
             if (kb == 1 && half) break;
@@ -2258,6 +2274,9 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(MINW)))
             }
             const bf16x8 pb0 = __builtin_bit_cast(bf16x8, make_uint4(b0w[0], b0w[1], b0w[2], b0w[3]));
             const bf16x8 pb1 = __builtin_bit_cast(bf16x8, make_uint4(b1w[0], b1w[1], b1w[2], b1w[3]));
+            if (DBG && b == 1 && h == 8 && qb == 1 && wave == 2 && t == 1 && (lane == 14 || lane == 30 || lane == 46))
+                printf("K%d P lane %d kb %d: %08x %08x %08x %08x | %08x %08x %08x %08x\n", SKIP, lane, kb, b0w[0], b0w[1],
+                       b0w[2], b0w[3], b1w[0], b1w[1], b1w[2], b1w[3]);
 #pragma unroll
             for (int dt = 0; dt < NDT; ++dt) {
                 const unsigned off = so + kb * 512 + dt * 2048;
@@ -2270,6 +2289,13 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(MINW)))
         }
     };
 
+    const bool dbg = DBG && b == 1 && h == 8 && qb == 1 && wave == 2;
+    auto trace = [&](int t) {
+        if (!dbg) return;
+        if (lane == 14) printf("K%d t %2d m %a\n", SKIP, t, m);
+        if (lane == 30) printf("K%d t %2d o7 %a o22 %a\n", SKIP, t, o[0][0][3], o[0][1][2]);
+        if (lane == 46) printf("K%d t %2d sum %a\n", SKIP, t, o[0][4][0]);
+    };
     if (PRIO && wave >= NW / 2) __builtin_amdgcn_s_setprio(1);
     if (nkt > 0) issue(0);
     for (int t = 0; t < nkt; t += 2) {
@@ -2277,11 +2303,13 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(MINW)))
         __builtin_amdgcn_s_barrier();
         if (t + 1 < nkt) issue(t + 1);
         tile_step(t, 0);
+        if (DBG) trace(t);
         if (t + 1 < nkt) {
             vm_wait<0>();
             __builtin_amdgcn_s_barrier();
             if (t + 2 < nkt) issue(t + 2);
             tile_step(t + 1, TILE);
+            if (DBG) trace(t + 1);
         }
     }
 
@@ -2907,6 +2935,15 @@ bool launch_attn_dev(int kind, const AttnArgs& a, int B, int T, int H, hipStream
                               // at DFN5B T 730; the pair whose rare 1-ulp difference round 3 recorded)
         hipLaunchKernelGGL((attn_m32_kernel<HD, 8, 1, true, false, false, true>), dim3(cdiv(T, 256) * H * B), dim3(512),
                            0, st, a);
+    } else if (kind == 76 || kind == 77) {  // dev: kinds 58 / 62 with the printf trace (DBG)
+        if constexpr (HD == 72) {
+            if (kind == 76)
+                hipLaunchKernelGGL((attn_hyb_kernel<HD, 8, 4, true, 0, true>), dim3(cdiv(T, 256) * H * B), dim3(512), 0, st, a);
+            else
+                hipLaunchKernelGGL((attn_hyb_kernel<HD, 8, 4, true, 2, true>), dim3(cdiv(T, 256) * H * B), dim3(512), 0, st, a);
+        } else {
+            return false;
+        }
     } else if (kind == 63) {  // dev: kind 62 as in round 2 (the skipped block's fill and the accumulator
                               // init as per-tile register moves)
         if constexpr (HD != 64)

@@ -131,7 +131,9 @@ def test_fp8_towers_tiny_vs_reference(cuda, golden, name):
 # fp8-vs-bf16 drift bounds on DFN5B-H's production batch (random weights, seeded): the bf16 row is
 # the reference's precision, so these bound what --fp8 changes in the embeddings and rankings.
 FP8_DRIFT = {"cos_img_min": 0.995, "cos_img_mean": 0.997, "cos_txt_min": 0.99, "cos_txt_mean": 0.994,
-             "i2t_top1_agreement": 0.92, "i2t_top10_overlap": 0.72}
+             "i2t_top1_agreement": 0.92, "i2t_top10_overlap": 0.72,
+             # the whole production batch (round 4; measured r03 0.916 / 0.721 at 500 x 2 500)
+             "i2t_top1_agreement_batch": 0.88, "i2t_top10_overlap_batch": 0.68}
 
 
 @pytest.mark.slow
@@ -187,6 +189,7 @@ def test_fp8_dfn5b_full_size_vs_oracle(cuda, monkeypatch):
     assert ci.min() >= FP8_DRIFT["cos_img_min"] and ci.mean() >= FP8_DRIFT["cos_img_mean"]
     assert ct.min() >= FP8_DRIFT["cos_txt_min"] and ct.mean() >= FP8_DRIFT["cos_txt_mean"]
     assert top1 >= FP8_DRIFT["i2t_top1_agreement"] and over >= FP8_DRIFT["i2t_top10_overlap"]
+    assert top1_all >= FP8_DRIFT["i2t_top1_agreement_batch"] and over_all >= FP8_DRIFT["i2t_top10_overlap_batch"]
     del bf
     sd_cpu = {k: v.float().cpu() for k, v in sd.items()}
     del sd
