@@ -915,25 +915,31 @@ int launch_pipe6(const GemmArgs& a, hipStream_t s) {
 // group: conflict-free both ways. The round-2/3 layout (pitch 144 B, 18 KiB) was 2-way on both
 // (rows li and li + 8 share banks for the writes; rows r and r + 1 for the reads): 19 M
 // SQ_LDS_BANK_CONFLICT cycles per fc1 launch (profiles/r03_v12_pmc_gemm_util_fc1.json).
-template <class C, int ACT, bool SWZ = true>
+// PASSES (pipe10, round 4): the sub-tile staged and stored in PASSES row bands through a region of
+// 128 / PASSES rows per wave (2: 8 KiB per wave, 64 KiB for the block, two of the five ring units).
+template <class C, int ACT, bool SWZ = true, int PASSES = 1>
 __device__ __forceinline__ void gemm_epilogue_wave(const GemmArgs& p, char* lds, f32x4 (&acc)[C::FM][C::FN], int m0,
                                                    int n0, int wave, int wm, int wn, int g, int li, int lane) {
     static_assert(C::TM == 128 && C::TN == 64 && C::FM == 8 && C::FN == 4, "per-wave epilogue: 128 x 64 wave tiles");
+    static_assert(PASSES == 1 || (PASSES == 2 && SWZ), "one or two staging passes");
     constexpr bool GLU = ACT == MME_ACT_GEGLU_TANH;
     constexpr int RACT = GLU ? MME_ACT_NONE : ACT;
-    constexpr int PITCH = SWZ ? 128 : 144, REGION = 128 * PITCH;
+    constexpr int PITCH = SWZ ? 128 : 144, REGION = 128 * PITCH / PASSES, BAND = 128 / PASSES;
     char* reg = lds + wave * REGION;
     const int rm0 = m0 + wm * C::TM, cn0 = n0 + wn * C::TN;  // this wave's sub-tile origin
     const int rr = lane >> 3, cc = lane & 7;                 // store phase: row rr of 8, 16-B chunk cc
-    u16x8 rv[16];
-    if (!GLU && p.res) {  // residual rows first: their latency overlaps the staging below
+    u16x8 rv[16 / PASSES];  // residual rows of the current pass (all 16 row groups with one pass)
+    auto load_res = [&](int ps) __attribute__((always_inline)) {
+        if (!GLU && p.res) {  // residual rows first: their latency overlaps the staging below
 #pragma unroll
-        for (int q = 0; q < 16; ++q) {
-            const int gr = min(rm0 + q * 8 + rr, p.M - 1), gc = min(cn0 + cc * 8, p.N - 8);
-            const int r2 = p.res_period ? gr % p.res_period : gr;
-            rv[q] = *reinterpret_cast<const u16x8*>(p.res + (size_t)r2 * p.ldr + gc);
+            for (int q = 0; q < 16 / PASSES; ++q) {
+                const int gr = min(rm0 + (ps * (16 / PASSES) + q) * 8 + rr, p.M - 1), gc = min(cn0 + cc * 8, p.N - 8);
+                const int r2 = p.res_period ? gr % p.res_period : gr;
+                rv[q] = *reinterpret_cast<const u16x8*>(p.res + (size_t)r2 * p.ldr + gc);
+            }
         }
-    }
+    };
+    if constexpr (PASSES == 1) load_res(0);
     float lr[C::FM], lm[C::FM];
     if (p.ln_stats) {
 #pragma unroll
@@ -945,21 +951,23 @@ __device__ __forceinline__ void gemm_epilogue_wave(const GemmArgs& p, char* lds,
         }
     }
 #pragma unroll
+    for (int ps = 0; ps < PASSES; ++ps) {
+    if constexpr (PASSES > 1) load_res(ps);
+#pragma unroll
     for (int j = 0; j < C::FN; ++j) {
-        const int nl = j * 16 + 4 * g;  // within the wave's 64 columns
         float bv[4] = {0.f, 0.f, 0.f, 0.f}, cs[4] = {0.f, 0.f, 0.f, 0.f};
         if (p.ln_stats) {
-            const int c4 = min(cn0 + nl, p.N - 4);
+            const int c4 = min(cn0 + j * 16 + 4 * g, p.N - 4);
             const float4 b4 = *reinterpret_cast<const float4*>(p.ln_b + c4);
             const float4 s4 = *reinterpret_cast<const float4*>(p.ln_cs + c4);
             bv[0] = b4.x, bv[1] = b4.y, bv[2] = b4.z, bv[3] = b4.w;
             cs[0] = s4.x, cs[1] = s4.y, cs[2] = s4.z, cs[3] = s4.w;
         } else if (p.bias) {
 #pragma unroll
-            for (int r = 0; r < 4; ++r) bv[r] = bf2f(p.bias[min(cn0 + nl + r, p.N - 1)]);
+            for (int r = 0; r < 4; ++r) bv[r] = bf2f(p.bias[min(cn0 + j * 16 + 4 * g + r, p.N - 1)]);
         }
 #pragma unroll
-        for (int i = 0; i < C::FM; ++i) {
+        for (int i = ps * (C::FM / PASSES); i < (ps + 1) * (C::FM / PASSES); ++i) {
             bf16x4 o;
             if (p.ln_stats) {
 #pragma unroll
@@ -981,21 +989,21 @@ __device__ __forceinline__ void gemm_epilogue_wave(const GemmArgs& p, char* lds,
                 }
             }
             if constexpr (SWZ)  // chunk 2 j + g / 2 ^ (row & 7), half (g & 1) ^ (row >> 3 & 1); row & 15 = li
-                *reinterpret_cast<bf16x4*>(reg + (i * 16 + li) * PITCH + (((2 * j + (g >> 1)) ^ (li & 7)) << 4) +
-                                           (((g & 1) ^ (li >> 3)) << 3)) = o;
+                *reinterpret_cast<bf16x4*>(reg + (i * 16 + li - ps * BAND) * PITCH +
+                                           (((2 * j + (g >> 1)) ^ (li & 7)) << 4) + (((g & 1) ^ (li >> 3)) << 3)) = o;
             else
-                *reinterpret_cast<bf16x4*>(reg + (i * 16 + li) * PITCH + nl * 2) = o;
+                *reinterpret_cast<bf16x4*>(reg + (i * 16 + li) * PITCH + (j * 16 + 4 * g) * 2) = o;
         }
     }
     // the wave's own LDS writes precede its reads (LDS executes one wave's instructions in order)
     bf16* Cout = reinterpret_cast<bf16*>(p.C);
 #pragma unroll
-    for (int q = 0; q < 16; ++q) {
+    for (int q = ps * (16 / PASSES); q < (ps + 1) * (16 / PASSES); ++q) {
         const int row = q * 8 + rr;
         const int gr = rm0 + row, gc = cn0 + cc * 8;
         u16x8 v;
         if constexpr (SWZ) {  // row & 7 = rr; bit 3 of the row = q & 1 (a static half swap)
-            const u16x8 w = *reinterpret_cast<const u16x8*>(reg + row * PITCH + ((cc ^ rr) << 4));
+            const u16x8 w = *reinterpret_cast<const u16x8*>(reg + (row - ps * BAND) * PITCH + ((cc ^ rr) << 4));
             v = (q & 1) ? u16x8{w[4], w[5], w[6], w[7], w[0], w[1], w[2], w[3]} : w;
         } else {
             v = *reinterpret_cast<const u16x8*>(reg + row * PITCH + cc * 16);
@@ -1011,7 +1019,8 @@ __device__ __forceinline__ void gemm_epilogue_wave(const GemmArgs& p, char* lds,
         } else if (p.res) {
             u16x8 o;
 #pragma unroll
-            for (int e = 0; e < 8; ++e) o[e] = __builtin_bit_cast(unsigned short, f2bf(bits2f(v[e]) + bits2f(rv[q][e])));
+            for (int e = 0; e < 8; ++e)
+                o[e] = __builtin_bit_cast(unsigned short, f2bf(bits2f(v[e]) + bits2f(rv[q - ps * (16 / PASSES)][e])));
             __builtin_nontemporal_store(o, reinterpret_cast<u16x8*>(Cout + (size_t)gr * p.ldc + gc));
             if (p.row_part) {  // the wave's 64 columns of this row = one statistics slice (gemm_epilogue_lds)
                 float xf[8], sum = 0.f;
@@ -1030,6 +1039,7 @@ __device__ __forceinline__ void gemm_epilogue_wave(const GemmArgs& p, char* lds,
             __builtin_nontemporal_store(v, reinterpret_cast<u16x8*>(Cout + (size_t)gr * p.ldc + gc));
         }
     }
+    }  // passes
 }
 
 // ---------------------------------------------------------------------------
@@ -1366,6 +1376,245 @@ __global__ __launch_bounds__(C::NT, 2) void gemm_pipe9_kernel(GemmArgs p) {
         pipe9_tile<C, ACT, true, PRIO, ESWZ>(p, lds, m0, n0, wave);
     else
         pipe9_tile<C, ACT, false, PRIO, ESWZ>(p, lds, m0, n0, wave);
+}
+
+// ---------------------------------------------------------------------------
+// pipe10 (round 4): persistent pipe9. One 8-wave workgroup per CU walks the tiles
+// v = blockIdx.x, + gridDim.x, ... in pipe9's order (xcd_remap of the same ids, so every tile runs
+// on the XCD it would run on as a pipe9 block); per tile pipe9's main loop, K order and MFMAs
+// unchanged (bit-identical outputs). What changes is the seam between tiles, which costs pipe9
+// ~17 % of an fc1 launch (tools/gemm_bench.py at K = 1 152 / 2 304 / 4 608: 2.33 / 4.29 / 8.14 ms):
+// the next tile's first three units are DMA'd into ring slots 0-2 as soon as this tile's last
+// fragment reads are done, i.e. under its epilogue, which stages through slots 3-4 only (two
+// 64-row passes, 8 KiB per wave); after the epilogue (and its stores) every wave waits for its own
+// loads, one barrier frees slots 3-4 and units 3-4 follow. The split grid's 512 x 128 tiles run as
+// pipe9's do (pipe6_tile, whole LDS) with a barrier after each and a full prologue for the next.
+// Barrier counts stay equal for the two wave rows: per tile pipe9's, plus one after the epilogue.
+// ---------------------------------------------------------------------------
+template <class C, int GROUP_M, int ACT, bool LATE, bool SPLIT>
+__device__ __forceinline__ void pipe10_run(const GemmArgs& p, char* lds, const int wave) {
+    static_assert(C::BM == 256 && C::BN == 256 && C::FN == 4 && C::FM == 8 && C::NW == 8, "pipe10: 256 x 256, 8 waves");
+    constexpr int UNIT = 32768;
+    const int lane = threadIdx.x & 63;
+    const int wm = wave / C::WN, wn = wave % C::WN;
+    const int g = lane >> 4, li = lane & 15;
+    const int nbm = (p.M + C::BM - 1) / C::BM, nbn = (p.N + C::BN - 1) / C::BN, nfn = p.N / C::BN;
+    const int ntiles = SPLIT ? split_tiles(nbm, nfn) : nbm * nbn;
+
+    const i32x4 rA = raw_rsrc(p.A, (unsigned)((size_t)p.M * p.lda * 2));
+    const i32x4 rB = raw_rsrc(p.B, (unsigned)((size_t)p.N * p.ldb * 2));
+    const unsigned lds0 = (unsigned)(uintptr_t)(LDS_AS char*)lds;
+    const unsigned lw = __builtin_amdgcn_readfirstlane(lds0 + wave * 4096);
+    const int sw = (li >> 1) & 7;
+    const unsigned a_row = lds0 + (wm * C::TM + li) * 128, b_row = lds0 + (wn * C::TN + li) * 128;
+    const unsigned c0 = ((0 + g) ^ sw) << 4, c1 = ((4 + g) ^ sw) << 4;
+    const unsigned a0 = a_row + c0, a1 = a_row + c1, b0 = b_row + c0, b1 = b_row + c1;
+    const int nk = p.K / 64;
+
+    unsigned offA[4], offB[4];
+    auto set_off = [&](int m0, int n0) __attribute__((always_inline)) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int prow = (wave * 4 + q) * 8 + (lane >> 3);
+            const int logical = swz(prow, lane & 7);
+            offA[q] = ((unsigned)min(m0 + prow, p.M - 1) * (unsigned)p.lda + logical * 8) * 2u;
+            offB[q] = ((unsigned)min(n0 + prow, p.N - 1) * (unsigned)p.ldb + logical * 8) * 2u;
+        }
+    };
+    // tile coordinates of virtual block v; true for a split-grid 512 x 128 tile
+    auto coords = [&](int v, int& m0, int& n0) __attribute__((always_inline)) -> bool {
+        const int tile = xcd_remap(v, ntiles);
+        if constexpr (SPLIT) {
+            return split_coords(tile, nbm, nfn, m0, n0);
+        } else {
+            int bm, bn;
+            tile_coords<GROUP_M>(tile, nbm, nbn, bm, bn);
+            m0 = bm * C::BM;
+            n0 = bn * C::BN;
+            return false;
+        }
+    };
+
+    f32x4 acc[C::FM][C::FN];
+    bf16x8 b[C::FN], a[8];
+    auto step = [&](unsigned aa, unsigned bb, bool dma, unsigned m0base, const unsigned (&voff)[4], i32x4 rs,
+                    unsigned soff, int wm_, int wc_, bool end_barrier) __attribute__((always_inline)) {
+        ds_read16<0>(b[0], bb);
+        ds_read16<2048>(b[1], bb);
+        ds_read16<4096>(b[2], bb);
+        ds_read16<6144>(b[3], bb);
+        ds_read16<0>(a[0], aa);
+        ds_read16<2048>(a[1], aa);
+        ds_read16<4096>(a[2], aa);
+        ds_read16<6144>(a[3], aa);
+        ds_read16<8192>(a[4], aa);
+        ds_read16<10240>(a[5], aa);
+        ds_read16<12288>(a[6], aa);
+        ds_read16<14336>(a[7], aa);
+        if (dma) dma4(m0base, voff, rs, soff);
+        if (wm_ == 0) vm_wait<0>();
+        else if (wm_ == 4) vm_wait<4>();
+        lgkm_wait<0>();
+        __builtin_amdgcn_s_barrier();
+        __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+#pragma unroll
+            for (int j = 0; j < C::FN; ++j)
+                acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b[j], a[i], acc[i][j], 0, 0, 0);
+        __builtin_amdgcn_s_setprio(0);
+        __builtin_amdgcn_sched_barrier(0);
+        if (wc_ == 0) vm_wait<0>();
+        else if (wc_ == 4) vm_wait<4>();
+        if (end_barrier) __builtin_amdgcn_s_barrier();
+    };
+    unsigned kB, kA;
+    auto stage = [&](int sa, bool dB, bool dA, int need, bool last) __attribute__((always_inline)) {
+        const int sb = sa == 4 ? 0 : sa + 1;
+        const int iB = sa + 3 >= 5 ? sa - 2 : sa + 3, iA = sa + 4 >= 5 ? sa - 1 : sa + 4;
+        step(a0 + sa * UNIT, b0 + sb * UNIT, dB, lw + iB * UNIT, offB, rB, kB, -1, -1, true);
+        step(a1 + sa * UNIT, b1 + sb * UNIT, dA, lw + iA * UNIT, offA, rA, kA, LATE ? need : -1, LATE ? -1 : need,
+             !(LATE && last));
+        kB += 128;
+        kA += 128;
+    };
+
+    int v = blockIdx.x;
+    if (v >= ntiles) return;  // whole workgroup
+    int m0, n0;
+    bool split = coords(v, m0, n0);
+    bool primed = false;  // this tile's units 0-4 issued and 0-2 landed (by the previous tile's seam)
+    while (true) {
+        if (split) {
+            pipe6_tile<Pipe512x128, ACT, 1, 0>(p, lds, m0, n0);
+            __builtin_amdgcn_s_barrier();  // every wave's epilogue LDS reads done before the next DMA
+            v += gridDim.x;
+            if (v >= ntiles) break;
+            split = coords(v, m0, n0);
+            primed = false;
+            continue;
+        }
+        if (!primed) {  // pipe9's prologue: units 0..4 (A0 B0 A1 B1 A2) into slots 0..4
+            set_off(m0, n0);
+            dma4(lw + 0 * UNIT, offA, rA, 0);
+            dma4(lw + 1 * UNIT, offB, rB, 0);
+            dma4(lw + 2 * UNIT, offA, rA, 128);
+            dma4(lw + 3 * UNIT, offB, rB, 128);
+            dma4(lw + 4 * UNIT, offA, rA, 256);
+            vm_wait<12>();  // units 0 and 1 (stage 0) landed
+            __builtin_amdgcn_s_barrier();
+            if (LATE) __builtin_amdgcn_s_barrier();
+        }
+#pragma unroll
+        for (int i = 0; i < C::FM; ++i)
+#pragma unroll
+            for (int j = 0; j < C::FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+        kB = 128;
+        kA = 256;
+        stage(0, false, false, 4, false);
+        int s = 1;
+        for (; s + 5 <= nk - 2; s += 5) {
+            stage(2, true, true, 4, false);
+            stage(4, true, true, 4, false);
+            stage(1, true, true, 4, false);
+            stage(3, true, true, 4, false);
+            stage(0, true, true, 4, false);
+        }
+        if (s < nk - 2) {
+            stage(2, true, true, 4, false);
+            if (++s < nk - 2) {
+                stage(4, true, true, 4, false);
+                if (++s < nk - 2) {
+                    stage(1, true, true, 4, false);
+                    if (++s < nk - 2) {
+                        stage(3, true, true, 4, false);
+                        ++s;
+                    }
+                }
+            }
+        }
+        const int sa2 = (2 * s) % 5, sa1 = sa2 >= 3 ? sa2 - 3 : sa2 + 2;
+        stage(sa2, true, false, 0, false);
+        stage(sa1, false, false, -1, true);
+        vm_wait<0>();
+        // the accumulators pass through an empty asm: otherwise hipcc sinks the last stage's MFMAs
+        // into the epilogue's branches and spills (the same as gemm_mx11's)
+#pragma unroll
+        for (int i = 0; i < C::FM; ++i)
+#pragma unroll
+            for (int j = 0; j < C::FN; ++j) asm volatile("" : "+v"(acc[i][j]));
+        // every wave's fragment reads of this tile precede the barrier closing the late row's last
+        // memory phase, which this wave has passed: the whole ring is free of reads
+        const int vn = v + gridDim.x;
+        int m1 = 0, n1 = 0;
+        const bool has_next = vn < ntiles;
+        const bool split1 = has_next ? coords(vn, m1, n1) : false;
+        const bool prime = has_next && !split1;
+        if (prime) {  // the next tile's A0 B0 A1 under this tile's epilogue (offsets recomputed after it:
+                      // not held live across the epilogue)
+            set_off(m1, n1);
+            dma4(lw + 0 * UNIT, offA, rA, 0);
+            dma4(lw + 1 * UNIT, offB, rB, 0);
+            dma4(lw + 2 * UNIT, offA, rA, 128);
+        }
+        {  // the lane id from a volatile asm: the epilogue's lane-derived addresses are recomputed per
+           // tile instead of being hoisted to kernel entry and spilled around the tile loop
+            int ln;
+            asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(ln));
+            gemm_epilogue_wave<C, ACT, true, 2>(p, lds + 3 * UNIT, acc, m0, n0, wave, wm, wn, ln >> 4, ln & 15, ln);
+        }
+        vm_wait<0>();  // own pieces of units 0-2 landed (and this wave's stores retired)
+        __builtin_amdgcn_s_barrier();  // staging reads of every wave done: slots 3-4 free
+        if (!has_next) break;
+        v = vn;
+        m0 = m1;
+        n0 = n1;
+        split = split1;
+        primed = prime;
+        if (prime) {  // B1 A2 into slots 3-4; then pipe9's prologue barriers (units 0-2 landed for every wave)
+            set_off(m0, n0);
+            dma4(lw + 3 * UNIT, offB, rB, 128);
+            dma4(lw + 4 * UNIT, offA, rA, 256);
+            __builtin_amdgcn_s_barrier();
+            if (LATE) __builtin_amdgcn_s_barrier();
+        }
+    }
+}
+
+template <class C, int GROUP_M, int ACT, bool SPLIT>
+__global__ __launch_bounds__(C::NT, 2) void gemm_pipe10_kernel(GemmArgs p) {
+    __shared__ __attribute__((aligned(16))) char lds[5 * 32768];
+    static_assert(Pipe512x128::LDS <= 5 * 32768, "pipe10 LDS");
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    if (wave >= C::NW / 2)
+        pipe10_run<C, GROUP_M, ACT, true, SPLIT>(p, lds, wave);
+    else
+        pipe10_run<C, GROUP_M, ACT, false, SPLIT>(p, lds, wave);
+}
+
+template <class C, int GROUP_M, bool SPLIT>
+int launch_pipe10(const GemmArgs& a, hipStream_t s) {
+    const int nbm = (a.M + C::BM - 1) / C::BM, nbn = (a.N + C::BN - 1) / C::BN;
+    const int ntiles = SPLIT ? split_tiles(nbm, a.N / C::BN) : nbm * nbn;
+    const dim3 grid(std::min(ntiles, 256)), block(C::NT);  // one workgroup per CU (160 KiB of LDS)
+    switch (a.act) {
+        case MME_ACT_GELU_TANH:
+            hipLaunchKernelGGL((gemm_pipe10_kernel<C, GROUP_M, MME_ACT_GELU_TANH, SPLIT>), grid, block, 0, s, a);
+            break;
+        case MME_ACT_QUICK_GELU:
+            hipLaunchKernelGGL((gemm_pipe10_kernel<C, GROUP_M, MME_ACT_QUICK_GELU, SPLIT>), grid, block, 0, s, a);
+            break;
+        case MME_ACT_GELU_ERF:
+            hipLaunchKernelGGL((gemm_pipe10_kernel<C, GROUP_M, MME_ACT_GELU_ERF, SPLIT>), grid, block, 0, s, a);
+            break;
+        case MME_ACT_GEGLU_TANH:
+            hipLaunchKernelGGL((gemm_pipe10_kernel<C, GROUP_M, MME_ACT_GEGLU_TANH, SPLIT>), grid, block, 0, s, a);
+            break;
+        default:
+            hipLaunchKernelGGL((gemm_pipe10_kernel<C, GROUP_M, MME_ACT_NONE, SPLIT>), grid, block, 0, s, a);
+            break;
+    }
+    return mme_check_launch("mme_gemm");
 }
 
 template <class C, int GROUP_M, int ACT, int DIAG = 0, bool SPLIT = false, bool WEPI = false>
@@ -2319,6 +2568,11 @@ int gemm_dispatch(GemmArgs a, int variant, hipStream_t s) {
             if (variant == 81)
                 return N % 256 == 128 ? launch_pipe9<Pipe256, 4, true, 1>(a, s) : launch_pipe9<Pipe256, 4, false, 1>(a, s);
             return N % 256 == 128 ? launch_pipe9<Pipe256, 4, true, 2>(a, s) : launch_pipe9<Pipe256, 4, false, 2>(a, s);
+        case 90:  // dev: pipe10 (persistent pipe9, next tile's prologue under the epilogue); pipe9 for the
+                  // split grid (its 512 x 128 tiles inlined into the loop spill ~100 VGPRs)
+            if (!pipe8_ok(a)) break;
+            if (N % 256 == 128) return launch_pipe9<Pipe256, 4, true>(a, s);
+            return launch_pipe10<Pipe256, 4, false>(a, s);
         case 84:  // dev: pipe9 with the round-2/3 epilogue staging (pitch 144 B: 2-way LDS bank conflicts)
             if (!pipe8_ok(a)) break;
             if (N % 256 == 128) return launch_pipe9<Pipe256, 4, true, 0, false>(a, s);

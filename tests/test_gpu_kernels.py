@@ -234,6 +234,30 @@ def test_attention_m32_8wave_skip_vs_kind38(cuda, B, T, H, causal, lens):
     assert nd <= 1e-5 * d.numel() + 1 and bool((d <= 2 * ulp).all())
 
 
+@pytest.mark.dev
+@pytest.mark.parametrize("M,N,K,act", [(70001, 4352, 1152, 1), (5000, 5120, 1280, 2), (300, 1024, 192, 1),
+                                       (2000, 4096, 1024, 0), (129, 512, 256, 1)])
+def test_gemm_pipe10_bit_identical_to_pipe9(cuda, M, N, K, act):
+    """Dev form 90 (pipe10: persistent pipe9 with the next tile's first units DMA'd under the epilogue,
+    two-pass staging) runs pipe9's main loop and epilogue arithmetic: bit-identical outputs, with the
+    LayerNorm-fold epilogue and with bias + activation, ragged M, fewer tiles than CUs and many per CU."""
+    g = torch.Generator(device="cuda").manual_seed(M + N + K)
+    x = rnd(M, K, gen=g)
+    w = rnd(N, K, scale=K ** -0.5, gen=g)
+    b = rnd(N, scale=0.1, gen=g)
+    gam = (1 + 0.1 * torch.randn(K, device="cuda", generator=g)).to(torch.bfloat16)
+    bet = rnd(K, scale=0.1, gen=g)
+    f = ops.LNFolded(w, b, gam, bet)
+    st = ops.rowstats(x, 1e-6, d=K)
+    outs = []
+    for form in (None, 90):
+        with ops.kernel_forms(**({} if form is None else {"gemm": form})):
+            outs.append((ops.gemm_lnfold(x, f, st, act=act), ops.gemm(x, w, b, act=act)))
+        torch.cuda.synchronize()
+    for a_, b_ in zip(outs[0], outs[1]):
+        assert torch.equal(a_, b_), f"pipe10 differs from pipe9 ({M}x{N}x{K}, act {act})"
+
+
 def test_attention_production_full_grid(cuda):
     """The production hd-72 kernel over the bench's full launch grid (417 images x 16 heads x
     3 query blocks of SigLIP vision; 239 before round 3's larger execution batches) against the fp32

@@ -1,7 +1,8 @@
 #!/usr/bin/env python3
 """A/B of two GEMM dispatch variants on the encoder shapes, with a bit-exactness check.
 
-For every case: run variant A and variant B (mme_gemm_variant) on identical inputs,
+For every case: run variant A and variant B (per-call forms, ops.kernel_forms; -1 = production)
+on identical inputs,
 require identical output bytes, then time interleaved rounds (HIP events, median of
 rounds) — cdna_hip_programming.md §5.4 rule 24. Cases cover the production epilogues:
 LayerNorm-folded (QKV, fc1 + gelu_tanh / quick_gelu), residual (o_proj / fc2, patch
@@ -10,7 +11,6 @@ embed with a position-table period) and plain bias.
     python tools/pers_ab.py [--a -1] [--b 60] [--rows 174231] [--rounds 5] [--iters 5]
 """
 import argparse
-import ctypes
 import json
 import os
 import statistics
@@ -45,9 +45,8 @@ def main():
     ap.add_argument("--cases", default=",".join(CASES))
     ap.add_argument("--check-only", action="store_true")
     args = ap.parse_args()
-    lib = _lib.load()
-    lib.mme_gemm_variant.restype = ctypes.c_int
-    lib.mme_gemm_variant.argtypes = [ctypes.c_int]
+    def form(v):
+        return ops.kernel_forms(**({} if v == -1 else {"gemm": v}))
     g = torch.Generator(device="cuda").manual_seed(0)
     out = {"rows": args.rows, "a": args.a, "b": args.b}
     for name in args.cases.split(","):
@@ -77,9 +76,9 @@ def main():
 
         outs = {}
         for v in (args.a, args.b):
-            lib.mme_gemm_variant(v)
             o = torch.empty(M, N, dtype=torch.bfloat16, device="cuda")
-            run(o)
+            with form(v):
+                run(o)
             torch.cuda.synchronize()
             outs[v] = o
         same = torch.equal(outs[args.a], outs[args.b])
@@ -92,15 +91,15 @@ def main():
             o = outs[args.a]
             for _ in range(args.rounds):
                 for v in (args.a, args.b):
-                    lib.mme_gemm_variant(v)
                     s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-                    s.record()
-                    for _ in range(args.iters):
-                        if epi == "res":
-                            ops.gemm(x, w, bias, residual=res, out=o)  # out-of-place residual: same traffic
-                        else:
-                            run(o)
-                    e.record()
+                    with form(v):
+                        s.record()
+                        for _ in range(args.iters):
+                            if epi == "res":
+                                ops.gemm(x, w, bias, residual=res, out=o)  # out-of-place residual: same traffic
+                            else:
+                                run(o)
+                        e.record()
                     torch.cuda.synchronize()
                     t[v].append(s.elapsed_time(e) / args.iters)
             fl = 2.0 * M * N * K
@@ -112,7 +111,6 @@ def main():
         out[name] = r
         print(name, json.dumps(r), flush=True)
         del outs
-    lib.mme_gemm_variant(-1)
     print(json.dumps(out), flush=True)
 
 
