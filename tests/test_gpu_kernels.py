@@ -250,8 +250,8 @@ def test_gemm_pipe10_bit_identical_to_pipe9(cuda, M, N, K, act):
     f = ops.LNFolded(w, b, gam, bet)
     st = ops.rowstats(x, 1e-6, d=K)
     outs = []
-    for form in (None, 90):
-        with ops.kernel_forms(**({} if form is None else {"gemm": form})):
+    for form in (80, 90):  # dev form 80 = pipe9 forced (production picks other kernels below 1 M outputs)
+        with ops.kernel_forms(gemm=form):
             outs.append((ops.gemm_lnfold(x, f, st, act=act), ops.gemm(x, w, b, act=act)))
         torch.cuda.synchronize()
     for a_, b_ in zip(outs[0], outs[1]):
