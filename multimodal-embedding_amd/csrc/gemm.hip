@@ -930,7 +930,7 @@ __device__ __forceinline__ void gemm_epilogue_wave(const GemmArgs& p, char* lds,
     const int rr = lane >> 3, cc = lane & 7;                 // store phase: row rr of 8, 16-B chunk cc
     u16x8 rv[16 / PASSES];  // residual rows of the current pass (all 16 row groups with one pass)
     auto load_res = [&](int ps) __attribute__((always_inline)) {
-        if (!GLU && p.res) {  // residual rows first: their latency overlaps the staging below
+        if (!GLU && p.res) {
 #pragma unroll
             for (int q = 0; q < 16 / PASSES; ++q) {
                 const int gr = min(rm0 + (ps * (16 / PASSES) + q) * 8 + rr, p.M - 1), gc = min(cn0 + cc * 8, p.N - 8);
@@ -939,7 +939,16 @@ __device__ __forceinline__ void gemm_epilogue_wave(const GemmArgs& p, char* lds,
             }
         }
     };
-    if constexpr (PASSES == 1) load_res(0);
+    if constexpr (PASSES == 1) {
+        if (!GLU && p.res) {  // residual rows first: their latency overlaps the staging below
+#pragma unroll
+            for (int q = 0; q < 16; ++q) {
+                const int gr = min(rm0 + q * 8 + rr, p.M - 1), gc = min(cn0 + cc * 8, p.N - 8);
+                const int r2 = p.res_period ? gr % p.res_period : gr;
+                rv[q] = *reinterpret_cast<const u16x8*>(p.res + (size_t)r2 * p.ldr + gc);
+            }
+        }
+    }
     float lr[C::FM], lm[C::FM];
     if (p.ln_stats) {
 #pragma unroll
