@@ -246,7 +246,12 @@ __global__ __launch_bounds__(256) void resample_patch_fused_kernel(
 //     offsets and LUT bases are computed once, then it walks every G / 3-rd patch.
 // The u8 raster of the P output rows stays in LDS ([P][G * P * 3]) and the LUT turns it into
 // the exact float32 -> bf16 values. Same integer sums, so the output is bit-identical.
-template <int P>
+// K (round 4): a compile-time tap count (5 for every registry tower: 224 px upscaled to 224-384);
+// the taps then run unconditionally (the coefficients past a window's count are exactly 0, and the
+// extra bytes they read lie inside the LDS allocation) as 24-bit multiplies (__mul24, v_mad_i32_i24:
+// |u8 * w| < 2^30 with |w| <= 2^22, exact), where the K = 0 form branches per tap around 32-bit
+// multiplies. Same integer sums, so the output is bit-identical.
+template <int P, int K = 0>
 __global__ __launch_bounds__(256) void resample_patch_p_kernel(
     const uint8_t* __restrict__ img, int n, int H, int W, int S, int top, int left, int kx, int ky,
     const int* __restrict__ xb, const int* __restrict__ xk, const int* __restrict__ yb, const int* __restrict__ yk,
@@ -284,9 +289,14 @@ __global__ __launch_bounds__(256) void resample_patch_p_kernel(
         const uint8_t* sp = in_l + xmin * 3 + c;
         for (int r = 0; r < R; ++r) {
             int sum = 1 << (PREC - 1);
+            if constexpr (K > 0) {
 #pragma unroll
-            for (int x = 0; x < 8; ++x)
-                if (x < cnt) sum += sp[r * rowb + 3 * x] * w[x];
+                for (int x = 0; x < K; ++x) sum += __mul24(sp[r * rowb + 3 * x], w[x]);
+            } else {
+#pragma unroll
+                for (int x = 0; x < 8; ++x)
+                    if (x < cnt) sum += sp[r * rowb + 3 * x] * w[x];
+            }
             hr[r * E + e] = (uint8_t)clip8(sum);
         }
     }
@@ -298,7 +308,12 @@ __global__ __launch_bounds__(256) void resample_patch_p_kernel(
             const int ymin = yb[2 * oy] - r0, cnt = yb[2 * oy + 1];
             const int* kk = yk + oy * ky;
             int sum = 1 << (PREC - 1);
-            for (int y = 0; y < cnt; ++y) sum += hr[(ymin + y) * E + e] * kk[y];
+            if constexpr (K > 0) {
+#pragma unroll
+                for (int y = 0; y < K; ++y) sum += __mul24(hr[(ymin + y) * E + e], kk[y]);
+            } else {
+                for (int y = 0; y < cnt; ++y) sum += hr[(ymin + y) * E + e] * kk[y];
+            }
             vr[kyy * E + e] = (uint8_t)clip8(sum);
         }
     }
@@ -418,6 +433,14 @@ extern "C" int mme_preprocess_u8(const uint8_t* imgs, int n, int H, int W, int r
         if (patch == 14 && kx <= 8 && ky <= 8 && kpad <= 8 * 256) {
             const long E = (long)(S / 14) * 14 * 3;
             const long lds = (((long)R * W * 3 + 15) & ~15L) + ((R * E + 15) & ~15L) + 14 * E;
+            // K = 5 taps: the LDS allocation must also cover the reads past a window (the last input
+            // row's bytes up to 4 pixels on, the h-pass rows up to 4 rows on: inside hr / vr)
+            const long lds5 = lds + 16;
+            if (kx == 5 && ky == 5 && lds5 <= FUSED_LDS && R >= 4) {
+                hipLaunchKernelGGL((resample_patch_p_kernel<14, 5>), dim3(n * (S / 14)), dim3(256), (unsigned)lds5, s,
+                                   imgs, n, H, W, S, top, left, kx, ky, xb, xk, yb, yk, na, kpad, (bf16*)out);
+                return mme_check_launch("mme_preprocess_u8");
+            }
             if (lds <= FUSED_LDS) {
                 hipLaunchKernelGGL(resample_patch_p_kernel<14>, dim3(n * (S / 14)), dim3(256), (unsigned)lds, s, imgs,
                                    n, H, W, S, top, left, kx, ky, xb, xk, yb, yk, na, kpad, (bf16*)out);
