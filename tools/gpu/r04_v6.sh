@@ -15,3 +15,6 @@ tail -4 ${P}_pp_pytest.log
 MME_DEV=1 timeout -k 10 300 python -u tools/attn_bench.py --cases siglip_vision --batch 417 \
     --variants 92,100,101,102,92,100,101,102 > ${P}_pp_bench.log 2>&1 || exit $?
 cat ${P}_pp_bench.log
+timeout -k 10 400 python -u bench.py --model Apple-DFN5B-H --fp8 --steps 3 --warmup 1 --no-cpu-baseline \
+    > ${P}_dfn5b_fp8_bench.log 2>&1 || exit $?
+tail -1 ${P}_dfn5b_fp8_bench.log | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print(d['value'], d['fp8_drift'], d['parity']['rows'])"
