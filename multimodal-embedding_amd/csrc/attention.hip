@@ -2065,8 +2065,17 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(2))) vo
 // starts (production kind 62 since round 3).
 // DBG (dev kinds 76 / 77, round 4): printf trace of one (batch 1, head 8, query 334) through the
 // tile loop -- running max, two O^T elements (d 7, d 22) and the weight sum -- per tile.
-template <int HD, int NW, int MINW, bool PRIO, int SKIP = 0, bool DBG = false>
+// RING (dev kind 78, round 4): LDS slots of the K / V tile ring. 2 = production (tile t + 1's DMA
+// issued after tile t's barrier; hipcc drains it with vmcnt(0) before tile t's V^T reads, which it
+// cannot prove disjoint from the DMA); 3 = tile t + 2's DMA issued there from inline asm (invisible
+// to hipcc), each tile waiting with a counted vmcnt that leaves the next tile's DMA in flight;
+// 4 (dev kind 79) = RING 3's DMA with the late wave row's PV one tile behind (stagger, below).
+// XT (RING 4 only, dev kinds 80 / 81): VALU trims of qks. 1 = exp2 arguments as packed FMAs (same
+// per-element fma: bit-identical); 2 = rescale O only when some query's max grows by more than 2^8 in
+// the exp2 domain (P <= 256 otherwise; the weight sums use the same stale max: not bit-identical).
+template <int HD, int NW, int MINW, bool PRIO, int SKIP = 0, bool DBG = false, int RING = 2, int XT = 0>
 __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(MINW))) void attn_hyb_kernel(AttnArgs a) {
+    static_assert(RING >= 2 && RING <= 4, "two to four ring slots");
     static_assert(HD == 72 || HD == 80, "80-deep QK^T, 80 PV rows");
     constexpr bool ONES = HD == 72;  // hd 72: V^T row 72 = ones (weight sums); hd 80: f32 sums
     constexpr int NCHL = HD / 8;     // K / V planes with data
@@ -2079,7 +2088,7 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(MINW)))
     constexpr int QB = NW * 32;
     static_assert(2 * NKS <= NCHL + NVP, "K reads past the head dim stay inside the tile");
     typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
-    __shared__ __attribute__((aligned(16))) char lds[2 * TILE];
+    __shared__ __attribute__((aligned(16))) char lds[RING * TILE];
 
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -2099,9 +2108,9 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(MINW)))
     const int Tk = a.seq_lens ? a.seq_lens[b] : T;
     const float c = a.scale_log2;
 
-    // the ones plane (V plane 9 at hd 72) in both ring slots
+    // the ones plane (V plane 9 at hd 72) in every ring slot
     if (ONES)
-        for (int i = tid; i < 2 * 64; i += NW * 64)
+        for (int i = tid; i < RING * 64; i += NW * 64)
             *reinterpret_cast<u16x8*>(lds + (i >> 6) * TILE + (2 * NCHL) * 1024 + (i & 63) * 16) =
                 u16x8{0x3F80, 0x3F80, 0x3F80, 0x3F80, 0x3F80, 0x3F80, 0x3F80, 0x3F80};
 
@@ -2122,8 +2131,8 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(MINW)))
     if (a.causal) nkt = min(nkt, (min(T, qb * QB + QB) + 63) / 64);
 
     auto vslot = [](int key, int plane) { return key ^ (4 * ((key >> 4) & 1) + 8 * (plane & 1)); };
-    auto issue = [&](int t) {
-        char* tb = lds + (t & 1) * TILE;
+    auto issue = [&](int t, int slot) {
+        char* tb = lds + slot * TILE;
 #pragma unroll
         for (int i = 0; i < MAXI; ++i) {
             const int idx = wave + NW * i;
@@ -2132,10 +2141,15 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(MINW)))
                 const int plane = isV ? idx - NCHL : idx;
                 const int key = isV ? vslot(lane, plane) : lane;  // slot lane holds this key (involution)
                 const bf16* src = base + (long)min(t * 64 + key, T - 1) * a.ld + (isV ? 2 : 1) * D + h * HD + plane * 8;
-                glds16(src, tb + idx * 1024);
+                if constexpr (RING >= 3)
+                    glds16_asm(src, tb + idx * 1024);  // counted by the ring's own waits only
+                else
+                    glds16(src, tb + idx * 1024);
             }
         }
     };
+    // this wave's DMA count per tile (wave-uniform): MAXI, or MAXI - 1 when its last chunk is past NINS
+    const bool full_issue = wave + NW * (MAXI - 1) < NINS;
 
     const unsigned lds0 = (unsigned)(uintptr_t)(LDS_AS char*)lds;
     const unsigned kb0 = lds0 + hh * 1024 + r * 16;  // K fragment: plane 2 ks + hh, key 32 kb + r
@@ -2289,6 +2303,123 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(MINW)))
         }
     };
 
+    // RING 4 (stagger): tile_step split at the P hand-off. qks(t): QK^T, mask, running max, lazy
+    // rescale of O, exp2, P packed into the PV B operands (pq); pvs(t): PV from pq. The early wave
+    // row (waves 0 .. NW/2-1) runs qks(t), pvs(t) between two barriers; the late row runs pvs(t - 1),
+    // qks(t), so on each SIMD one wave's MFMAs meet the other's softmax VALU. The O updates keep
+    // their order (PV(t - 1) before tile t's rescale), so both rows compute kind 62's arithmetic.
+    bf16x8 pq[2][2];
+    auto qks = [&](int t, const unsigned so) __attribute__((always_inline)) {
+        const bool half = SKIP && t * 64 + 32 >= Tk;
+        f32x16 sc[2];
+#pragma unroll
+        for (int kb = 0; kb < 2; ++kb) {
+            if (kb == 1 && half) {
+#pragma unroll
+                for (int e = 0; e < 16; ++e) {
+                    float f;
+                    asm volatile("v_mov_b32 %0, 0xff800000" : "=v"(f));
+                    sc[1][e] = f;
+                }
+            } else {
+                f32x16 z = {};
+#pragma unroll
+                for (int ks = 0; ks < NKS; ++ks) {
+                    const bf16x8 kf =
+                        *reinterpret_cast<const LDS_AS bf16x8*>((uintptr_t)(kb0 + so + kb * 512 + ks * 2048));
+                    z = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[ks], z, 0, 0, 0);
+                }
+                sc[kb] = z;
+            }
+        }
+        if ((t * 64 + 64 > Tk) || (a.causal && t * 64 + 63 > qw0)) {
+            const int q = qw0 + r;
+            const int lim = a.causal ? min(Tk, q + 1) : Tk;
+#pragma unroll
+            for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+                for (int e = 0; e < 16; ++e)
+                    if (t * 64 + kb * 32 + (e & 3) + 8 * (e >> 2) + 4 * hh >= lim) sc[kb][e] = -INFINITY;
+        }
+        float mloc = fmaxf(sc[0][0], sc[0][1]);
+#pragma unroll
+        for (int e = 2; e < 16; ++e) mloc = fmaxf(mloc, sc[0][e]);
+#pragma unroll
+        for (int e = 0; e < 16; ++e) mloc = fmaxf(mloc, sc[1][e]);
+        mloc = xmax32(mloc);
+        const float mnew = fmaxf(m, mloc);
+        if (__builtin_amdgcn_ballot_w64((XT & 2) ? (mloc - m) * c > 8.0f : mnew != m)) {
+            const float alpha = __builtin_amdgcn_exp2f((m - mnew) * c);
+            if (!ONES) lsum *= alpha;
+#pragma unroll
+            for (int u = 0; u < 2; ++u) {
+                const float au = __shfl(alpha, 16 * u + li, 64);
+#pragma unroll
+                for (int i = 0; i < NDT; ++i) o[u][i] *= au;
+            }
+            m = mnew;
+        } else if (!(XT & 2)) {
+            m = mnew;
+        }
+        const float mc = m * c;
+        float psum = 0.f;
+#pragma unroll
+        for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+            for (int e = 0; e < 16; e += 2) {
+                if (XT & 1) {
+                    const f32x2 x = pk_fma(f32x2{sc[kb][e], sc[kb][e + 1]}, f32x2{c, c}, f32x2{-mc, -mc});
+                    sc[kb][e] = __builtin_amdgcn_exp2f(x.x);
+                    sc[kb][e + 1] = __builtin_amdgcn_exp2f(x.y);
+                } else {
+                    sc[kb][e] = __builtin_amdgcn_exp2f(sc[kb][e] * c - mc);
+                    sc[kb][e + 1] = __builtin_amdgcn_exp2f(sc[kb][e + 1] * c - mc);
+                }
+                if (!ONES) {
+                    psum += sc[kb][e];
+                    psum += sc[kb][e + 1];
+                }
+            }
+        if (!ONES) lsum += psum;
+#pragma unroll
+        for (int kb = 0; kb < 2; ++kb) {
+            if (kb == 1 && half) break;
+            unsigned xw[4], yw[4];
+#pragma unroll
+            for (int w = 0; w < 4; ++w) {
+                bf16x2_t px = {f2bf(sc[kb][2 * w]), f2bf(sc[kb][2 * w + 1])};
+                bf16x2_t py = {f2bf(sc[kb][8 + 2 * w]), f2bf(sc[kb][8 + 2 * w + 1])};
+                xw[w] = __builtin_bit_cast(unsigned, px);
+                yw[w] = __builtin_bit_cast(unsigned, py);
+            }
+            unsigned b0w[4], b1w[4];
+#pragma unroll
+            for (int w = 0; w < 4; ++w) {
+                const auto sw = __builtin_amdgcn_permlane16_swap(xw[w], yw[w], false, false);
+                b0w[w] = sw[0];
+                b1w[w] = sw[1];
+            }
+            pq[kb][0] = __builtin_bit_cast(bf16x8, make_uint4(b0w[0], b0w[1], b0w[2], b0w[3]));
+            pq[kb][1] = __builtin_bit_cast(bf16x8, make_uint4(b1w[0], b1w[1], b1w[2], b1w[3]));
+        }
+    };
+    auto pvs = [&](int t, const unsigned so) __attribute__((always_inline)) {
+        const bool half = SKIP && t * 64 + 32 >= Tk;
+#pragma unroll
+        for (int kb = 0; kb < 2; ++kb) {
+            if (kb == 1 && half) break;
+#pragma unroll
+            for (int dt = 0; dt < NDT; ++dt) {
+                const unsigned off = so + kb * 512 + dt * 2048;
+                const s16x4 v0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS_AS s16x4*)(uintptr_t)(vbj[0] + off));
+                const s16x4 v1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS_AS s16x4*)(uintptr_t)(vbj[1] + off));
+                const bf16x8 vv = __builtin_bit_cast(bf16x8, __builtin_shufflevector(v0, v1, 0, 1, 2, 3, 4, 5, 6, 7));
+                o[0][dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vv, pq[kb][0], o[0][dt], 0, 0, 0);
+                o[1][dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vv, pq[kb][1], o[1][dt], 0, 0, 0);
+            }
+        }
+    };
+
     const bool dbg = DBG && b == 1 && h == 8 && qb == 1 && wave == 2;
     auto trace = [&](int t) {
         if (!dbg) return;
@@ -2297,20 +2428,92 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(MINW)))
         if (lane == 46) printf("K%d t %2d sum %a\n", SKIP, t, o[0][4][0]);
     };
     if (PRIO && wave >= NW / 2) __builtin_amdgcn_s_setprio(1);
-    if (nkt > 0) issue(0);
-    for (int t = 0; t < nkt; t += 2) {
-        vm_wait<0>();
-        __builtin_amdgcn_s_barrier();
-        if (t + 1 < nkt) issue(t + 1);
-        tile_step(t, 0);
-        if (DBG) trace(t);
-        if (t + 1 < nkt) {
+    if constexpr (RING == 2) {
+        (void)qks;
+        (void)pvs;
+        if (nkt > 0) issue(0, 0);
+        for (int t = 0; t < nkt; t += 2) {
             vm_wait<0>();
             __builtin_amdgcn_s_barrier();
-            if (t + 2 < nkt) issue(t + 2);
-            tile_step(t + 1, TILE);
-            if (DBG) trace(t + 1);
+            if (t + 1 < nkt) issue(t + 1, 1);
+            tile_step(t, 0);
+            if (DBG) trace(t);
+            if (t + 1 < nkt) {
+                vm_wait<0>();
+                __builtin_amdgcn_s_barrier();
+                if (t + 2 < nkt) issue(t + 2, 0);
+                tile_step(t + 1, TILE);
+                if (DBG) trace(t + 1);
+            }
         }
+    } else if constexpr (RING == 3) {
+        // Q landed before the first asm DMA: hipcc cannot count those, so it must not wait on Q later
+#pragma unroll
+        for (int ks = 0; ks < NKS; ++ks) asm volatile("" ::"v"(qf[ks]));
+        // tile t sits in slot t % 3; at tile t's barrier every wave is done with tile t - 1, whose
+        // slot takes tile t + 2. The wait leaves tile t + 1's DMA (this wave's last issue) in flight.
+        if (nkt > 0) issue(0, 0);
+        if (nkt > 1) issue(1, 1);
+        auto step = [&](int t, int slot) __attribute__((always_inline)) {
+            if (t + 1 < nkt) {
+                if (full_issue)
+                    vm_wait<MAXI>();
+                else
+                    vm_wait<MAXI - 1>();
+            } else {
+                vm_wait<0>();
+            }
+            __builtin_amdgcn_s_barrier();
+            if (t + 2 < nkt) issue(t + 2, slot == 0 ? 2 : slot - 1);
+            tile_step(t, slot * TILE);
+            if (DBG) trace(t);
+        };
+        for (int t = 0; t < nkt; t += 3) {
+            step(t, 0);
+            if (t + 1 < nkt) step(t + 1, 1);
+            if (t + 2 < nkt) step(t + 2, 2);
+        }
+    } else {
+        // RING 4 (stagger): tile t in slot t % 4. At tile t's barrier the late row still needs tile
+        // t - 1 (its PV), so tile t + 2 goes to the slot of tile t - 2.
+#pragma unroll
+        for (int ks = 0; ks < NKS; ++ks) asm volatile("" ::"v"(qf[ks]));
+        if (nkt > 0) issue(0, 0);
+        if (nkt > 1) issue(1, 1);
+        // one straight-line loop per row (a per-step branch on the row made hipcc spill O / P)
+        auto loop = [&](auto late_c) __attribute__((always_inline)) {
+            constexpr bool LATE = decltype(late_c)::value;
+            auto step = [&](int t, int slot) __attribute__((always_inline)) {
+                if (t + 1 < nkt) {
+                    if (full_issue)
+                        vm_wait<MAXI>();
+                    else
+                        vm_wait<MAXI - 1>();
+                } else {
+                    vm_wait<0>();
+                }
+                __builtin_amdgcn_s_barrier();
+                if (t + 2 < nkt) issue(t + 2, (slot + 2) & 3);
+                if constexpr (LATE) {
+                    if (t > 0) pvs(t - 1, ((slot + 3) & 3) * TILE);
+                    qks(t, slot * TILE);
+                } else {
+                    qks(t, slot * TILE);
+                    pvs(t, slot * TILE);
+                }
+            };
+            for (int t = 0; t < nkt; t += 4) {
+                step(t, 0);
+                if (t + 1 < nkt) step(t + 1, 1);
+                if (t + 2 < nkt) step(t + 2, 2);
+                if (t + 3 < nkt) step(t + 3, 3);
+            }
+            if (LATE && nkt > 0) pvs(nkt - 1, ((nkt - 1) & 3) * TILE);
+        };
+        if (wave >= NW / 2)
+            loop(std::integral_constant<bool, true>{});
+        else
+            loop(std::integral_constant<bool, false>{});
     }
 
     const float lq = ONES ? 0.f : xsum32(lsum);  // hd 80: query r's weight sum (S^T lanes)
@@ -2941,6 +3144,30 @@ bool launch_attn_dev(int kind, const AttnArgs& a, int B, int T, int H, hipStream
                 hipLaunchKernelGGL((attn_hyb_kernel<HD, 8, 4, true, 0, true>), dim3(cdiv(T, 256) * H * B), dim3(512), 0, st, a);
             else
                 hipLaunchKernelGGL((attn_hyb_kernel<HD, 8, 4, true, 2, true>), dim3(cdiv(T, 256) * H * B), dim3(512), 0, st, a);
+        } else {
+            return false;
+        }
+    } else if (kind == 78) {  // dev: kind 62 on a three-slot K / V ring (tile t + 2's DMA issued at tile t)
+        if constexpr (HD != 64)
+            hipLaunchKernelGGL((attn_hyb_kernel<HD, 8, 4, true, 2, false, 3>), dim3(cdiv(T, 256) * H * B), dim3(512), 0,
+                               st, a);
+        else
+            return false;
+    } else if (kind == 79) {  // dev: kind 62 staggered (RING 4): the late wave row runs PV one tile behind
+        if constexpr (HD != 64)
+            hipLaunchKernelGGL((attn_hyb_kernel<HD, 8, 4, true, 2, false, 4>), dim3(cdiv(T, 256) * H * B), dim3(512), 0,
+                               st, a);
+        else
+            return false;
+    } else if (kind == 80 || kind == 81) {  // dev: kind 79 with qks VALU trims (80: packed exp arguments +
+                                            // 2^8 rescale threshold; 81: packed exp arguments only)
+        if constexpr (HD != 64) {
+            if (kind == 80)
+                hipLaunchKernelGGL((attn_hyb_kernel<HD, 8, 4, true, 2, false, 4, 3>), dim3(cdiv(T, 256) * H * B),
+                                   dim3(512), 0, st, a);
+            else
+                hipLaunchKernelGGL((attn_hyb_kernel<HD, 8, 4, true, 2, false, 4, 1>), dim3(cdiv(T, 256) * H * B),
+                                   dim3(512), 0, st, a);
         } else {
             return false;
         }

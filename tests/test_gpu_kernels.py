@@ -134,7 +134,7 @@ PROD_ATTN_KINDS = (38, 41, 62, 65)  # in the production library; the rest are de
 
 @pytest.mark.parametrize("kind", [k if k in PROD_ATTN_KINDS else pytest.param(k, marks=pytest.mark.dev)
                                   for k in (38, 39, 40, 41, 42, 43, 44, 45, 46, 47, 48, 49, 50, 51, 52, 54, 55, 56,
-                                            57, 58, 59, 60, 61, 62, 63, 65)])
+                                            57, 58, 59, 60, 61, 62, 63, 65, 78, 79, 80, 81)])
 @pytest.mark.parametrize("B,T,H,hd,causal,lens", [
     (2, 729, 4, 72, False, None),       # SigLIP vision geometry
     (2, 520, 3, 72, False, [520, 301]),  # key padding, partial last tile
@@ -217,6 +217,25 @@ def test_attention_pingpong_skip_bit_identical_to_kind58(cuda, kind, B, T, H, ca
     nd, d, _ = _skip_pair(qkv, B, T, H, 72, sl, causal, 58, kind)
     assert nd == 0, f"kind {kind} differs from kind 58 on {nd} outputs (max {d.max().item():.3g}, " \
                     f"first {(d > 0).nonzero()[:4].tolist()})"
+
+
+@pytest.mark.dev
+@pytest.mark.parametrize("kind", [78, 79, 81])
+@pytest.mark.parametrize("B,T,H,causal,lens", SKIP_CASES + [(1, 64, 2, False, None), (1, 65, 1, False, None),
+                                                         (2, 129, 2, False, None), (2, 200, 2, True, None),
+                                                         (1, 320, 3, False, None)])
+def test_attention_ring_forms_vs_kind62(cuda, kind, B, T, H, causal, lens):
+    """Dev kinds 78 (kind 62 on a three-slot K / V ring, asm DMA), 79 (four slots, the late wave row's
+    PV one tile behind: the stagger) and 81 (kind 79 with packed exp arguments: the same per-element
+    fma) run kind 62's arithmetic in the same order: identical outputs
+    expected, held to the skip test's bound (the hyb loop's rare 1-ulp code-generation effect), across
+    tile counts 1-5 (the ring and its 3- / 4-way unrolled loops) and padded / causal rows."""
+    g = torch.Generator(device="cuda").manual_seed(B * T + 72)
+    qkv = rnd(B * T, 3 * H * 72, scale=1.5, gen=g)
+    sl = None if lens is None else torch.tensor(lens, dtype=torch.int32, device="cuda")
+    nd, d, ulp = _skip_pair(qkv, B, T, H, 72, sl, causal, 62, kind)
+    print(f"kinds 62/{kind}: {nd} of {d.numel()} outputs differ, max {d.max().item():.3g}")
+    assert nd <= 1e-5 * d.numel() + 1 and bool((d <= 2 * ulp).all())
 
 
 @pytest.mark.dev
