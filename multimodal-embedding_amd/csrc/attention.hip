@@ -1369,7 +1369,9 @@ __global__ __launch_bounds__(256, 2) void attn_short_pf_kernel(AttnArgs a, int u
 // unskipped). The same skip in 8-wave blocks (DFN5B,
 // T = 730) measured 18 % slower than kind 38 (0.59 vs 0.50 ms, profiles/r03_v11_attn_dfn5b_ab.log)
 // and is not built.
-template <int HD, int NW, int MINW, bool PRIO, bool DPV = false, bool PF = false, bool SKIP = false>
+// THR (round 4, kinds 86-88): rescale O only when a query's running max grows by more than 2^8 in the
+// exp2 domain (attn_hyb_kernel's XT 2; P <= 256 otherwise, the weight sums share the stale max).
+template <int HD, int NW, int MINW, bool PRIO, bool DPV = false, bool PF = false, bool SKIP = false, bool THR = false>
 __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(MINW))) void attn_m32_kernel(AttnArgs a) {
     constexpr int NSTG = DPV ? 3 : 2;
     constexpr bool ONES = HD % 32 != 0;
@@ -1527,14 +1529,15 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(MINW)))
         for (int e = 0; e < 16; ++e) mloc = fmaxf(mloc, sc[1][e]);
         mloc = xmax32(mloc);
         const float mnew = fmaxf(m, mloc);
-        if (__builtin_amdgcn_ballot_w64(mnew != m)) {
+        if (__builtin_amdgcn_ballot_w64(THR ? (mloc - m) * c > 8.0f : mnew != m)) {
             const float alpha = __builtin_amdgcn_exp2f((m - mnew) * c);
             if (!ONES) lsum *= alpha;
 #pragma unroll
             for (int i = 0; i < NDB; ++i) o[i] *= alpha;
+            if (THR) m = mnew;
         }
-        m = mnew;
-        const float mc = mnew * c;
+        if (!THR) m = mnew;
+        const float mc = m * c;
         float psum = 0.f;
 #pragma unroll
         for (int kb = 0; kb < 2; ++kb)
@@ -2070,9 +2073,9 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(2))) vo
 // cannot prove disjoint from the DMA); 3 = tile t + 2's DMA issued there from inline asm (invisible
 // to hipcc), each tile waiting with a counted vmcnt that leaves the next tile's DMA in flight;
 // 4 (dev kind 79) = RING 3's DMA with the late wave row's PV one tile behind (stagger, below).
-// XT (RING 4 only, dev kinds 80 / 81): VALU trims of qks. 1 = exp2 arguments as packed FMAs (same
-// per-element fma: bit-identical); 2 = rescale O only when some query's max grows by more than 2^8 in
-// the exp2 domain (P <= 256 otherwise; the weight sums use the same stale max: not bit-identical).
+// XT (dev kinds 80-83): VALU trims. 1 = exp2 arguments as packed FMAs (RING 4's qks only; the same
+// per-element fma); 2 = rescale O only when some query's max grows by more than 2^8 in the exp2
+// domain (P <= 256 otherwise; the weight sums use the same stale max: not bit-identical to kind 62).
 template <int HD, int NW, int MINW, bool PRIO, int SKIP = 0, bool DBG = false, int RING = 2, int XT = 0>
 __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(MINW))) void attn_hyb_kernel(AttnArgs a) {
     static_assert(RING >= 2 && RING <= 4, "two to four ring slots");
@@ -2239,7 +2242,7 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(MINW)))
         for (int e = 0; e < 16; ++e) mloc = fmaxf(mloc, sc[1][e]);
         mloc = xmax32(mloc);
         const float mnew = fmaxf(m, mloc);
-        if (__builtin_amdgcn_ballot_w64(mnew != m)) {
+        if (__builtin_amdgcn_ballot_w64((XT & 2) ? (mloc - m) * c > 8.0f : mnew != m)) {
             const float alpha = __builtin_amdgcn_exp2f((m - mnew) * c);  // of query r
             if (!ONES) lsum *= alpha;
 #pragma unroll
@@ -2248,9 +2251,10 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(MINW)))
 #pragma unroll
                 for (int i = 0; i < NDT; ++i) o[u][i] *= au;
             }
+            if (XT & 2) m = mnew;
         }
-        m = mnew;
-        const float mc = mnew * c;
+        if (!(XT & 2)) m = mnew;
+        const float mc = m * c;
         if (DBG && b == 1 && h == 8 && qb == 1 && wave == 2 && t == 1 && (lane == 14 || lane == 46))
             printf("K%d mc lane %d: m %a c %a mc %a\n", SKIP, lane, mnew, c, mc);
         float psum = 0.f;
@@ -3004,6 +3008,28 @@ bool launch_attn(int kind, const AttnArgs& a, int B, int T, int H, hipStream_t s
             hipLaunchKernelGGL((attn_hyb_kernel<HD, 8, 4, true, 2>), dim3(cdiv(T, 256) * H * B), dim3(512), 0, st, a);
         else
             hipLaunchKernelGGL((attn_m32_kernel<HD, 8, 1, true>), dim3(cdiv(T, 256) * H * B), dim3(512), 0, st, a);
+    } else if (kind == 86)  // kind 65 with the 2^8 rescale threshold: production for hd 80 in 9-wave blocks
+        hipLaunchKernelGGL((attn_m32_kernel<HD, 9, 1, true, false, false, true, true>), dim3(cdiv(T, 288) * H * B),
+                           dim3(576), 0, st, a);
+    else if (kind == 87)  // kind 38 with the threshold: production for hd 80 in 8-wave blocks (DFN5B T 730)
+        hipLaunchKernelGGL((attn_m32_kernel<HD, 8, 1, true, false, false, false, true>), dim3(cdiv(T, 256) * H * B),
+                           dim3(512), 0, st, a);
+    else if (kind == 88)  // kind 41 with the threshold: kind 86's no-skip identity reference
+        hipLaunchKernelGGL((attn_m32_kernel<HD, 9, 1, true, false, false, false, true>), dim3(cdiv(T, 288) * H * B),
+                           dim3(576), 0, st, a);
+    else if (kind == 83 || kind == 84) {  // kinds 62 / 58 rescaling O only when a query's running max grows
+                                            // by more than 2^8 in the exp2 domain (XT 2): production for hd 72
+                                            // since round 4 (kind 83; 84 = its no-skip identity reference)
+        if constexpr (HD != 64) {
+            if (kind == 83)
+                hipLaunchKernelGGL((attn_hyb_kernel<HD, 8, 4, true, 2, false, 2, 2>), dim3(cdiv(T, 256) * H * B),
+                                   dim3(512), 0, st, a);
+            else
+                hipLaunchKernelGGL((attn_hyb_kernel<HD, 8, 4, true, 0, false, 2, 2>), dim3(cdiv(T, 256) * H * B),
+                                   dim3(512), 0, st, a);
+        } else {
+            hipLaunchKernelGGL((attn_m32_kernel<HD, 8, 1, true>), dim3(cdiv(T, 256) * H * B), dim3(512), 0, st, a);
+        }
     } else
         return launch_attn_dev<HD>(kind, a, B, T, H, st);
     return true;
@@ -3151,14 +3177,14 @@ bool launch_attn_dev(int kind, const AttnArgs& a, int B, int T, int H, hipStream
         if constexpr (HD != 64)
             hipLaunchKernelGGL((attn_hyb_kernel<HD, 8, 4, true, 2, false, 3>), dim3(cdiv(T, 256) * H * B), dim3(512), 0,
                                st, a);
-        else
-            return false;
+        else  // hd 64: kind 38's kernel, as the other hyb kinds
+            hipLaunchKernelGGL((attn_m32_kernel<HD, 8, 1, true>), dim3(cdiv(T, 256) * H * B), dim3(512), 0, st, a);
     } else if (kind == 79) {  // dev: kind 62 staggered (RING 4): the late wave row runs PV one tile behind
         if constexpr (HD != 64)
             hipLaunchKernelGGL((attn_hyb_kernel<HD, 8, 4, true, 2, false, 4>), dim3(cdiv(T, 256) * H * B), dim3(512), 0,
                                st, a);
         else
-            return false;
+            hipLaunchKernelGGL((attn_m32_kernel<HD, 8, 1, true>), dim3(cdiv(T, 256) * H * B), dim3(512), 0, st, a);
     } else if (kind == 80 || kind == 81) {  // dev: kind 79 with qks VALU trims (80: packed exp arguments +
                                             // 2^8 rescale threshold; 81: packed exp arguments only)
         if constexpr (HD != 64) {
@@ -3169,7 +3195,14 @@ bool launch_attn_dev(int kind, const AttnArgs& a, int B, int T, int H, hipStream
                 hipLaunchKernelGGL((attn_hyb_kernel<HD, 8, 4, true, 2, false, 4, 1>), dim3(cdiv(T, 256) * H * B),
                                    dim3(512), 0, st, a);
         } else {
-            return false;
+            hipLaunchKernelGGL((attn_m32_kernel<HD, 8, 1, true>), dim3(cdiv(T, 256) * H * B), dim3(512), 0, st, a);
+        }
+    } else if (kind == 82) {  // dev: the 2^8 rescale threshold on kind 79's stagger
+        if constexpr (HD != 64) {
+            hipLaunchKernelGGL((attn_hyb_kernel<HD, 8, 4, true, 2, false, 4, 2>), dim3(cdiv(T, 256) * H * B),
+                               dim3(512), 0, st, a);
+        } else {
+            hipLaunchKernelGGL((attn_m32_kernel<HD, 8, 1, true>), dim3(cdiv(T, 256) * H * B), dim3(512), 0, st, a);
         }
     } else if (kind == 63) {  // dev: kind 62 as in round 2 (the skipped block's fill and the accumulator
                               // init as per-tile register moves)
@@ -3281,14 +3314,17 @@ int attention_entry(int form, const void* qkv, int ld_qkv, void* out, int ld_out
     // 80 rows -- 9 % less MFMA work than either single-shape form under the power cap): SigLIP
     // vision level to 2 % faster than kind 30 (profiles/r02_attn_hyb_bench.log, r02_hyb_attn.log);
     // kind 62 = kind 58 skipping the last tile's second 32-key block (wholly past T = 729): +1.2 %
-    // (profiles/r02_hyb_skip_bench.log, 4 of 4 A/B pairs).
+    // (profiles/r02_hyb_skip_bench.log, 4 of 4 A/B pairs). Round 4: kind 83 = kind 62 rescaling O only
+    // when a query's running max grows by more than 2^8 in the exp2 domain (the rescale branch ran on
+    // almost every tile: ~27 of ~174 VALU per wave and tile): 628 -> 660 TF/s at the job's 417-image
+    // batch (profiles/r04_v19_attn_threshold_ab.log); mean |error| vs fp64 0.00045 -> 0.00052.
     int kind = T <= 64 ? 16
                : (T <= 128 || hd == 64) ? 0
                : (hd == 80 && pad9 * 10 < min(pad8, pad4) * 9) ? 65
                : hd == 80 && pad8 * 10 <= pad4 * 11 ? 38
                : pad9 * 10 < min(pad8, pad4) * 9 ? 35
                : (hd == 80 && pad12 <= pad8 && pad12 * 10 <= pad4 * 11) ? 23
-               : (pad8 * 10 <= pad4 * 11 ? (hd == 72 ? 62 : 11) : 14);
+               : (pad8 * 10 <= pad4 * 11 ? (hd == 72 ? 83 : 11) : 14);
 #ifdef MME_DEV
     if (form >= 1 && form <= 4 && hd == 72) {  // dev-only diagnostic builds
         const dim3 grid(cdiv(T, 128) * H * B);

@@ -129,12 +129,13 @@ def test_attention(cuda, B, T, H, hd, causal, lens):
     torch.testing.assert_close(out.float(), ref, atol=2e-2, rtol=2e-2)
 
 
-PROD_ATTN_KINDS = (38, 41, 62, 65)  # in the production library; the rest are development forms (libmme_dev.so)
+PROD_ATTN_KINDS = (38, 41, 58, 62, 65, 83, 84, 86, 87, 88)  # in the production library; the rest are development forms (libmme_dev.so)
 
 
 @pytest.mark.parametrize("kind", [k if k in PROD_ATTN_KINDS else pytest.param(k, marks=pytest.mark.dev)
                                   for k in (38, 39, 40, 41, 42, 43, 44, 45, 46, 47, 48, 49, 50, 51, 52, 54, 55, 56,
-                                            57, 58, 59, 60, 61, 62, 63, 65, 78, 79, 80, 81)])
+                                            57, 58, 59, 60, 61, 62, 63, 65, 78, 79, 80, 81, 82, 83, 84,
+                                            86, 87, 88)])
 @pytest.mark.parametrize("B,T,H,hd,causal,lens", [
     (2, 729, 4, 72, False, None),       # SigLIP vision geometry
     (2, 520, 3, 72, False, [520, 301]),  # key padding, partial last tile
@@ -181,12 +182,13 @@ def _skip_pair(qkv, B, T, H, hd, sl, causal, ref, kind):
     return int((d > 0).sum()), d, ulp
 
 
-@pytest.mark.parametrize("hd,kind,ref", [(80, 65, 41), (72, 62, 58)])
+@pytest.mark.parametrize("hd,kind,ref", [(80, 65, 41), (72, 62, 58), (72, 83, 84), (80, 86, 88)])
 @pytest.mark.parametrize("B,T,H,causal,lens", SKIP_CASES)
 def test_attention_skip_vs_unskipped(cuda, hd, kind, ref, B, T, H, causal, lens):
     """The production kernels that skip a tile's second 32-key block when it lies wholly past the keys
-    (kind 65: attn_m32_kernel in 9-wave blocks, hd 80; kind 62: attn_hyb_kernel, hd 72) against the same
-    kernels without the skip (kinds 41 / 58). Round 4 found (tools/attn_skip_diff.py,
+    (kind 65: attn_m32_kernel in 9-wave blocks, hd 80; kind 62: attn_hyb_kernel, hd 72; kind 83: kind 62
+    with the 2^8 rescale threshold, production for hd 72 since round 4) against the same kernels without
+    the skip (kinds 41 / 58 / 84). Round 4 found (tools/attn_skip_diff.py,
     profiles/r04_v7_attn_skip_*.log): the skip itself is exact -- an MFMA with an all-zero operand leaves
     its accumulator bit-identical (tools/mfma_zero_probe.hip) and the ping-pong kernel carrying the same
     skip (dev kind 70) equals kind 58 on every output (test below) -- and the rare differences are a
