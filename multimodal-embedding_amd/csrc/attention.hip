@@ -42,9 +42,11 @@ struct AttnArgs {
     float scale_log2;
 };
 
-template <int HD, int DIAG = 0>
+template <int HD, int DIAG = 0, bool THR = false>
 __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(AttnArgs a) {
     // DIAG (dev builds, wrong results): 1 no K/V global loads, 2 no exp2, 3 no PV MFMA, 4 no QK MFMA
+    // THR (round 4, kind 89): O and the weight sum rescaled only when a query's running max grows by
+    // more than 2^8 in the exp2 domain (attn_hyb_kernel's XT 2), instead of on every tile
     // QK^T reduction depth covered by 16x16x32 steps: 64, or 96 for head dims
     // 72/80 zero-padded. Only same-shape MFMA accumulation chains are used: a
     // 16x16x16 tail step chained on a 16x16x32 result was observed to be
@@ -199,6 +201,27 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(AttnArgs a) {
             mloc = fmaxf(mloc, __shfl_xor(mloc, 16, 64));
             mloc = fmaxf(mloc, __shfl_xor(mloc, 32, 64));
             const float mnew = fmaxf(m[u], mloc);
+            if (THR) {
+                if (__builtin_amdgcn_ballot_w64((mloc - m[u]) * c > 8.0f)) {
+                    const float alpha = __builtin_amdgcn_exp2f((m[u] - mnew) * c);
+                    m[u] = mnew;
+                    lsum[u] *= alpha;
+#pragma unroll
+                    for (int i = 0; i < NDT; ++i) o[u][i] *= alpha;
+                }
+                const float mc = m[u] * c;
+                float psum = 0.f;
+#pragma unroll
+                for (int kt = 0; kt < 4; ++kt)
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        const float pv = __builtin_amdgcn_exp2f(sc[u][kt][r] * c - mc);
+                        sc[u][kt][r] = pv;
+                        psum += pv;
+                    }
+                lsum[u] += psum;
+                continue;
+            }
             const float alpha = __builtin_amdgcn_exp2f((m[u] - mnew) * c);
             m[u] = mnew;
             const float mc = mnew * c;
@@ -3017,6 +3040,8 @@ bool launch_attn(int kind, const AttnArgs& a, int B, int T, int H, hipStream_t s
     else if (kind == 88)  // kind 41 with the threshold: kind 86's no-skip identity reference
         hipLaunchKernelGGL((attn_m32_kernel<HD, 9, 1, true, false, false, false, true>), dim3(cdiv(T, 288) * H * B),
                            dim3(576), 0, st, a);
+    else if (kind == 89)  // kind 0 (attn_fwd_kernel) with the 2^8 rescale threshold
+        hipLaunchKernelGGL((attn_fwd_kernel<HD, 0, true>), dim3(cdiv(T, 128) * H * B), dim3(256), 0, st, a);
     else if (kind == 83 || kind == 84) {  // kinds 62 / 58 rescaling O only when a query's running max grows
                                             // by more than 2^8 in the exp2 domain (XT 2): production for hd 72
                                             // since round 4 (kind 83; 84 = its no-skip identity reference)
