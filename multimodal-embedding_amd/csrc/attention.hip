@@ -3343,10 +3343,13 @@ int attention_entry(int form, const void* qkv, int ld_qkv, void* out, int ld_out
     // when a query's running max grows by more than 2^8 in the exp2 domain (the rescale branch ran on
     // almost every tile: ~27 of ~174 VALU per wave and tile): 628 -> 660 TF/s at the job's 417-image
     // batch (profiles/r04_v19_attn_threshold_ab.log); mean |error| vs fp64 0.00045 -> 0.00052.
+    // The same threshold in attn_m32_kernel (hd 80: kinds 86 / 87 = 65 / 38, ViT-H +3 %, DFN5B +4.5 %) and
+    // attn_fwd_kernel (kind 89 = kind 0: CLIP-L vision +3 %, CLIP causal text +1 %;
+    // profiles/r04_v20_attn_threshold_hd80_hd64_ab.log).
     int kind = T <= 64 ? 16
-               : (T <= 128 || hd == 64) ? 0
-               : (hd == 80 && pad9 * 10 < min(pad8, pad4) * 9) ? 65
-               : hd == 80 && pad8 * 10 <= pad4 * 11 ? 38
+               : (T <= 128 || hd == 64) ? 89
+               : (hd == 80 && pad9 * 10 < min(pad8, pad4) * 9) ? 86
+               : hd == 80 && pad8 * 10 <= pad4 * 11 ? 87
                : pad9 * 10 < min(pad8, pad4) * 9 ? 35
                : (hd == 80 && pad12 <= pad8 && pad12 * 10 <= pad4 * 11) ? 23
                : (pad8 * 10 <= pad4 * 11 ? (hd == 72 ? 83 : 11) : 14);
