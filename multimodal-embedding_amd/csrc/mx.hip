@@ -1165,9 +1165,9 @@ int launch_mx9(const MxArgs& a, hipStream_t s) {
 
 #endif  // MME_DEV
 
-// Kernel form per call (mme_gemm_mx_form): -1 = production (mx10 where its geometry holds), 0 = the
-// round-2 kernel, 2 = its per-wave epilogue alone, 3 = + the scale wave (mx10's fallback), 9 = mx9
-// (development build). The development build keeps a process-wide default (mme_gemm_mx_variant).
+// Kernel form per call (mme_gemm_mx_form): -1 = production (mx11 where its geometry holds, else mx10),
+// 10 = mx10, 0 = the round-2 kernel, 2 = its per-wave epilogue alone, 3 = + the scale wave (mx10's
+// fallback), 9 = mx9 (development build). The development build keeps a process-wide default (mme_gemm_mx_variant).
 #ifdef MME_DEV
 int g_mx_variant = -1;
 inline int mx_default_form() { return g_mx_variant; }
