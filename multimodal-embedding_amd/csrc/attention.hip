@@ -3222,6 +3222,18 @@ bool launch_attn_dev(int kind, const AttnArgs& a, int B, int T, int H, hipStream
         } else {
             hipLaunchKernelGGL((attn_m32_kernel<HD, 8, 1, true>), dim3(cdiv(T, 256) * H * B), dim3(512), 0, st, a);
         }
+    } else if (kind >= 91 && kind <= 93) {  // dev: kind 86 in 5-wave (160-query; 93: <= 128 VGPRs) / 4-wave
+                                            // blocks: more, smaller blocks per CU to overlap the prologues at
+                                            // T 257 (ViT-H)
+        if (kind == 91)
+            hipLaunchKernelGGL((attn_m32_kernel<HD, 5, 1, true, false, false, true, true>), dim3(cdiv(T, 160) * H * B),
+                               dim3(320), 0, st, a);
+        else if (kind == 93)  // 5-wave blocks held to 128 VGPRs: three blocks per CU
+            hipLaunchKernelGGL((attn_m32_kernel<HD, 5, 4, true, false, false, true, true>), dim3(cdiv(T, 160) * H * B),
+                               dim3(320), 0, st, a);
+        else
+            hipLaunchKernelGGL((attn_m32_kernel<HD, 4, 1, true, false, false, true, true>), dim3(cdiv(T, 128) * H * B),
+                               dim3(256), 0, st, a);
     } else if (kind == 82) {  // dev: the 2^8 rescale threshold on kind 79's stagger
         if constexpr (HD != 64) {
             hipLaunchKernelGGL((attn_hyb_kernel<HD, 8, 4, true, 2, false, 4, 2>), dim3(cdiv(T, 256) * H * B),

@@ -135,7 +135,7 @@ PROD_ATTN_KINDS = (38, 41, 58, 62, 65, 83, 84, 86, 87, 88, 89)  # in the product
 @pytest.mark.parametrize("kind", [k if k in PROD_ATTN_KINDS else pytest.param(k, marks=pytest.mark.dev)
                                   for k in (38, 39, 40, 41, 42, 43, 44, 45, 46, 47, 48, 49, 50, 51, 52, 54, 55, 56,
                                             57, 58, 59, 60, 61, 62, 63, 65, 78, 79, 80, 81, 82, 83, 84,
-                                            86, 87, 88, 89)])
+                                            86, 87, 88, 89, 91, 92, 93)])
 @pytest.mark.parametrize("B,T,H,hd,causal,lens", [
     (2, 729, 4, 72, False, None),       # SigLIP vision geometry
     (2, 520, 3, 72, False, [520, 301]),  # key padding, partial last tile
