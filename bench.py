@@ -207,17 +207,21 @@ def retrieval_parity(tables, metrics, caps_per_image: int = 5):
         _, rsc = R.topk(s, k + 1)
         tied = np.zeros(len(ridx), bool)
         tied[ranked.tie_rows.cpu().numpy()] = True
-        same, near = R.compare_topk(ranked.idx.cpu().numpy(), ridx, rsc, exact_rows=tied)
+        only = []
+        same, near = R.compare_topk(ranked.idx.cpu().numpy(), ridx, rsc, exact_rows=tied,
+                                    dev_score=ranked.score.cpu().numpy(), oracle_only=only)
         rows[name] = {"rows_identical": f"{int(same.sum())}/{len(same)}", "near_tie_rows": int(near.sum()),
                       "decisive_rows_differing": int((~same & ~near).sum()),
-                      "exact_tie_rows_torch_order": int(ranked.tie_rows.numel())}
+                      "exact_tie_rows_torch_order": int(ranked.tie_rows.numel()),
+                      "oracle_only_exact_tie_rows": len(only)}
         for kr, h in zip((1, 5, 10), R.hits(s, tc).sum(0)):
             ref_metrics[f"{name}_R@{kr}"] = 100.0 * h / n
     return {"recall_identical": all(ref_metrics[k] == metrics[k] for k in ref_metrics),
             "oracle_recall": {k: round(v, 2) for k, v in ref_metrics.items()}, "rows": rows,
             "near_tie_rule": "neighbouring oracle scores among the top 11 within 1e-5*|s1|; exact ties are not "
                              "exempt on rows the device finds tied too (torch.topk's order, replayed on both "
-                             "sides), an oracle-only exact tie is a near tie",
+                             "sides); an oracle-only exact tie is a near tie only where the device's own "
+                             "scores differ at that place (counted in oracle_only_exact_tie_rows)",
             "checker": "oracle/retrieval.py on the job's own embeddings (numpy fp32 + torch.topk order, host)",
             "seconds": round(time.time() - t0, 2)}
 

@@ -215,7 +215,7 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(AttnArgs a) {
                 for (int kt = 0; kt < 4; ++kt)
 #pragma unroll
                     for (int r = 0; r < 4; ++r) {
-                        const float pv = __builtin_amdgcn_exp2f(sc[u][kt][r] * c - mc);
+                        const float pv = __builtin_amdgcn_exp2f(__builtin_fmaf(sc[u][kt][r], c, -mc));
                         sc[u][kt][r] = pv;
                         psum += pv;
                     }
@@ -230,7 +230,7 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(AttnArgs a) {
             for (int kt = 0; kt < 4; ++kt)
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
-                    const float pv = DIAG == 2 ? sc[u][kt][r] * c - mc : __builtin_amdgcn_exp2f(sc[u][kt][r] * c - mc);
+                    const float pv = DIAG == 2 ? __builtin_fmaf(sc[u][kt][r], c, -mc) : __builtin_amdgcn_exp2f(__builtin_fmaf(sc[u][kt][r], c, -mc));
                     sc[u][kt][r] = pv;
                     psum += pv;
                 }
@@ -472,8 +472,8 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(MINW)))
             for (int kt = 0; kt < 4; ++kt)
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
-                    const float pv = DIAG == 2 ? sc[u][kt][r] * c - mc
-                                               : __builtin_amdgcn_exp2f(sc[u][kt][r] * c - mc);
+                    const float pv = DIAG == 2 ? __builtin_fmaf(sc[u][kt][r], c, -mc)
+                                               : __builtin_amdgcn_exp2f(__builtin_fmaf(sc[u][kt][r], c, -mc));
                     sc[u][kt][r] = pv;
                     psum += pv;
                 }
@@ -769,7 +769,7 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(MINW)))
                 for (int kt = 0; kt < 4; ++kt)
 #pragma unroll
                     for (int r = 0; r < 4; ++r) {
-                        const float pv = __builtin_amdgcn_exp2f(sc[u][kt][r] * c - mc);
+                        const float pv = __builtin_amdgcn_exp2f(__builtin_fmaf(sc[u][kt][r], c, -mc));
                         sc[u][kt][r] = pv;
                         if (!ONES) psum += pv;
                     }
@@ -1097,7 +1097,7 @@ __global__ __launch_bounds__(256, 3) void attn_short_kernel(AttnArgs a, int unit
         for (int kt = 0; kt < 4; ++kt)
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
-                const float pv = __builtin_amdgcn_exp2f(sc[u][kt][r] * c - mc);
+                const float pv = __builtin_amdgcn_exp2f(__builtin_fmaf(sc[u][kt][r], c, -mc));
                 sc[u][kt][r] = pv;
                 psum += pv;
             }
@@ -1297,7 +1297,7 @@ __global__ __launch_bounds__(256, 2) void attn_short_pf_kernel(AttnArgs a, int u
             for (int kt = 0; kt < 4; ++kt)
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
-                    const float pv = __builtin_amdgcn_exp2f(sc[u][kt][r] * c - mc);
+                    const float pv = __builtin_amdgcn_exp2f(__builtin_fmaf(sc[u][kt][r], c, -mc));
                     sc[u][kt][r] = pv;
                     psum += pv;
                 }
@@ -1566,7 +1566,7 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(MINW)))
         for (int kb = 0; kb < 2; ++kb)
 #pragma unroll
             for (int e = 0; e < 16; ++e) {
-                const float pv = __builtin_amdgcn_exp2f(sc[kb][e] * c - mc);
+                const float pv = __builtin_amdgcn_exp2f(__builtin_fmaf(sc[kb][e], c, -mc));
                 sc[kb][e] = pv;
                 if (!ONES) psum += pv;
             }
@@ -1868,7 +1868,7 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(2))) vo
         for (int kb = 0; kb < 2; ++kb)
 #pragma unroll
             for (int e = 0; e < 16; ++e) {
-                const float pv = __builtin_amdgcn_exp2f(s2[kb][e] * c - mc);
+                const float pv = __builtin_amdgcn_exp2f(__builtin_fmaf(s2[kb][e], c, -mc));
                 s2[kb][e] = pv;
                 if (!ONES) psum += pv;
             }
@@ -1994,7 +1994,7 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(2))) vo
             for (int kb = 0; kb < 2; ++kb)
 #pragma unroll
                 for (int e = 0; e < 16; ++e) {
-                    const float pv = __builtin_amdgcn_exp2f(sc[u][kb][e] * c - mc);
+                    const float pv = __builtin_amdgcn_exp2f(__builtin_fmaf(sc[u][kb][e], c, -mc));
                     sc[u][kb][e] = pv;
                     if (!ONES) psum += pv;
                 }
@@ -2285,7 +2285,7 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(MINW)))
         for (int kb = 0; kb < 2; ++kb)
 #pragma unroll
             for (int e = 0; e < 16; ++e) {
-                sc[kb][e] = __builtin_amdgcn_exp2f(sc[kb][e] * c - mc);
+                sc[kb][e] = __builtin_amdgcn_exp2f(__builtin_fmaf(sc[kb][e], c, -mc));
                 if (!ONES) psum += sc[kb][e];
             }
         if (!ONES) lsum += psum;
@@ -2399,8 +2399,8 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(MINW)))
                     sc[kb][e] = __builtin_amdgcn_exp2f(x.x);
                     sc[kb][e + 1] = __builtin_amdgcn_exp2f(x.y);
                 } else {
-                    sc[kb][e] = __builtin_amdgcn_exp2f(sc[kb][e] * c - mc);
-                    sc[kb][e + 1] = __builtin_amdgcn_exp2f(sc[kb][e + 1] * c - mc);
+                    sc[kb][e] = __builtin_amdgcn_exp2f(__builtin_fmaf(sc[kb][e], c, -mc));
+                    sc[kb][e + 1] = __builtin_amdgcn_exp2f(__builtin_fmaf(sc[kb][e + 1], c, -mc));
                 }
                 if (!ONES) {
                     psum += sc[kb][e];
@@ -2751,7 +2751,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(MINW))) voi
 #pragma unroll
         for (int kb = 0; kb < 2; ++kb)
 #pragma unroll
-            for (int e = 0; e < 16; ++e) sc[kb][e] = __builtin_amdgcn_exp2f(sc[kb][e] * c - mc);
+            for (int e = 0; e < 16; ++e) sc[kb][e] = __builtin_amdgcn_exp2f(__builtin_fmaf(sc[kb][e], c, -mc));
         phalf = t * 64 + 32 >= Tk;
 #pragma unroll
         for (int kb = 0; kb < 2; ++kb) {

@@ -1601,11 +1601,26 @@ __global__ __launch_bounds__(C::NT, 2) void gemm_pipe10_kernel(GemmArgs p) {
         pipe10_run<C, GROUP_M, ACT, false, SPLIT>(p, lds, wave);
 }
 
+// Workgroups of a persistent GEMM grid: one per CU (160 KiB of LDS each), rounded down to a multiple of
+// the 8 XCDs so every XCD walks an equal share of the tile order (xcd_remap); the CU count is the
+// device's own (a compute-partitioned device has fewer than 256), read once per device.
+int persistent_grid(int ntiles) {
+    static int cus[64] = {0};
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) dev = 0;
+    if (cus[dev] == 0) {
+        int n = 0;
+        if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
+        cus[dev] = n >= 8 ? n / 8 * 8 : n;
+    }
+    return std::min(ntiles, cus[dev]);
+}
+
 template <class C, int GROUP_M, bool SPLIT>
 int launch_pipe10(const GemmArgs& a, hipStream_t s) {
     const int nbm = (a.M + C::BM - 1) / C::BM, nbn = (a.N + C::BN - 1) / C::BN;
     const int ntiles = SPLIT ? split_tiles(nbm, a.N / C::BN) : nbm * nbn;
-    const dim3 grid(std::min(ntiles, 256)), block(C::NT);  // one workgroup per CU (160 KiB of LDS)
+    const dim3 grid(persistent_grid(ntiles)), block(C::NT);
     switch (a.act) {
         case MME_ACT_GELU_TANH:
             hipLaunchKernelGGL((gemm_pipe10_kernel<C, GROUP_M, MME_ACT_GELU_TANH, SPLIT>), grid, block, 0, s, a);

@@ -332,19 +332,25 @@ class ColPaliProcessor:
     """process_images / process_queries / score (main.py:403,423,467) over the device path.
 
     Images: u8 arrays / PIL -> pixel_values by the PIL-exact preprocess kernel (448 square).
-    Queries: strings through the offline hash tokenizer (vocab files absent) or
-    pre-tokenized id lists; ColPali layout, left padding to the batch-longest."""
+    Queries: pre-tokenized id lists, or strings through the checkpoint's tokenizer (`tokenizer=`:
+    an HF-compatible callable, asked for the caption body only, `add_special_tokens=False`; the
+    ColPali layout adds bos, the query prefix, the augmentation pads and the newline); without
+    one, strings raise unless `allow_hash_tokenizer=True` selects the offline word-hash stand-in.
+    ColPali layout, left padding to the batch-longest."""
 
-    def __init__(self, spec: ColPaliSpec, device="cuda"):
+    def __init__(self, spec: ColPaliSpec, device="cuda", tokenizer=None, allow_hash_tokenizer: bool = False):
         from .colpali import ColPaliScorer
         from .config import TextConfig
         from .processor import HashTokenizer, Processor
         self.spec = spec
         self.device = torch.device(device)
         t = spec.text
-        self.tokenizer = HashTokenizer(t.vocab, spec.bos_id, spec.eos_id, spec.pad_id, 1 << 20, reserved=3)
-        self.tokenizer.hi = min(self.tokenizer.hi, spec.image_token_id)  # never emit <image>
-        self.tokenizer.lo = max(self.tokenizer.lo, spec.newline_id + 1)
+        self.text_tokenizer = tokenizer
+        self.tokenizer = None
+        if tokenizer is None and allow_hash_tokenizer:
+            self.tokenizer = HashTokenizer(t.vocab, spec.bos_id, spec.eos_id, spec.pad_id, 1 << 20, reserved=3)
+            self.tokenizer.hi = min(self.tokenizer.hi, spec.image_token_id)  # never emit <image>
+            self.tokenizer.lo = max(self.tokenizer.lo, spec.newline_id + 1)
         shim = type("S", (), {"image_proc": spec.image_proc,
                               "text": TextConfig(hidden=1, intermediate=1, layers=0, heads=1, act="none", eps=0.0)})
         self._img = Processor(shim, device=device)
@@ -366,16 +372,26 @@ class ColPaliProcessor:
         return b
 
     def process_queries(self, queries, **_):
-        toks = [self.tokenizer.encode(q) if isinstance(q, str) else [int(x) for x in q] for q in queries]
+        from .processor import _as_rows, _ids, no_string_tokenizer
+        strs = [q for q in queries if isinstance(q, str)]
+        body = iter(())
+        if strs and self.text_tokenizer is not None:
+            body = iter(_as_rows(_ids(self.text_tokenizer(strs, add_special_tokens=False, padding=False,
+                                                          truncation=False))))
+        elif strs and self.tokenizer is None:
+            raise no_string_tokenizer("ColPaliProcessor.process_queries")
+        toks = [(next(body) if self.text_tokenizer is not None else self.tokenizer.encode(q))
+                if isinstance(q, str) else [int(x) for x in q] for q in queries]
         return self._batch([self.spec.query_tokens(t) for t in toks])
 
     def score(self, qs, ps, **kw):
         return self._scorer.score(qs, ps, **kw)
 
 
-def load_colpali(name: str = "ColPali-v1.3", seed: int = 0, device="cuda", state_dict=None):
+def load_colpali(name: str = "ColPali-v1.3", seed: int = 0, device="cuda", state_dict=None, tokenizer=None,
+                 allow_hash_tokenizer: bool = False):
     """(model, processor) — the offline counterpart of ColPali.from_pretrained / ColPaliProcessor
-    (main.py:808-812)."""
+    (main.py:808-812); `tokenizer` / `allow_hash_tokenizer` as ColPaliProcessor."""
     spec = get_spec(name)
     return ColPaliModel.from_spec(spec, seed=seed, device=device, state_dict=state_dict), \
-        ColPaliProcessor(spec, device=device)
+        ColPaliProcessor(spec, device=device, tokenizer=tokenizer, allow_hash_tokenizer=allow_hash_tokenizer)

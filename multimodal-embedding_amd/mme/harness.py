@@ -4,10 +4,15 @@ Restates run_bootstrap_benchmark (main.py:478-667) for the device-resident
 path:
   * images in dataset order; captions all_captions[5i + j] = caption j of
     image i; T2I queries = caption 0 of each image (main.py:503-529);
-  * timed region = encode n images + n T2I captions + 5n captions
-    (main.py:534-559) plus both score directions and recall (the v28
-    definition the published QPS uses, …v28_publication_ready.py:305-408);
-    warmup runs outside the region (v28);
+  * CSV timing columns exactly as main.py:534-559, 657-660 define them:
+    the clock starts BEFORE the warmup, Encoding_Time = warmup + the three
+    encodes (n images, n T2I captions, 5n captions), QPS = Img_per_sec =
+    n / Encoding_Time, Time = everything up to the metrics (bootstrap
+    included);
+  * the v28 end-to-end rate (…v28_publication_ready.py:305-408: warmup
+    outside, encode + both score directions + recall inside; the definition
+    bench.py's headline `value` and the published A40 47.1 img/s use) is
+    returned beside the row (`timings=`), not in the CSV;
   * metrics on the identity sample (SURVEY.md §0.5), I2T orientation fixed;
   * CSV columns of main.py:642-665 (identity sample: mean = lower = upper,
     std = 0).
@@ -43,23 +48,39 @@ def encode_job(model, images_u8: torch.Tensor, caption_ids: torch.Tensor, captio
     return img, t2i, all_txt
 
 
+def timing_columns(n: int, t_start: float, t_encoded: float, t_done: float) -> Dict[str, float]:
+    """The CSV's four timing columns from three clock readings (main.py:534-559, 657-660):
+    t_start before the warmup, t_encoded after the third encode, t_done after the metrics."""
+    enc = t_encoded - t_start
+    return {"Time": t_done - t_start, "QPS": n / enc, "Encoding_Time": enc, "Img_per_sec": n / enc}
+
+
+def _sync() -> None:
+    if torch.cuda.is_available():
+        torch.cuda.synchronize()
+
+
 def run_benchmark(model, images_u8: torch.Tensor, caption_ids: torch.Tensor, caption_lens=None,
                   caps_per_image: int = 5, warmup: bool = True, n_iterations: int = 0, seed: int = 0,
-                  **kw) -> Dict[str, object]:
+                  timings: Optional[Dict[str, float]] = None, clock=time.time, **kw) -> Dict[str, object]:
     """One timed encode + retrieval job; returns the reference's result row.
 
     n_iterations > 0: the metrics are the bootstrap of run_bootstrap_benchmark
     (main.py:563-651: resamples with replacement, mean / 95 % CI / std per metric) on
-    the device (mme.bootstrap); 0: the identity sample (mean = lower = upper, std 0)."""
+    the device (mme.bootstrap); 0: the identity sample (mean = lower = upper, std 0).
+    timings (a dict, optional) receives warmup_s / encode_s / retrieval_s and the v28 rate
+    e2e_img_per_sec = n / (encode_s + retrieval_s) (warmup outside, as v28 times it)."""
     name = model.spec.name
-    if warmup:  # v28: warmup outside the timed region
+    _sync()
+    t_start = clock()  # main.py:534: the clock starts before the warmup
+    if warmup:  # main.py:537-543: two items through the same encode path
         encode_job(model, images_u8[:2], caption_ids[: 2 * caps_per_image], None if caption_lens is None else
                    caption_lens[: 2 * caps_per_image], caps_per_image, **kw)
-    torch.cuda.synchronize()
-    t0 = time.time()
+    _sync()
+    t_warm = clock()
     img, t2i, all_txt = encode_job(model, images_u8, caption_ids, caption_lens, caps_per_image, **kw)
-    torch.cuda.synchronize()
-    t_enc = time.time() - t0
+    _sync()
+    t_encoded = clock()
     n = images_u8.shape[0]
     row: Dict[str, object] = {"Model": name}
     if n_iterations > 0:
@@ -72,13 +93,13 @@ def run_benchmark(model, images_u8: torch.Tensor, caption_ids: torch.Tensor, cap
         for k in METRIC_KEYS:
             v = metrics[k]
             row[f"{k}_mean"], row[f"{k}_lower"], row[f"{k}_upper"], row[f"{k}_std"] = v, v, v, 0.0
-    torch.cuda.synchronize()
-    t_total = time.time() - t0
-    row["Time"] = t_total
-    row["QPS"] = n / t_total
-    row["Encoding_Time"] = t_enc
-    row["Img_per_sec"] = n / t_enc
+    _sync()
+    t_done = clock()
+    row.update(timing_columns(n, t_start, t_encoded, t_done))
     row["_failure_analysis"] = {}
+    if timings is not None:
+        timings.update(warmup_s=t_warm - t_start, encode_s=t_encoded - t_warm, retrieval_s=t_done - t_encoded,
+                       e2e_img_per_sec=n / (t_done - t_warm))
     return row
 
 

@@ -505,10 +505,12 @@ class CLIPModel(DualEncoder):
 
 
 def load_model(name: str, seed: int = 0, device="cuda", state_dict=None, batch_size: Optional[int] = None,
-               fp8: bool = False) -> Tuple[DualEncoder, "object"]:
+               fp8: bool = False, tokenizer=None, allow_hash_tokenizer: bool = False) -> Tuple[DualEncoder, "object"]:
     """(model, processor) for a registry name — the offline counterpart of
     from_pretrained(m_info['id']) (main.py:808-820). fp8=True: the mx8 encoder
-    GEMM mode of BASELINE configs[4] (DualEncoder.enable_fp8)."""
+    GEMM mode of BASELINE configs[4] (DualEncoder.enable_fp8). tokenizer: the
+    checkpoint's HF tokenizer for caption strings (main.py:427); without it strings
+    raise unless allow_hash_tokenizer=True (mme.processor)."""
     from .processor import Processor
     spec = get_spec(name)
     if batch_size is not None:
@@ -517,4 +519,4 @@ def load_model(name: str, seed: int = 0, device="cuda", state_dict=None, batch_s
     model = cls.from_spec(spec, seed=seed, device=device, state_dict=state_dict)
     if fp8:
         model.enable_fp8()
-    return model, Processor(spec, device=device)
+    return model, Processor(spec, device=device, tokenizer=tokenizer, allow_hash_tokenizer=allow_hash_tokenizer)

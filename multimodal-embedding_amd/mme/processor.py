@@ -6,12 +6,17 @@ runs on the device (libmme mme_preprocess_u8); this module only turns PIL
 images / arrays into a u8 NHWC tensor and computes the resize geometry.
 
 Text: the reference tokenizes with the model's HF tokenizer (main.py:427,
-padding=True, truncation=True). The vocab files do not exist offline, so
-strings go through a deterministic word-hash tokenizer with the model's
-special tokens (documented stand-in); pre-tokenized id lists pass through
-unchanged. Padding/truncation semantics match HF: right padding to the
-batch's longest row with pad_id, attention_mask 1/0, truncation to max_pos
-keeping the trailing eos.
+padding=True, truncation=True). A caller that has the checkpoint's tokenizer
+passes it (`Processor(spec, tokenizer=tok)`, `load_model(..., tokenizer=tok)`):
+any HF-compatible callable `tok(batch, padding=..., truncation=..., max_length=...)`
+returning `input_ids` / `attention_mask`. A batch of strings is then handed to it
+whole, exactly as main.py:427 does, and its padding / mask come back unchanged.
+Pre-tokenized id lists pass through unchanged, padded here with HF's semantics:
+right padding to the batch's longest row with pad_id, attention_mask 1/0,
+truncation to max_pos keeping the trailing eos. Strings with no tokenizer raise:
+the offline vocab-free stand-in (`HashTokenizer`, deterministic word hashes with
+the model's special tokens) must be asked for explicitly with
+`allow_hash_tokenizer=True`, so real captions are never silently hashed.
 """
 from __future__ import annotations
 
@@ -81,14 +86,49 @@ class HashTokenizer:
         return [self.lo + zlib.crc32(w.encode()) % span for w in text.lower().split()]
 
 
-class Processor:
-    """processor(images=..., text=..., return_tensors='pt', padding=True, truncation=True)."""
+def _as_rows(x) -> List[List[int]]:
+    """input_ids of a tokenizer's output (tensor, array or nested lists) -> list of int lists."""
+    if isinstance(x, torch.Tensor):
+        x = x.tolist()
+    elif isinstance(x, np.ndarray):
+        x = x.tolist()
+    return [[int(v) for v in r] for r in x]
 
-    def __init__(self, spec: ModelSpec, device="cuda"):
+
+def _ids(enc):
+    """`input_ids` of a BatchEncoding / dict / object returned by a tokenizer."""
+    try:
+        return enc["input_ids"]
+    except (KeyError, TypeError):
+        return enc.input_ids
+
+
+def _mask(enc):
+    try:
+        return enc["attention_mask"]
+    except (KeyError, TypeError):
+        return getattr(enc, "attention_mask", None)
+
+
+def no_string_tokenizer(what: str) -> ValueError:
+    return ValueError(
+        f"{what} got caption strings but no tokenizer: pass the checkpoint's tokenizer (tokenizer=...), "
+        "pre-tokenized id lists, or allow_hash_tokenizer=True for the offline word-hash stand-in")
+
+
+class Processor:
+    """processor(images=..., text=..., return_tensors='pt', padding=True, truncation=True).
+
+    tokenizer: the model's HF-compatible tokenizer (called on batches of strings, main.py:427);
+    allow_hash_tokenizer: without one, hash strings with the offline stand-in instead of raising."""
+
+    def __init__(self, spec: ModelSpec, device="cuda", tokenizer=None, allow_hash_tokenizer: bool = False):
         self.spec = spec
         self.device = torch.device(device)
         t = spec.text
-        self.tokenizer = HashTokenizer(t.vocab, t.bos_id, t.eos_id, t.pad_id, t.max_pos)
+        self.text_tokenizer = tokenizer
+        self.tokenizer = HashTokenizer(t.vocab, t.bos_id, t.eos_id, t.pad_id, t.max_pos) \
+            if tokenizer is None and allow_hash_tokenizer else None
 
     # ---- images
     def images_to_u8(self, images) -> List[torch.Tensor]:
@@ -119,10 +159,20 @@ class Processor:
 
     # ---- text
     def tokenize(self, texts: Sequence[Union[str, Sequence[int]]], truncation: bool = True) -> List[List[int]]:
+        """Unpadded id rows; strings go to the tokenizer (padding=False) or the explicit hash stand-in."""
         t = self.spec.text
+        strs = [x for x in texts if isinstance(x, str)]
+        delegated = iter(())
+        if strs and self.text_tokenizer is not None:
+            delegated = iter(_as_rows(_ids(self.text_tokenizer(
+                strs, padding=False, truncation=truncation, max_length=t.max_pos))))
+        elif strs and self.tokenizer is None:
+            raise no_string_tokenizer("Processor")
         rows = []
         for x in texts:
-            if isinstance(x, str):
+            if isinstance(x, str) and self.text_tokenizer is not None:
+                rows.append(next(delegated))
+            elif isinstance(x, str):
                 body = self.tokenizer.encode(x)
                 pre = [t.bos_id] if t.bos_id is not None else []
                 room = t.max_pos - len(pre) - 1
@@ -156,6 +206,14 @@ class Processor:
             raise ValueError("processor needs images= or text=")
         if isinstance(text, str):
             text = [text]
+        if self.text_tokenizer is not None and text and all(isinstance(x, str) for x in text):
+            # main.py:427: the checkpoint's tokenizer pads and masks the batch itself
+            enc = self.text_tokenizer(list(text), padding=padding, truncation=truncation,
+                                      max_length=self.spec.text.max_pos, return_tensors="pt")
+            ids = torch.as_tensor(_ids(enc), dtype=torch.int64)
+            m = _mask(enc)
+            mask = torch.ones_like(ids) if m is None else torch.as_tensor(m, dtype=torch.int64)
+            return BatchFeature(input_ids=ids, attention_mask=mask)
         return self.pad(self.tokenize(text, truncation=truncation))
 
 

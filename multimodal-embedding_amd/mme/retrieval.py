@@ -55,11 +55,12 @@ TIE_ROWS_BYTES = 1 << 30
 
 
 class Ranked:
-    """rank_rows' result: hit counters per k, the top-kmax table in torch.topk's order, and the rows
-    that were re-selected in that order (with their per-k index lists)."""
+    """rank_rows' result: hit counters per k, the top-kmax table in torch.topk's order, the rows
+    that were re-selected in that order (with their per-k index lists), and the fused pass's
+    top-(kmax+1) scores per row (descending)."""
 
-    def __init__(self, hits, idx, tie_rows, tie_idx):
-        self.hits, self.idx, self.tie_rows, self.tie_idx = hits, idx, tie_rows, tie_idx
+    def __init__(self, hits, idx, tie_rows, tie_idx, score=None):
+        self.hits, self.idx, self.tie_rows, self.tie_idx, self.score = hits, idx, tie_rows, tie_idx, score
 
 
 def rank_rows(q: torch.Tensor, d: torch.Tensor, tgt_count: int, ks: Sequence[int] = KS, row_offset: int = 0,
@@ -92,13 +93,15 @@ def rank_rows(q: torch.Tensor, d: torch.Tensor, tgt_count: int, ks: Sequence[int
             rows = tie[lo:lo + per]
             S = ops.sim_scores(q.index_select(0, rows), d)
             tstart = ((rows + row_offset) * tgt_count).to(torch.int32)
-            for j, k in enumerate(kk):
-                ik, _ = ops.topk_rows_torch(S, k)
-                ops.recall_hits(ik, tgt_count, [k], tgt_start=tstart, hits=hits[j:j + 1])
-                parts[k].append(ik)
+            sel = {}
+            for k in parts:  # one selection per distinct k (kk repeats k when nd < max(ks))
+                sel[k] = ops.topk_rows_torch(S, k)[0]
+                parts[k].append(sel[k])
+            for j, k in enumerate(kk):  # but a hit counter per requested k
+                ops.recall_hits(sel[k], tgt_count, [k], tgt_start=tstart, hits=hits[j:j + 1])
             idx.index_copy_(0, rows, parts[kmax][-1])  # torch.topk(row, kmax): the table's own order
         tie_idx = {k: torch.cat(v) for k, v in parts.items()}
-    return Ranked(hits, idx, tie, tie_idx)
+    return Ranked(hits, idx, tie, tie_idx, sc)
 
 
 def recall_counts(img: torch.Tensor, t2i_txt: torch.Tensor, all_txt: torch.Tensor, caps_per_image: int = 5,

@@ -65,6 +65,26 @@ def test_exact_ties_kernel_order_and_torch_order(cuda):
     assert ranked.hits.tolist() == R.hits(s, 3).sum(0).tolist()
 
 
+@pytest.mark.parametrize("nd", [3, 5, 7])
+def test_exact_ties_fewer_columns_than_k(cuda, nd):
+    """nd < 10 columns, every one an exact duplicate: k = min(k, nd) repeats (e.g. [1, 5, 5] at nd 5), so
+    rank_rows must keep ONE torch-order selection per distinct k (tie_idx[k] lines up with tie_rows)
+    while counting hits for every requested k; hits and order equal the oracle's torch.topk replay."""
+    from oracle import retrieval as R
+    g = torch.Generator().manual_seed(nd)
+    doc = torch.nn.functional.normalize(torch.randn(1, 64, generator=g), dim=-1).to(torch.bfloat16)
+    docs = doc.repeat(nd, 1)
+    q = torch.nn.functional.normalize(torch.randn(6, 64, generator=g), dim=-1).to(torch.bfloat16)
+    s = R.scores(q.float().numpy(), docs.float().numpy())
+    ranked = retrieval.rank_rows(q.cuda(), docs.cuda(), 1)
+    assert ranked.tie_rows.numel() == 6
+    for k in {min(x, nd) for x in (1, 5, 10)}:
+        assert ranked.tie_idx[k].shape == (ranked.tie_rows.numel(), k)
+    tidx, _ = R.topk(s, nd)
+    assert np.array_equal(ranked.idx.cpu().numpy(), tidx)
+    assert ranked.hits.tolist() == R.hits(s, 1).sum(0).tolist()
+
+
 def _device_hit_flags(ranked, tgt_count, n_cols, row_offset=0, ks=(1, 5, 10)):
     """[rows, len(ks)] bool from rank_rows' tables: rows without a tie from the torch-order top-10
     table, re-selected rows from their per-k selections."""

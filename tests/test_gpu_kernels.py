@@ -187,22 +187,19 @@ def _skip_pair(qkv, B, T, H, hd, sl, causal, ref, kind):
 def test_attention_skip_vs_unskipped(cuda, hd, kind, ref, B, T, H, causal, lens):
     """The production kernels that skip a tile's second 32-key block when it lies wholly past the keys
     (kind 65: attn_m32_kernel in 9-wave blocks, hd 80; kind 62: attn_hyb_kernel, hd 72; kind 83: kind 62
-    with the 2^8 rescale threshold, production for hd 72 since round 4) against the same kernels without
-    the skip (kinds 41 / 58 / 84). Round 4 found (tools/attn_skip_diff.py,
-    profiles/r04_v7_attn_skip_*.log): the skip itself is exact -- an MFMA with an all-zero operand leaves
-    its accumulator bit-identical (tools/mfma_zero_probe.hip) and the ping-pong kernel carrying the same
-    skip (dev kind 70) equals kind 58 on every output (test below) -- and the rare differences are a
-    deterministic, code-generation-dependent effect inside these kernels' compiled loops: printf
-    instrumentation of the UNSKIPPED kernel alone moves 3 outputs. Bound: at most 2 bf16 ulps of
-    max(|x|, 1/16) on fewer than 1e-5 of the outputs (measured: 0-18 of 0.1-3.7 M, max 2^-10)."""
+    with the 2^8 rescale threshold, production for hd 72 since round 4; kind 86: kind 65 with it) against
+    the same kernels without the skip (kinds 41 / 58 / 84 / 88): bit-identical on every output. An MFMA
+    with an all-zero operand leaves its accumulator unchanged (tools/mfma_zero_probe.hip), and since
+    round 5 attention.hip is built with -ffp-contract=off and states its FMAs explicitly (the exp2
+    argument fma(s, c, -m c)), so no kernel's arithmetic depends on where the compiler contracts a
+    multiply-add: round 4's rare 1-2 ulp differences between these pairs were exactly that
+    (profiles/r05_v1_skip_contract_{on,off}.log: 0 of every output differ with contraction off)."""
     g = torch.Generator(device="cuda").manual_seed(B * T + hd)
     qkv = rnd(B * T, 3 * H * hd, scale=1.5, gen=g)
     sl = None if lens is None else torch.tensor(lens, dtype=torch.int32, device="cuda")
-    nd, d, ulp = _skip_pair(qkv, B, T, H, hd, sl, causal, ref, kind)
+    nd, d, _ = _skip_pair(qkv, B, T, H, hd, sl, causal, ref, kind)
     first = (d > 0).nonzero()[:4].tolist()
-    print(f"kind {kind} vs {ref}: {nd} of {d.numel()} outputs differ, max {d.max().item():.3g}, first {first}")
-    assert nd <= 1e-5 * d.numel() + 1, f"kind {kind} differs from kind {ref} on {nd} outputs (first {first})"
-    assert bool((d <= 2 * ulp).all()), f"kind {kind} vs {ref}: a difference above 2 bf16 ulps of max(|x|, 1/16)"
+    assert nd == 0, f"kind {kind} differs from kind {ref} on {nd} outputs (max {d.max().item():.3g}, first {first})"
 
 
 @pytest.mark.dev
@@ -446,6 +443,29 @@ def test_gemm_lnfold(cuda, M, N, K, act):
     e_fold = (out.float() - ref).abs().mean().item()
     e_unf = (unf - ref).abs().mean().item()
     assert e_fold <= 1.5 * e_unf + 1e-4, (e_fold, e_unf)
+
+
+@pytest.mark.parametrize("M,N,K,act", [(303993, 4352, 1152, 1), (70001, 4352, 1152, 2), (5000, 5120, 1280, 2),
+                                       (300, 4096, 1024, 1), (129, 8192, 256, 2)])
+def test_gemm_dispatched_fc1_bit_identical_to_pipe6(cuda, M, N, K, act):
+    """The production fc1 dispatch (LayerNorm fold + gelu_tanh / quick_gelu on the persistent GEMM, grid
+    from the device's CU count) against form 47 (pipe6, in the production library): the kernels share
+    K order, MFMAs and epilogue arithmetic, so every output is bit-identical -- SigLIP's execution batch
+    (417 images), ragged M, fewer tiles than CUs and many per CU."""
+    g = torch.Generator(device="cuda").manual_seed(M + N + K)
+    x = rnd(M, K, gen=g)
+    w = rnd(N, K, scale=K ** -0.5, gen=g)
+    b = rnd(N, scale=0.1, gen=g)
+    gam = (1 + 0.1 * torch.randn(K, device="cuda", generator=g)).to(torch.bfloat16)
+    bet = rnd(K, scale=0.1, gen=g)
+    f = ops.LNFolded(w, b, gam, bet)
+    st = ops.rowstats(x, 1e-6, d=K)
+    prod = (ops.gemm_lnfold(x, f, st, act=act), ops.gemm(x, w, b, act=act))
+    with ops.kernel_forms(gemm=47):
+        ref = (ops.gemm_lnfold(x, f, st, act=act), ops.gemm(x, w, b, act=act))
+    torch.cuda.synchronize()
+    for p_, r_ in zip(prod, ref):
+        assert torch.equal(p_, r_), f"dispatched fc1 differs from pipe6 ({M}x{N}x{K}, act {act})"
 
 
 # mme_gemm_res_stats: the residual GEMM's output is bit-identical to mme_gemm's, and the

@@ -31,8 +31,12 @@ def main():
         out[k] = {"dispatches": len(v), "mean": sum(v.values()) / max(len(v), 1)}
     m = {k: v["mean"] for k, v in out.items() if isinstance(v, dict)}
     if "GRBM_GUI_ACTIVE" in m and "SQ_VALU_MFMA_BUSY_CYCLES" in m:
-        # MFMA-busy per SIMD: the counter sums over the chip's 1 024 SIMDs
-        out["mfma_busy_frac"] = m["SQ_VALU_MFMA_BUSY_CYCLES"] / (1024 * m["GRBM_GUI_ACTIVE"])
+        # MFMA-busy per SIMD: SQ_VALU_MFMA_BUSY_CYCLES sums over the chip's 1 024 SIMDs, GRBM_GUI_ACTIVE
+        # over its 8 XCDs (one XCD's active cycles = GRBM_GUI_ACTIVE / 8; MI355X_MICROARCH.md, DVFS
+        # give-back), so the busy fraction is MFMA cycles / (1 024 x GRBM_GUI_ACTIVE / 8) -- the same
+        # normalisation as tools/pmc_gemm_util.sh (round 4 divided by 1 024 x GRBM_GUI_ACTIVE: 8x low)
+        out["mfma_busy_frac"] = m["SQ_VALU_MFMA_BUSY_CYCLES"] / (1024 * m["GRBM_GUI_ACTIVE"] / 8)
+        out["xcd_active_cycles"] = m["GRBM_GUI_ACTIVE"] / 8
     print(json.dumps(out, indent=1))
 
 
