@@ -57,6 +57,62 @@ __device__ __forceinline__ float wave_max(float v) {
     return v;
 }
 
+// ---------------------------------------------------------------------------
+// LayerNorm rows held by HALF a wave (round 5): lane hl = lane & 31 of half h = lane >> 5 owns the 16-B
+// chunks hl + 32 c of its row, c < LNH_MAXC (d <= 2 048). At the encoder widths this fills the lanes
+// where a whole wave per row left a third of them idle on the last chunk (d = 1 280: 160 chunks = 5 per
+// lane, against 64 + 64 + 32 over a 64-lane wave; d = 1 152: 4.5 against 3 x 64 for 144). The bf16
+// LayerNorm (norm.hip layernorm_kernel) and the LayerNorm -> mx8 kernel (mx.hip layernorm_mx_kernel)
+// share these helpers, so their statistics are the same bits (tests/test_gpu_mx.py).
+// ---------------------------------------------------------------------------
+constexpr int LNH_MAXC = 8;  // d <= 2 048; the kernels instantiate the smallest count that holds their d
+
+__device__ __forceinline__ float half_sum(float v) {
+#pragma unroll
+    for (int o = 16; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+
+template <int MAXC>
+__device__ __forceinline__ void ln_load_half(const bf16* __restrict__ xr, int nch, int hl, float (&v)[MAXC][8]) {
+#pragma unroll
+    for (int c = 0; c < MAXC; ++c) {
+        const int ch = hl + 32 * c;
+        if (ch < nch) {
+            const u16x8 u = *reinterpret_cast<const u16x8*>(xr + ch * 8);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) v[c][e] = bits2f(u[e]);
+        } else {
+#pragma unroll
+            for (int e = 0; e < 8; ++e) v[c][e] = 0.f;
+        }
+    }
+}
+
+// fp32 mean and rsqrt(biased variance + eps), two passes over the registers (nn.LayerNorm)
+template <int MAXC>
+__device__ __forceinline__ void ln_stats_half(const float (&v)[MAXC][8], int nch, int hl, int d, float eps,
+                                              float& mean, float& rstd) {
+    float s = 0.f;
+#pragma unroll
+    for (int c = 0; c < MAXC; ++c)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) s += v[c][e];
+    mean = half_sum(s) / d;
+    float s2 = 0.f;
+#pragma unroll
+    for (int c = 0; c < MAXC; ++c) {
+        if (hl + 32 * c < nch) {
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+                const float t = v[c][e] - mean;
+                s2 += t * t;
+            }
+        }
+    }
+    rstd = rsqrtf(half_sum(s2) / d + eps);
+}
+
 // async global -> LDS copy of 16 bytes per lane; LDS destination is the
 // wave-uniform `lds_base` + lane*16 (gfx950 global_load_lds_dwordx4).
 __device__ __forceinline__ void glds16(const void* gsrc, void* lds_base) {
@@ -72,6 +128,32 @@ __device__ __forceinline__ void wait_vmcnt0() { asm volatile("s_waitcnt vmcnt(0)
 __device__ __forceinline__ void glds16_asm(const void* gsrc, void* lds_base) {
     const unsigned m0 = __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)(LDS_AS char*)lds_base);
     asm volatile("s_mov_b32 m0, %1\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(gsrc), "s"(m0) : "memory", "m0");
+}
+
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ f32x2 pk_fma(f32x2 a, f32x2 b, f32x2 c) { return __builtin_elementwise_fma(a, b, c); }
+
+// gelu(x) = x Phi(x) (nn.GELU(approximate="none"), the ViT-H / LAION-CLIP-H MLP) through the complementary
+// error function, Phi(x) = erfc(-x / sqrt2) / 2, so neither tail loses digits to the cancellation of
+// 1 + erf(x / sqrt2). erfc(z), z = |x| / sqrt2 >= 0, by the Chebyshev fit of Numerical Recipes' erfcc
+// (fractional error < 1.2e-7 for every z): t = 1 / (1 + z / 2), erfc(z) = t exp(-z^2 + P(t)), nine FMAs
+// + one v_rcp_f32 + one v_exp_f32 and no branch, where libm's erff is a branchy piecewise evaluation
+// (~30 VALU per element: gemm_pipe9 with gelu_erf held 5 600 FMAs, 1 100 cndmasks and 824 branches
+// against 480 / 76 / 248 with gelu_tanh). Max relative error 2.9e-6 on [-12, 12] against float64 erfc
+// (the fp32 erf form 0.5 x (1 + erf) reaches 6.7e-2 in the negative tail); tests/test_host_logic.py.
+#define MME_ERFC_P(t)                                                                                                  \
+    pk_fma(t, pk_fma(t, pk_fma(t, pk_fma(t, pk_fma(t, pk_fma(t, pk_fma(t, pk_fma(t, pk_fma(t, f32x2{0.17087277f, 0.17087277f},     \
+    f32x2{-0.82215223f, -0.82215223f}), f32x2{1.48851587f, 1.48851587f}), f32x2{-1.13520398f, -1.13520398f}),               \
+    f32x2{0.27886807f, 0.27886807f}), f32x2{-0.18628806f, -0.18628806f}), f32x2{0.09678418f, 0.09678418f}),                 \
+    f32x2{0.37409196f, 0.37409196f}), f32x2{1.00002368f, 1.00002368f}), f32x2{-1.26551223f, -1.26551223f})
+
+__device__ __forceinline__ f32x2 gelu_erf2(f32x2 x) {
+    const f32x2 z = f32x2{__builtin_fabsf(x.x), __builtin_fabsf(x.y)} * 0.70710678118654752f;
+    const f32x2 d = pk_fma(z, f32x2{0.5f, 0.5f}, f32x2{1.0f, 1.0f});
+    const f32x2 t = f32x2{__builtin_amdgcn_rcpf(d.x), __builtin_amdgcn_rcpf(d.y)};
+    const f32x2 a = pk_fma(-z, z, MME_ERFC_P(t)) * 1.4426950408889634f;
+    const f32x2 h = (t * 0.5f) * f32x2{__builtin_amdgcn_exp2f(a.x), __builtin_amdgcn_exp2f(a.y)};  // Phi(-|x|)
+    return x * f32x2{x.x >= 0.f ? 1.0f - h.x : h.x, x.y >= 0.f ? 1.0f - h.y : h.y};
 }
 
 // Activation codes shared by the GEMM epilogue and the host (mme.h MME_ACT_*).
@@ -93,7 +175,7 @@ __device__ __forceinline__ float apply_act(float x, int act) {
             return x * __builtin_amdgcn_rcpf(1.0f + e);
         }
         case MME_ACT_GELU_ERF:
-            return 0.5f * x * (1.0f + erff(x * 0.7071067811865476f));
+            return gelu_erf2(f32x2{x, x}).x;
         default:
             return x;
     }
@@ -105,8 +187,6 @@ __device__ __forceinline__ float apply_act(float x, int act) {
 // (one multiply fewer than the scalar form; fp32 rounding differs by ~1 ulp,
 // far below the bf16 output). Used by the GEMM epilogue, where these VALU
 // cycles are pure overhead on the MFMA pipe (fc1: ~25 % of its epilogue time).
-typedef float f32x2 __attribute__((ext_vector_type(2)));
-__device__ __forceinline__ f32x2 pk_fma(f32x2 a, f32x2 b, f32x2 c) { return __builtin_elementwise_fma(a, b, c); }
 __device__ __forceinline__ f32x2 apply_act2(f32x2 x, int act) {
     switch (act) {
         case MME_ACT_GELU_TANH: {
@@ -121,7 +201,7 @@ __device__ __forceinline__ f32x2 apply_act2(f32x2 x, int act) {
             return x * f32x2{__builtin_amdgcn_rcpf(d.x), __builtin_amdgcn_rcpf(d.y)};
         }
         case MME_ACT_GELU_ERF:
-            return f32x2{apply_act(x.x, act), apply_act(x.y, act)};
+            return gelu_erf2(x);
         default:
             return x;
     }

@@ -2631,10 +2631,12 @@ int gemm_dispatch(GemmArgs a, int variant, hipStream_t s) {
         // non-split grid, bit-identical to pipe9 (test_gemm_pipe10_bit_identical_to_pipe9): fc1 (LN fold
         // + gelu_tanh) 1 118 -> 1 135 TF/s, quick_gelu / bias + gelu fc1 +1.0 % (profiles/r04_v10_pipe10_ab.log);
         // the split grid stays on pipe9 (its 512 x 128 tiles inlined into pipe10's loop spill), and so do
-        // the epilogues pipe10 was not measured with or spills in (gelu_erf: 22 VGPRs)
+        // the epilogues pipe10 was not measured with; round 5: gelu_erf on pipe10 too (the branch-free
+        // erfc form of common.h took it from 22 spilled VGPRs to pipe10's usual 2)
         if (pipe8_ok(a)) {
             if (N % 256 == 128) return launch_pipe9<Pipe256, 4, true>(a, s);
-            if (a.act == MME_ACT_GELU_TANH || a.act == MME_ACT_QUICK_GELU) return launch_pipe10<Pipe256, 4, false>(a, s);
+            if (a.act == MME_ACT_GELU_TANH || a.act == MME_ACT_QUICK_GELU || a.act == MME_ACT_GELU_ERF)
+                return launch_pipe10<Pipe256, 4, false>(a, s);
             return launch_pipe9<Pipe256, 4, false>(a, s);
         }
         if (N % 256 == 128) return launch_pipe6<Pipe256, 4, 1, 0, true>(a, s);

@@ -445,8 +445,41 @@ def test_gemm_lnfold(cuda, M, N, K, act):
     assert e_fold <= 1.5 * e_unf + 1e-4, (e_fold, e_unf)
 
 
+@pytest.mark.parametrize("act", [1, 2, 3])
+@pytest.mark.parametrize("M,N", [(4096, 4352), (2048, 1152)])
+def test_gemm_activation_vs_float64(cuda, M, N, act):
+    """The epilogue activations on exactly representable pre-activations: A[m, 0] = x_m (bf16), B[n, 0] = 1,
+    everything else 0, so acc = x_m exactly and the output is bf16(act(x_m)) (every column the same). Against
+    the float64 formula rounded to bf16: gelu_tanh / quick_gelu on v_exp_f32 + v_rcp_f32, gelu_erf
+    (nn.GELU's exact form, LAION-CLIP-H) through the branch-free erfc fit of common.h (round 5; libm erff
+    before): >= 99.5 % bit-identical, the rest one bf16 ulp, over x in [-10, 10] and the tails."""
+    K = 64
+    x = torch.cat([torch.linspace(-10, 10, M - 64, device="cuda"), torch.logspace(-6, 1.2, 64, device="cuda")])
+    xb = x.to(torch.bfloat16)
+    A = torch.zeros(M, K, device="cuda", dtype=torch.bfloat16)
+    A[:, 0] = xb
+    B = torch.zeros(N, K, device="cuda", dtype=torch.bfloat16)
+    B[:, 0] = 1
+    out = ops.gemm(A, B, None, act=act)
+    xd = xb.double()
+    if act == 1:  # 0.5 x (1 + tanh u) = x sigmoid(2 u): the form without cancellation in the negative tail
+        ref = xd * torch.sigmoid(2 * math.sqrt(2 / math.pi) * (xd + 0.044715 * xd ** 3))
+    elif act == 2:
+        ref = xd * torch.sigmoid(1.702 * xd)
+    else:
+        ref = 0.5 * xd * torch.special.erfc(-xd / math.sqrt(2))
+    rb = ref.float().to(torch.bfloat16)
+    got = out[:, 0]
+    assert torch.equal(out, got[:, None].expand(-1, N)), "columns differ"
+    same = (got == rb).float().mean().item()
+    ulp = (rb.float().abs().clamp_min(2.0 ** -126) * 2.0 ** -7)
+    err = (got.float() - rb.float()).abs()
+    print(f"act {act}: {same:.5f} bit-identical to the float64 formula, max err / ulp {(err / ulp).max().item():.2f}")
+    assert same >= 0.995 and bool((err <= ulp * 1.01).all())
+
+
 @pytest.mark.parametrize("M,N,K,act", [(303993, 4352, 1152, 1), (70001, 4352, 1152, 2), (5000, 5120, 1280, 2),
-                                       (300, 4096, 1024, 1), (129, 8192, 256, 2)])
+                                       (300, 4096, 1024, 1), (129, 8192, 256, 2), (116935, 5120, 1280, 3)])
 def test_gemm_dispatched_fc1_bit_identical_to_pipe6(cuda, M, N, K, act):
     """The production fc1 dispatch (LayerNorm fold + gelu_tanh / quick_gelu on the persistent GEMM, grid
     from the device's CU count) against form 47 (pipe6, in the production library): the kernels share

@@ -331,3 +331,26 @@ def test_compare_topk_oracle_only_exact_ties():
     assert near_old.all()                   # without device scores: the round-4 rule
     _, near_flagged = R.compare_topk(dev_idx, ref_idx, ref_sc, exact_rows=np.ones(2, bool), dev_score=dev_sc)
     assert not near_flagged.any()           # rows the device flagged replay torch's order: never exempt
+
+
+def test_gelu_erfc_fit_accuracy():
+    """The branch-free gelu_erf of csrc/common.h restated in float32 numpy (exact rcp / exp2 where the device
+    uses v_rcp_f32 / v_exp_f32, 1 ulp each): Numerical Recipes' erfcc Chebyshev fit, x Phi(x) with
+    Phi(x) = erfc(-x / sqrt2) / 2. Relative error against float64 below 5e-6 wherever |gelu| > 1e-6 and
+    absolute error below 5e-7 everywhere on [-12, 12]."""
+    from scipy.special import erfc
+    x = np.linspace(-12, 12, 400_001).astype(np.float32)
+    f = np.float32
+    z = (np.abs(x) * f(0.70710678118654752)).astype(np.float32)
+    t = (f(1) / (z * f(0.5) + f(1))).astype(np.float32)
+    p = f(0.17087277)
+    for c in (-0.82215223, 1.48851587, -1.13520398, 0.27886807, -0.18628806, 0.09678418, 0.37409196, 1.00002368,
+              -1.26551223):
+        p = (t * p + f(c)).astype(np.float32)
+    a = ((p - z * z) * f(1.4426950408889634)).astype(np.float32)
+    h = (t * f(0.5) * np.exp2(a)).astype(np.float32)
+    g = (x * np.where(x >= 0, f(1) - h, h)).astype(np.float32)
+    ref = x.astype(np.float64) * 0.5 * erfc(-x.astype(np.float64) / math.sqrt(2))
+    big = np.abs(ref) > 1e-6
+    assert (np.abs(g - ref)[big] / np.abs(ref)[big]).max() < 5e-6
+    assert np.abs(g - ref).max() < 5e-7
