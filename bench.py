@@ -74,6 +74,9 @@ def parse():
                    help="every rank on cuda:0 (rehearse N ranks on a one-GPU box; needs --backend gloo)")
     p.add_argument("--fp8", action="store_true",
                    help="mx8 encoder GEMMs (BASELINE configs[4]: DFN5B-H fp8 weights on the fp8 MFMA)")
+    p.add_argument("--gemm-form", type=int, default=None,
+                   help="A/B only: run every GEMM call with this libmme kernel form (mme.ops.kernel_forms; "
+                        "47 = pipe6, 95 = pipe10 on every non-split shape); reported on the line")
     return p.parse_args()
 
 
@@ -229,33 +232,21 @@ def retrieval_parity(tables, metrics, caps_per_image: int = 5):
 def fp8_drift(model_name, dev, imgs, t2i_ids, cap_ids, fp8_tables, img_batch, txt_batch, caps: int = 5):
     """fp8 against bf16 over the WHOLE job (checker; after the timed region, --fp8 only): the same
     weights (seed 0) loaded without the mx8 GEMMs encode the job's images and captions, and the
-    job's fp8 tables are compared with them: per-row cosine of the embeddings, and the I2T ranking
-    (every image against all 5n captions, mme_sim_topk) as top-1 agreement and top-10 overlap.
-    tests/test_gpu_mx.py asserts the same quantities (FP8_DRIFT) on a production batch."""
-    from mme import ops
+    job's fp8 tables are compared with them (mme.mx.job_drift: per-row cosine of the embeddings, the
+    I2T ranking -- every image against all 5n captions, mme_sim_topk -- as top-1 agreement and top-10
+    overlap, and `drift_ok` against mme.mx.JOB_DRIFT_BOUNDS, which tests/test_gpu_mx.py asserts on the
+    same job)."""
+    from mme import mx
     from mme.models import load_model
     t0 = time.time()
     bf, _ = load_model(model_name, seed=0, device=dev, fp8=False)
-    img = bf.encode_images(imgs, batch=img_batch)
-    t2i = bf.encode_texts(t2i_ids, exec_batch=txt_batch)
-    allc = bf.encode_texts(cap_ids, exec_batch=txt_batch)
+    bf_tables = {"img": bf.encode_images(imgs, batch=img_batch), "t2i": bf.encode_texts(t2i_ids, exec_batch=txt_batch),
+                 "all": bf.encode_texts(cap_ids, exec_batch=txt_batch)}
     del bf
-
-    def cos(a, b):
-        a, b = a.float(), b.float()
-        return (a * b).sum(1) / (a.norm(dim=1) * b.norm(dim=1)).clamp_min(1e-30)
-    ci, ct, ca = cos(fp8_tables["img"], img), cos(fp8_tables["t2i"], t2i), cos(fp8_tables["all"], allc)
-    i8, _ = ops.sim_topk(fp8_tables["img"], fp8_tables["all"], 10)
-    i16, _ = ops.sim_topk(img, allc, 10)
-    top1 = (i8[:, 0] == i16[:, 0]).float().mean().item()
-    ov = (i8[:, :, None] == i16[:, None, :]).any(2).float().mean().item()
+    d = mx.job_drift(fp8_tables, bf_tables)
     torch.cuda.synchronize()
-    return {"images": int(img.shape[0]), "captions": int(allc.shape[0]),
-            "cos_img_min": round(ci.min().item(), 5), "cos_img_mean": round(ci.mean().item(), 5),
-            "cos_txt_min": round(min(ct.min().item(), ca.min().item()), 5),
-            "cos_txt_mean": round(ca.mean().item(), 5),
-            "i2t_top1_agreement": round(top1, 4), "i2t_top10_overlap": round(ov, 4),
-            "checker": "the same weights in bf16 (mme, no mx8 GEMMs) over the whole job", "seconds": round(time.time() - t0, 2)}
+    d.update(checker="the same weights in bf16 (mme, no mx8 GEMMs) over the whole job", seconds=round(time.time() - t0, 2))
+    return d
 
 
 def encoder_parity(spec, imgs_u8, cap_ids, dev_img, dev_txt, bar: float = 0.999):
@@ -581,6 +572,11 @@ def main():
         # BEFORE anything touches the GPU (this parent never initialises HIP), and exit with
         # the first failing rank's status
         sys.exit(launch.spawn_ranks(args.gpus, [os.path.abspath(__file__)] + sys.argv[1:]))
+    if args.gemm_form is not None:  # thread-local form for this process's GEMM calls (no HIP call here)
+        import contextlib
+        from mme import ops as _ops
+        _forms = contextlib.ExitStack()
+        _forms.enter_context(_ops.kernel_forms(gemm=args.gemm_form))
     _, _, local = launch.env_rank_world()
     if args.same_device:
         local = 0
@@ -744,7 +740,8 @@ def main():
         "config": {"workload": f"{args.model}: {n} images x {caps * n} captions (+{n} T2I), encode + sim + top-10 "
                                f"recall", "n_images": n, "n_captions": caps * n, "image_in": "224x224x3 u8",
                    "image_size": spec.vision.image_size, "seq_len": spec.text.max_pos, "img_batch": args.img_batch,
-                   "txt_batch": args.txt_batch, "global_batch": n, "parallelism": f"image-shard x{world}"},
+                   "txt_batch": args.txt_batch, "global_batch": n, "parallelism": f"image-shard x{world}",
+                   **({"gemm_form": args.gemm_form} if args.gemm_form is not None else {})},
         "recall": {k: round(v, 2) for k, v in metrics.items()},
         # last timed step, device events, max over ranks; retrieval = all-gather (N > 1) + T2I / I2T /
         # I2T-Sym similarity + fused top-10 + recall counters + counter all-reduce

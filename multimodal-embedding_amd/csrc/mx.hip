@@ -94,58 +94,31 @@ __global__ __launch_bounds__(256) void mx_quant_kernel(const bf16* __restrict__ 
 
 // ---------------------------------------------------------------------------
 // LayerNorm -> mx8 (the QKV / fc1 operand straight from the norm): same
-// statistics as layernorm_kernel (norm.hip), the output rounded to bf16 (the
-// value the bf16 path would feed the GEMM) and then block-quantised.
-// One wave per row; lane chunks ch = lane + 64c, so 4 consecutive lanes hold
-// one 32-element block.
+// statistics as layernorm_kernel (norm.hip; the shared common.h ln_*_half helpers),
+// the output rounded to bf16 (the value the bf16 path would feed the GEMM) and then
+// block-quantised. One row per HALF wave (round 5: at d = 1 280 every lane holds 5
+// chunks, where a whole wave per row left a third of its lanes idle on the last one);
+// lane chunks ch = hl + 32 c, so 4 consecutive lanes hold one 32-element block.
 // ---------------------------------------------------------------------------
-constexpr int LN_MAXC = 4;
+template <int MAXC>
 __global__ __launch_bounds__(256) void layernorm_mx_kernel(const bf16* __restrict__ x, int ldx,
                                                            const bf16* __restrict__ g, const bf16* __restrict__ b,
                                                            int rows, int d, float eps, const int32_t* __restrict__ idx,
                                                            uint8_t* __restrict__ q, int ldq, uint8_t* __restrict__ sc,
                                                            int rows_pad) {
-    const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
-    const int lane = threadIdx.x & 63;
-    if (row >= rows) return;  // whole wave exits together
+    const int row = blockIdx.x * 8 + (threadIdx.x >> 5);
+    const int hl = threadIdx.x & 31;
+    if (row >= rows) return;  // the half wave's 32 lanes together
     const long src = idx ? idx[row] : row;
     const int nch = d >> 3;
-    const bf16* xr = x + src * ldx;
-    float v[LN_MAXC][8];
+    float v[MAXC][8];
+    ln_load_half(x + src * ldx, nch, hl, v);
+    float mean, rstd;
+    ln_stats_half(v, nch, hl, d, eps, mean, rstd);
 #pragma unroll
-    for (int c = 0; c < LN_MAXC; ++c) {
-        const int ch = lane + c * 64;
-        if (ch < nch) {
-            const u16x8 u = *reinterpret_cast<const u16x8*>(xr + ch * 8);
-#pragma unroll
-            for (int e = 0; e < 8; ++e) v[c][e] = bits2f(u[e]);
-        } else {
-#pragma unroll
-            for (int e = 0; e < 8; ++e) v[c][e] = 0.f;
-        }
-    }
-    float s = 0.f;
-#pragma unroll
-    for (int c = 0; c < LN_MAXC; ++c)
-#pragma unroll
-        for (int e = 0; e < 8; ++e) s += v[c][e];
-    const float mean = wave_sum(s) / d;
-    float s2 = 0.f;
-#pragma unroll
-    for (int c = 0; c < LN_MAXC; ++c) {
-        if (lane + c * 64 < nch) {
-#pragma unroll
-            for (int e = 0; e < 8; ++e) {
-                const float t = v[c][e] - mean;
-                s2 += t * t;
-            }
-        }
-    }
-    const float rstd = rsqrtf(wave_sum(s2) / d + eps);
-#pragma unroll
-    for (int c = 0; c < LN_MAXC; ++c) {
-        const int ch = lane + c * 64;
-        if (c * 64 >= nch) break;  // wave-uniform
+    for (int c = 0; c < MAXC; ++c) {
+        const int ch = hl + 32 * c;
+        if (c * 32 >= nch) break;  // uniform over the half wave
         float o[8];
         float a = 0.f;
         if (ch < nch) {
@@ -1222,13 +1195,20 @@ extern "C" int mme_layernorm_mx(const void* x, int ldx, const void* gamma, const
                                 float eps, const int32_t* rows_idx, void* q, int ldq, void* scales, int rows_pad,
                                 void* stream) {
     MME_REQUIRE(x && gamma && beta && q && scales, "mme_layernorm_mx: null pointer");
-    MME_REQUIRE(rows >= 0 && d > 0 && d % 32 == 0 && d <= 8 * 64 * LN_MAXC, "mme_layernorm_mx: d=%d unsupported", d);
+    MME_REQUIRE(rows >= 0 && d > 0 && d % 32 == 0 && d <= 8 * 32 * LNH_MAXC, "mme_layernorm_mx: d=%d unsupported", d);
     MME_REQUIRE(ldx % 8 == 0 && ldx >= d && ldq % 16 == 0 && ldq >= d, "mme_layernorm_mx: bad leading dims");
     MME_REQUIRE(rows_pad >= rows && rows_pad % 256 == 0, "mme_layernorm_mx: rows_pad must be >= rows, multiple of 256");
     if (rows == 0) return MME_OK;
-    hipLaunchKernelGGL(layernorm_mx_kernel, dim3(cdiv(rows, 4)), dim3(256), 0, as_stream(stream), (const bf16*)x, ldx,
-                       (const bf16*)gamma, (const bf16*)beta, rows, d, eps, rows_idx, (uint8_t*)q, ldq,
-                       (uint8_t*)scales, rows_pad);
+    const int mc = (d / 8 + 31) / 32;  // chunks per lane of a half-wave row
+#define MME_LN_MX(MC)                                                                                                  \
+    hipLaunchKernelGGL(layernorm_mx_kernel<MC>, dim3(cdiv(rows, 8)), dim3(256), 0, as_stream(stream), (const bf16*)x,   \
+                       ldx, (const bf16*)gamma, (const bf16*)beta, rows, d, eps, rows_idx, (uint8_t*)q, ldq,            \
+                       (uint8_t*)scales, rows_pad)
+    if (mc <= 3) MME_LN_MX(3);
+    else if (mc <= 4) MME_LN_MX(4);
+    else if (mc <= 5) MME_LN_MX(5);
+    else MME_LN_MX(LNH_MAXC);
+#undef MME_LN_MX
     return mme_check_launch("mme_layernorm_mx");
 }
 

@@ -25,39 +25,26 @@ __device__ __forceinline__ void load_row(const bf16* xr, int nch, int lane, floa
 
 // nn.LayerNorm on a bf16 row (TF:models/siglip/modeling_siglip.py:329-331):
 // fp32 mean / biased variance, y = (x - mean) * rsqrt(var + eps) * gamma + beta.
+// Round 5: one row per HALF wave (common.h ln_*_half), 8 rows per 256-thread block.
+constexpr int LN_ROWS_PER_BLOCK = 8;
+template <int MAXC>
 __global__ __launch_bounds__(256) void layernorm_kernel(const bf16* __restrict__ x, int ldx,
                                                         const bf16* __restrict__ g, const bf16* __restrict__ b,
                                                         bf16* __restrict__ y, int ldy, int rows, int d, float eps,
                                                         const int32_t* __restrict__ idx) {
-    const int row = blockIdx.x * ROWS_PER_BLOCK + (threadIdx.x >> 6);
-    const int lane = threadIdx.x & 63;
-    if (row >= rows) return;
+    const int row = blockIdx.x * LN_ROWS_PER_BLOCK + (threadIdx.x >> 5);
+    const int hl = threadIdx.x & 31;
+    if (row >= rows) return;  // the half wave's 32 lanes together (its shuffles stay inside the half)
     const long src = idx ? idx[row] : row;
     const int nch = d >> 3;
     float v[MAXC][8];
-    load_row(x + src * ldx, nch, lane, v);
-    float s = 0.f;
-#pragma unroll
-    for (int c = 0; c < MAXC; ++c)
-#pragma unroll
-        for (int e = 0; e < 8; ++e) s += v[c][e];
-    const float mean = wave_sum(s) / d;
-    float s2 = 0.f;
-#pragma unroll
-    for (int c = 0; c < MAXC; ++c) {
-        if (lane + c * 64 < nch) {
-#pragma unroll
-            for (int e = 0; e < 8; ++e) {
-                const float t = v[c][e] - mean;
-                s2 += t * t;
-            }
-        }
-    }
-    const float rstd = rsqrtf(wave_sum(s2) / d + eps);
+    ln_load_half(x + src * ldx, nch, hl, v);
+    float mean, rstd;
+    ln_stats_half(v, nch, hl, d, eps, mean, rstd);
     bf16* yr = y + (long)row * ldy;
 #pragma unroll
     for (int c = 0; c < MAXC; ++c) {
-        const int ch = lane + c * 64;
+        const int ch = hl + 32 * c;
         if (ch < nch) {
             const u16x8 gu = *reinterpret_cast<const u16x8*>(g + ch * 8);
             const u16x8 bu = *reinterpret_cast<const u16x8*>(b + ch * 8);
@@ -147,9 +134,20 @@ extern "C" int mme_layernorm(const void* x, int ldx, const void* gamma, const vo
     MME_REQUIRE(rows >= 0 && d > 0 && d % 8 == 0 && d <= 8 * 64 * MAXC, "mme_layernorm: d=%d unsupported", d);
     MME_REQUIRE(ldx % 8 == 0 && ldy % 8 == 0 && ldx >= d && ldy >= d, "mme_layernorm: bad leading dims");
     if (rows == 0) return MME_OK;
-    hipLaunchKernelGGL(layernorm_kernel, dim3(cdiv(rows, ROWS_PER_BLOCK)), dim3(256), 0, as_stream(stream),
-                       (const bf16*)x, ldx, (const bf16*)gamma, (const bf16*)beta, (bf16*)y, ldy, rows, d, eps,
-                       rows_idx);
+    const int nch = d / 8, mc = (nch + 31) / 32;  // chunks per lane of a half-wave row
+    const dim3 grid(cdiv(rows, LN_ROWS_PER_BLOCK)), block(256);
+    if (mc <= 3)
+        hipLaunchKernelGGL(layernorm_kernel<3>, grid, block, 0, as_stream(stream), (const bf16*)x, ldx, (const bf16*)gamma,
+                           (const bf16*)beta, (bf16*)y, ldy, rows, d, eps, rows_idx);
+    else if (mc <= 4)
+        hipLaunchKernelGGL(layernorm_kernel<4>, grid, block, 0, as_stream(stream), (const bf16*)x, ldx, (const bf16*)gamma,
+                           (const bf16*)beta, (bf16*)y, ldy, rows, d, eps, rows_idx);
+    else if (mc <= 5)
+        hipLaunchKernelGGL(layernorm_kernel<5>, grid, block, 0, as_stream(stream), (const bf16*)x, ldx, (const bf16*)gamma,
+                           (const bf16*)beta, (bf16*)y, ldy, rows, d, eps, rows_idx);
+    else
+        hipLaunchKernelGGL(layernorm_kernel<LNH_MAXC>, grid, block, 0, as_stream(stream), (const bf16*)x, ldx,
+                           (const bf16*)gamma, (const bf16*)beta, (bf16*)y, ldy, rows, d, eps, rows_idx);
     return mme_check_launch("mme_layernorm");
 }
 

@@ -262,3 +262,30 @@ def test_gemm_mx_wave_epilogue_bit_identical(cuda, M, N, K, kind):
     for o in outs[1:]:
         for p, q in zip(outs[0], o):
             assert torch.equal(p, q), f"mx GEMM form differs from the round-2 kernel ({kind}, {M}x{N}x{K})"
+
+
+@pytest.mark.slow
+def test_fp8_dfn5b_whole_job_drift():
+    """BASELINE configs[4] at its whole-job size: DFN5B-H, 5 000 synthetic images x 25 000 captions (+ the
+    5 000 T2I captions), exactly bench.py --model Apple-DFN5B-H --fp8's inputs, execution batches and
+    weights, encoded with the mx8 encoder GEMMs and in bf16. The job-level drift (mme.mx.job_drift: per-row
+    cosine, I2T top-1 agreement and top-10 overlap over all 5 000 x 25 000) must stay within
+    mme.mx.JOB_DRIFT_BOUNDS, the bounds the bench line's `drift_ok` reports against."""
+    import bench
+    from mme import get_spec
+    from mme.config import exec_batches
+    from mme.harness import encode_job
+    from mme.models import load_model
+    spec = get_spec("Apple-DFN5B-H")
+    imgs, ids = bench.synth_inputs(spec, 5000, 5, "cuda")
+    eb_img, eb_txt = exec_batches(spec)
+    tables = {}
+    for fp8 in (True, False):
+        model, _ = load_model("Apple-DFN5B-H", seed=0, device="cuda", fp8=fp8)
+        img, t2i, allc = encode_job(model, imgs, ids, None, 5, eb_img, eb_txt)
+        tables[fp8] = {"img": img, "t2i": t2i, "all": allc}
+        del model
+    d = mx.job_drift(tables[True], tables[False])
+    print(f"fp8 vs bf16 over the whole job: {d}")
+    assert d["drift_ok"], f"fp8 whole-job drift out of bounds: {d}"
+
