@@ -2988,6 +2988,233 @@ __global__ __launch_bounds__(256) void probe_attn_img_kernel(const bf16* __restr
     }
 }
 
+// ---------------------------------------------------------------------------
+// attn_m32p_kernel (round 5, kind 94): attn_m32_kernel's 9-wave, one-block-per-(image, head) form
+// (kind 86: SKIP + 2^8 rescale threshold; ViT-H / LAION-CLIP-H, T = 257) as a PERSISTENT loop. Kind 86
+// runs only 5 key tiles per block and, at 130 VGPRs (3 waves per SIMD), one 9-wave block fills a CU,
+// so every block's Q load and first K / V DMA (~2-4 us of a ~17 us block) are exposed.
+// Here one block per CU walks (image, head) units with ONE continuous K / V ring across unit
+// boundaries: while the last tile of unit u runs, the next unit's tile 0 is DMA'd into the other ring
+// slot and its Q fragments are loaded into a second register set, so the next unit starts on landed
+// data. Units are dealt to the XCDs in contiguous ranges (the XCD's 32 blocks work on 2 images' 32
+// heads at a time: their rows share L2 lines). Per-tile arithmetic, K order and MFMA chains are kind 86's
+// (the ring slot is a runtime offset instead of an unrolled immediate), so the outputs are bit-identical
+// to kind 86 (tests/test_gpu_kernels.py::test_attention_persistent_vith_bit_identical).
+// Non-causal attention with T <= 32 NW (one query block per unit).
+// ---------------------------------------------------------------------------
+template <int HD, int NW>
+__global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(1))) void attn_m32p_kernel(AttnArgs a,
+                                                                                                   int nunits) {
+    constexpr int NSTG = 2;
+    constexpr bool ONES = HD % 32 != 0;
+    constexpr int NCHL = HD / 8;
+    constexpr int NKS = (HD + 15) / 16;
+    constexpr int NDB = (HD + (ONES ? 1 : 0) + 31) / 32;
+    constexpr int NVP = 4 * NDB;
+    constexpr int TILE = (NCHL + NVP) * 1024;
+    constexpr int NINS = 2 * NCHL;
+    constexpr int MAXI = (NINS + NW - 1) / NW;
+    static_assert(2 * NKS <= NCHL + NVP, "K reads past the head dim stay inside the tile");
+    __shared__ __attribute__((aligned(16))) char lds[NSTG * TILE];
+
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int r = lane & 31, hh = lane >> 5;
+    const int T = a.T, D = a.H * HD;
+    const float c = a.scale_log2;
+    const int qw0 = wave * 32;
+
+    // this block's units: XCD x = blockIdx % 8 owns a contiguous range, its blocks interleave in it
+    int u, uend, ustep;
+    {
+        const int x = blockIdx.x & 7, l = blockIdx.x >> 3, gx = gridDim.x >> 3;
+        const int q8 = nunits >> 3, r8 = nunits & 7;
+        const int start = x < r8 ? x * (q8 + 1) : r8 * (q8 + 1) + (x - r8) * q8;
+        u = start + l;
+        uend = start + q8 + (x < r8 ? 1 : 0);
+        ustep = gx;
+    }
+    if (u >= uend) return;  // whole block
+
+    // V planes past the data: the ones plane (ONES) and zero padding, in both ring slots (once)
+    constexpr int NPAD = NVP > NCHL ? NVP - NCHL : 1;
+    for (int i = tid; i < NSTG * (NVP - NCHL) * 64; i += NW * 64) {
+        const int slot = i / (NPAD * 64), rem = i % (NPAD * 64);
+        const int pl = NCHL + rem / 64;
+        const unsigned short v = (ONES && pl == NCHL) ? 0x3F80 : 0;
+        *reinterpret_cast<u16x8*>(lds + slot * TILE + (NCHL + pl) * 1024 + (rem & 63) * 16) =
+            u16x8{v, v, v, v, v, v, v, v};
+    }
+
+    auto unit_base = [&](int uu) -> const bf16* { return a.qkv + (long)(uu / a.H) * T * a.ld; };
+    auto load_q = [&](int uu, bf16x8 (&qd)[NKS]) __attribute__((always_inline)) {
+        const bf16* qrow = unit_base(uu) + (long)min(qw0 + r, T - 1) * a.ld + (uu % a.H) * HD;
+#pragma unroll
+        for (int ks = 0; ks < NKS; ++ks) {
+            const int col = ks * 16 + 8 * hh;
+            qd[ks] = col < HD ? *reinterpret_cast<const bf16x8*>(qrow + col) : bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
+        }
+    };
+    // tile t of unit uu into ring slot `slot`
+    auto issue = [&](int uu, int t, int slot) __attribute__((always_inline)) {
+        char* tb = lds + slot * TILE;
+        const bf16* base = unit_base(uu);
+        const int h = uu % a.H;
+#pragma unroll
+        for (int i = 0; i < MAXI; ++i) {
+            const int idx = wave + NW * i;
+            if (i < MAXI - 1 || idx < NINS) {
+                const bool isV = idx >= NCHL;
+                const int plane = isV ? idx - NCHL : idx;
+                const int key = isV ? lane ^ (4 * (plane & 3)) : lane;
+                const bf16* src = base + (long)min(t * 64 + key, T - 1) * a.ld + (isV ? 2 : 1) * D + h * HD + plane * 8;
+                glds16(src, tb + idx * 1024);
+            }
+        }
+    };
+
+    const unsigned lds0 = (unsigned)(uintptr_t)(LDS_AS char*)lds;
+    const unsigned kb0 = lds0 + hh * 1024 + r * 16;
+    unsigned vbj[2];
+    {
+        const int i16 = lane & 15, q = i16 >> 2, p = i16 & 3, half = (lane >> 4) & 1;
+        const int cc = 2 * half + (p >> 1);
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+            vbj[j] = lds0 + (NCHL + cc) * 1024 + (((8 * j + 4 * hh + q) ^ (4 * cc)) * 16) + (p & 1) * 8;
+    }
+
+    bf16x8 qf[NKS], qn[NKS];
+    f32x16 o[NDB];
+    float m = -1e30f;
+    int Tk = 0;
+
+    // kind 86's tile arithmetic (attn_m32_kernel with SKIP and THR), ring slot at a runtime offset
+    auto tile = [&](int t, const unsigned so) __attribute__((always_inline)) {
+        const bool half = t * 64 + 32 >= Tk;
+        f32x16 sc[2];
+#pragma unroll
+        for (int kb = 0; kb < 2; ++kb) {
+            f32x16 z;
+#pragma unroll
+            for (int e = 0; e < 16; ++e) z[e] = kb == 1 && half ? -INFINITY : 0.f;
+            if (kb == 1 && half) {
+                sc[kb] = z;
+                continue;
+            }
+#pragma unroll
+            for (int ks = 0; ks < NKS; ++ks) {
+                const bf16x8 kf = *reinterpret_cast<const LDS_AS bf16x8*>((uintptr_t)(kb0 + so + kb * 512 + ks * 2048));
+                z = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[ks], z, 0, 0, 0);
+            }
+            sc[kb] = z;
+        }
+        if (t * 64 + 64 > Tk) {
+#pragma unroll
+            for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+                for (int e = 0; e < 16; ++e)
+                    if (t * 64 + kb * 32 + (e & 3) + 8 * (e >> 2) + 4 * hh >= Tk) sc[kb][e] = -INFINITY;
+        }
+        float mloc = fmaxf(sc[0][0], sc[0][1]);
+#pragma unroll
+        for (int e = 2; e < 16; ++e) mloc = fmaxf(mloc, sc[0][e]);
+#pragma unroll
+        for (int e = 0; e < 16; ++e) mloc = fmaxf(mloc, sc[1][e]);
+        mloc = xmax32(mloc);
+        const float mnew = fmaxf(m, mloc);
+        if (__builtin_amdgcn_ballot_w64((mloc - m) * c > 8.0f)) {
+            const float alpha = __builtin_amdgcn_exp2f((m - mnew) * c);
+#pragma unroll
+            for (int i = 0; i < NDB; ++i) o[i] *= alpha;
+            m = mnew;
+        }
+        const float mc = m * c;
+#pragma unroll
+        for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+            for (int e = 0; e < 16; ++e) sc[kb][e] = __builtin_amdgcn_exp2f(__builtin_fmaf(sc[kb][e], c, -mc));
+        bf16x8 pk[4];
+#pragma unroll
+        for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+            for (int sp = 0; sp < 2; ++sp)
+#pragma unroll
+                for (int j = 0; j < 8; ++j) pk[2 * kb + sp][j] = f2bf(sc[kb][8 * sp + j]);
+#pragma unroll
+        for (int kb = 0; kb < 2; ++kb) {
+            if (kb == 1 && half) break;
+#pragma unroll
+            for (int sp = 0; sp < 2; ++sp)
+#pragma unroll
+                for (int db = 0; db < NDB; ++db) {
+                    const unsigned off = so + db * 4096 + kb * 512 + sp * 256;
+                    const s16x4 v0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS_AS s16x4*)(uintptr_t)(vbj[0] + off));
+                    const s16x4 v1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS_AS s16x4*)(uintptr_t)(vbj[1] + off));
+                    const bf16x8 vv = __builtin_bit_cast(bf16x8, __builtin_shufflevector(v0, v1, 0, 1, 2, 3, 4, 5, 6, 7));
+                    o[db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vv, pk[2 * kb + sp], o[db], 0, 0, 0);
+                }
+        }
+    };
+
+    if (wave >= NW / 2) __builtin_amdgcn_s_setprio(1);
+    load_q(u, qf);
+    issue(u, 0, 0);
+    int slot = 0;  // ring slot of the unit's current tile (continuous across units)
+    while (true) {
+        const int b = u / a.H, h = u % a.H;
+        Tk = a.seq_lens ? a.seq_lens[b] : T;
+        const int nkt = (Tk + 63) / 64;
+        const int un = u + ustep;
+        const bool more = un < uend;
+#pragma unroll
+        for (int i = 0; i < NDB; ++i)
+#pragma unroll
+            for (int e = 0; e < 16; ++e) o[i][e] = 0.f;
+        m = -1e30f;
+        for (int t = 0; t < nkt; ++t) {
+            vm_wait<0>();
+            __builtin_amdgcn_s_barrier();
+            if (t + 1 < nkt) {
+                issue(u, t + 1, slot ^ 1);
+            } else if (more) {  // the next unit's tile 0 and Q under this unit's last tile
+                issue(un, 0, slot ^ 1);
+                load_q(un, qn);
+            }
+            tile(t, slot ? TILE : 0);
+            slot ^= 1;
+        }
+        // normalise and store (attn_m32_kernel's epilogue)
+        {
+            constexpr int DB1 = HD / 32, REG1 = 4 * ((HD % 32) / 8);
+            static_assert(ONES, "the weight sums come from the ones plane");
+            const float inv = 1.0f / o[DB1][REG1];
+            const int q = qw0 + r;
+            bf16* orow = a.out + ((long)b * T + min(q, T - 1)) * a.ldo + h * HD;
+#pragma unroll
+            for (int db = 0; db < NDB; ++db)
+#pragma unroll
+                for (int mm = 0; mm < 4; mm += 2) {
+                    if (32 * db + 8 * mm >= HD) continue;
+                    bf16x4 v0, v1;
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) {
+                        v0[e] = f2bf(o[db][4 * mm + e] * inv);
+                        v1[e] = f2bf(o[db][4 * mm + 4 + e] * inv);
+                    }
+                    const uint2 x = __builtin_bit_cast(uint2, v0), y = __builtin_bit_cast(uint2, v1);
+                    const auto sx = __builtin_amdgcn_permlane32_swap(x.x, y.x, false, false);
+                    const auto sy = __builtin_amdgcn_permlane32_swap(x.y, y.y, false, false);
+                    const int d0 = 32 * db + 8 * (mm + hh);
+                    if (q < T && d0 + 8 <= HD) *reinterpret_cast<uint4*>(orow + d0) = make_uint4(sx[0], sy[0], sx[1], sy[1]);
+                }
+        }
+        if (!more) break;
+        u = un;
+        for (int ks = 0; ks < NKS; ++ks) qf[ks] = qn[ks];
+    }
+}
+
 template <int HD>
 bool launch_attn_dev(int kind, const AttnArgs& a, int B, int T, int H, hipStream_t st);
 
@@ -3034,7 +3261,18 @@ bool launch_attn(int kind, const AttnArgs& a, int B, int T, int H, hipStream_t s
     } else if (kind == 86)  // kind 65 with the 2^8 rescale threshold: production for hd 80 in 9-wave blocks
         hipLaunchKernelGGL((attn_m32_kernel<HD, 9, 1, true, false, false, true, true>), dim3(cdiv(T, 288) * H * B),
                            dim3(576), 0, st, a);
-    else if (kind == 87)  // kind 38 with the threshold: production for hd 80 in 8-wave blocks (DFN5B T 730)
+    else if (kind == 94) {  // kind 86 as a persistent loop over (image, head) units (T <= 288, non-causal)
+        if constexpr (HD % 32 != 0) {
+            if (a.causal || T > 288) return false;  // one non-causal query block per unit
+            const int nunits = B * H;
+            int dev = 0, ncu = 256;
+            if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+            const int grid = max(8, min(ncu / 8 * 8, (nunits + 7) / 8 * 8));
+            hipLaunchKernelGGL((attn_m32p_kernel<HD, 9>), dim3(grid), dim3(576), 0, st, a, nunits);
+        } else {
+            return false;
+        }
+    } else if (kind == 87)  // kind 38 with the threshold: production for hd 80 in 8-wave blocks (DFN5B T 730)
         hipLaunchKernelGGL((attn_m32_kernel<HD, 8, 1, true, false, false, false, true>), dim3(cdiv(T, 256) * H * B),
                            dim3(512), 0, st, a);
     else if (kind == 88)  // kind 41 with the threshold: kind 86's no-skip identity reference
@@ -3358,9 +3596,12 @@ int attention_entry(int form, const void* qkv, int ld_qkv, void* out, int ld_out
     // The same threshold in attn_m32_kernel (hd 80: kinds 86 / 87 = 65 / 38, ViT-H +3 %, DFN5B +4.5 %) and
     // attn_fwd_kernel (kind 89 = kind 0: CLIP-L vision +3 %, CLIP causal text +1 %;
     // profiles/r04_v20_attn_threshold_hd80_hd64_ab.log).
+    // Round 5: kind 94 = kind 86 as a persistent walk over (image, head) units, the next unit's Q and
+    // first K / V tile loaded under the current unit's last tile: ViT-H (T 257) at the 512-image batch
+    // 0.528 -> 0.491 ms (327 -> 352 TF/s), bit-identical (profiles/r05_v6_attn.log).
     int kind = T <= 64 ? 16
                : (T <= 128 || hd == 64) ? 89
-               : (hd == 80 && pad9 * 10 < min(pad8, pad4) * 9) ? 86
+               : (hd == 80 && pad9 * 10 < min(pad8, pad4) * 9) ? (T <= 288 && !causal ? 94 : 86)
                : hd == 80 && pad8 * 10 <= pad4 * 11 ? 87
                : pad9 * 10 < min(pad8, pad4) * 9 ? 35
                : (hd == 80 && pad12 <= pad8 && pad12 * 10 <= pad4 * 11) ? 23

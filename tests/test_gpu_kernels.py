@@ -129,7 +129,7 @@ def test_attention(cuda, B, T, H, hd, causal, lens):
     torch.testing.assert_close(out.float(), ref, atol=2e-2, rtol=2e-2)
 
 
-PROD_ATTN_KINDS = (38, 41, 58, 62, 65, 83, 84, 86, 87, 88, 89)  # in the production library; the rest are development forms (libmme_dev.so)
+PROD_ATTN_KINDS = (38, 41, 58, 62, 65, 83, 84, 86, 87, 88, 89, 94)  # in the production library; the rest are development forms (libmme_dev.so)
 
 
 @pytest.mark.parametrize("kind", [k if k in PROD_ATTN_KINDS else pytest.param(k, marks=pytest.mark.dev)
@@ -200,6 +200,29 @@ def test_attention_skip_vs_unskipped(cuda, hd, kind, ref, B, T, H, causal, lens)
     nd, d, _ = _skip_pair(qkv, B, T, H, hd, sl, causal, ref, kind)
     first = (d > 0).nonzero()[:4].tolist()
     assert nd == 0, f"kind {kind} differs from kind {ref} on {nd} outputs (max {d.max().item():.3g}, first {first})"
+
+
+@pytest.mark.parametrize("B,T,H,lens", [
+    (4, 257, 16, None),            # ViT-H/14-224
+    (37, 257, 16, None),           # 592 units: more than one block per CU, uneven XCD ranges
+    (512, 257, 16, None),          # the bench's execution batch: 8192 units, 32 per block
+    (3, 257, 5, [257, 100, 1]),    # key padding: each unit's own tile count and skip
+    (2, 200, 3, [200, 64]),
+    (1, 257, 1, None),             # one unit: 7 of 8 blocks exit at once
+    (2, 288, 2, None),             # a full 9-wave query block
+    (3, 65, 2, None),
+])
+def test_attention_persistent_vith_bit_identical(cuda, B, T, H, lens):
+    """Kind 94 (attn_m32p_kernel: kind 86's flash loop as a persistent walk over (image, head) units,
+    the next unit's first K / V tile and Q fragments loaded under the last tile of the current one)
+    against kind 86: bit-identical on every output, across unit counts below, near and far above the
+    CU count and per-image key lengths."""
+    g = torch.Generator(device="cuda").manual_seed(B * T + H)
+    qkv = rnd(B * T, 3 * H * 80, scale=1.5, gen=g)
+    sl = None if lens is None else torch.tensor(lens, dtype=torch.int32, device="cuda")
+    nd, d, _ = _skip_pair(qkv, B, T, H, 80, sl, False, 86, 94)
+    assert nd == 0, f"kind 94 differs from kind 86 on {nd} outputs (max {d.max().item():.3g}, " \
+                    f"first {(d > 0).nonzero()[:4].tolist()})"
 
 
 @pytest.mark.dev
@@ -499,6 +522,35 @@ def test_gemm_dispatched_fc1_bit_identical_to_pipe6(cuda, M, N, K, act):
     torch.cuda.synchronize()
     for p_, r_ in zip(prod, ref):
         assert torch.equal(p_, r_), f"dispatched fc1 differs from pipe6 ({M}x{N}x{K}, act {act})"
+
+
+@pytest.mark.parametrize("M,N,K", [(116935, 1280, 1280), (116935, 1280, 5120), (5000, 3840, 1280), (300, 1024, 1024)])
+def test_gemm_form95_bit_identical_to_pipe6(cuda, M, N, K):
+    """Form 95 (pipe10, the persistent GEMM, on every non-split epilogue: bias, residual + the next
+    LayerNorm's row statistics, LayerNorm fold) against form 47 (pipe6): bit-identical outputs and
+    statistics at ViT-H / CLIP shapes (whole 256-column tiles), ragged M, fewer tiles than CUs."""
+    g = torch.Generator(device="cuda").manual_seed(M + N + K)
+    x = rnd(M, K, gen=g)
+    w = rnd(N, K, scale=K ** -0.5, gen=g)
+    b = rnd(N, scale=0.1, gen=g)
+    res = rnd(M, N, gen=g)
+    gam = (1 + 0.1 * torch.randn(K, device="cuda", generator=g)).to(torch.bfloat16)
+    bet = rnd(K, scale=0.1, gen=g)
+    f = ops.LNFolded(w, b, gam, bet)
+    fold = K <= 2048  # the LayerNorm fold precedes the qkv / fc1 GEMMs (K = the model width)
+    st = ops.rowstats(x, 1e-6, d=K) if fold else None
+    outs = []
+    for form in (47, 95):
+        with ops.kernel_forms(gemm=form):
+            y = ops.gemm(x, w, b)
+            yl = ops.gemm_lnfold(x, f, st, act=0) if fold else y
+            sr = torch.empty(M, 2, device="cuda", dtype=torch.float32)
+            part = torch.empty(M * (N // 64) * 2, device="cuda", dtype=torch.float32)
+            yr = ops.gemm_res_stats(x, w, b, res, 1e-6, sr, part)
+            outs.append((y, yl, yr, sr))
+        torch.cuda.synchronize()
+    for a_, b_ in zip(outs[0], outs[1]):
+        assert torch.equal(a_, b_), f"form 95 differs from pipe6 ({M}x{N}x{K})"
 
 
 # mme_gemm_res_stats: the residual GEMM's output is bit-identical to mme_gemm's, and the

@@ -21,6 +21,7 @@ CASES = [  # name, B, T, H, hd, causal
     ("siglip_text_2500", 2500, 64, 16, 72, False),
     ("clipL_vision", 256, 577, 16, 64, False),
     ("vitH_vision", 256, 257, 16, 80, False),
+    ("vitH_256", 256, 256, 16, 80, False),  # ViT-H without the CLS row: whole 32-query waves
     ("dfn5b_vision", 128, 730, 16, 80, False),
     ("clip_text_causal", 1024, 77, 16, 64, True),
 ]
