@@ -3002,9 +3002,9 @@ __global__ __launch_bounds__(256) void probe_attn_img_kernel(const bf16* __restr
 // to kind 86 (tests/test_gpu_kernels.py::test_attention_persistent_vith_bit_identical).
 // Non-causal attention with T <= 32 NW (one query block per unit).
 // ---------------------------------------------------------------------------
-template <int HD, int NW>
-__global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(1))) void attn_m32p_kernel(AttnArgs a,
-                                                                                                   int nunits) {
+template <int HD, int NW, int MINW = 1>
+__global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(MINW))) void attn_m32p_kernel(AttnArgs a,
+                                                                                                      int nunits) {
     constexpr int NSTG = 2;
     constexpr bool ONES = HD % 32 != 0;
     constexpr int NCHL = HD / 8;
@@ -3215,6 +3215,22 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(1))) vo
     }
 }
 
+// attn_m32p_kernel launch: `per_cu` persistent blocks per CU (grid a multiple of 8 for the XCD ranges)
+template <int HD, int NW, int MINW>
+bool launch_m32p(const AttnArgs& a, int B, int T, int H, int per_cu, hipStream_t st) {
+    if constexpr (HD % 32 != 0) {
+        if (a.causal || T > 32 * NW) return false;  // one non-causal query block per unit
+        const int nunits = B * H;
+        int dev = 0, ncu = 256;
+        if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+        const int grid = max(8, min(per_cu * (ncu / 8 * 8), (nunits + 7) / 8 * 8));
+        hipLaunchKernelGGL((attn_m32p_kernel<HD, NW, MINW>), dim3(grid), dim3(NW * 64), 0, st, a, nunits);
+        return true;
+    } else {
+        return false;
+    }
+}
+
 template <int HD>
 bool launch_attn_dev(int kind, const AttnArgs& a, int B, int T, int H, hipStream_t st);
 
@@ -3262,16 +3278,7 @@ bool launch_attn(int kind, const AttnArgs& a, int B, int T, int H, hipStream_t s
         hipLaunchKernelGGL((attn_m32_kernel<HD, 9, 1, true, false, false, true, true>), dim3(cdiv(T, 288) * H * B),
                            dim3(576), 0, st, a);
     else if (kind == 94) {  // kind 86 as a persistent loop over (image, head) units (T <= 288, non-causal)
-        if constexpr (HD % 32 != 0) {
-            if (a.causal || T > 288) return false;  // one non-causal query block per unit
-            const int nunits = B * H;
-            int dev = 0, ncu = 256;
-            if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
-            const int grid = max(8, min(ncu / 8 * 8, (nunits + 7) / 8 * 8));
-            hipLaunchKernelGGL((attn_m32p_kernel<HD, 9>), dim3(grid), dim3(576), 0, st, a, nunits);
-        } else {
-            return false;
-        }
+        if (!launch_m32p<HD, 9, 1>(a, B, T, H, 1, st)) return false;
     } else if (kind == 87)  // kind 38 with the threshold: production for hd 80 in 8-wave blocks (DFN5B T 730)
         hipLaunchKernelGGL((attn_m32_kernel<HD, 8, 1, true, false, false, false, true>), dim3(cdiv(T, 256) * H * B),
                            dim3(512), 0, st, a);
@@ -3304,7 +3311,11 @@ template <int HD>
 bool launch_attn_dev(int kind, const AttnArgs& a, int B, int T, int H, hipStream_t st) {
     if (kind == 19)  // dev: short kernel, compact K pitch (4 blocks per CU): no gain, HBM-bound (0.138 / 0.136 ms)
         hipLaunchKernelGGL((attn_short_kernel<HD, true>), dim3(cdiv(B * H, 2)), dim3(256), 0, st, a, B * H);
-    else if (kind == 66) {  // dev: short kernel as a persistent loop with the next pair's loads in flight
+    else if (kind == 95) {  // dev: kind 94 in 8-wave blocks (T <= 256), one per CU
+        if (!launch_m32p<HD, 8, 1>(a, B, T, H, 1, st)) return false;
+    } else if (kind == 96) {  // dev: kind 94 in 8-wave blocks held to 128 VGPRs, two per CU
+        if (!launch_m32p<HD, 8, 4>(a, B, T, H, 2, st)) return false;
+    } else if (kind == 66) {  // dev: short kernel as a persistent loop with the next pair's loads in flight
         const int npairs = cdiv(B * H, 2);
         hipLaunchKernelGGL((attn_short_pf_kernel<HD>), dim3(min(npairs, 256 * 2)), dim3(256), 0, st, a, B * H, npairs);
     }
