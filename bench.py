@@ -77,6 +77,9 @@ def parse():
     p.add_argument("--gemm-form", type=int, default=None,
                    help="A/B only: run every GEMM call with this libmme kernel form (mme.ops.kernel_forms; "
                         "47 = pipe6, 95 = pipe10 on every non-split shape); reported on the line")
+    p.add_argument("--attn-form", type=int, default=None,
+                   help="A/B only: run every attention call with this libmme kernel form (mme.ops.kernel_forms; "
+                        "30 + kind forces a kernel kind); reported on the line")
     return p.parse_args()
 
 
@@ -524,7 +527,7 @@ def main_colpali(args, rank, world, dev):
     if "gemm" in kt:
         gk = kt["gemm"]
         achieved = gk["flops"] / (gk["ms"] / 1e3) / 1e12
-        roofline = {"bound": "mfma", "kernel": "mme_gemm (gemm_pipe9_kernel; gemm_pipe10_kernel for gelu_tanh / quick_gelu fc1)", "achieved": round(achieved, 1),
+        roofline = {"bound": "mfma", "kernel": "mme_gemm (gemm_pipe9_kernel; gemm_pipe10_kernel for the non-split gelu_tanh / quick_gelu / gelu_erf fc1)", "achieved": round(achieved, 1),
                     "peak": MFMA_BF16_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": round(achieved / MFMA_BF16_PEAK_TFLOPS, 4),
                     "traffic": None, "launches": gk["launches"], "avg_launch_ms": round(gk["ms"] / gk["launches"], 4),
                     "algorithmic_bytes_per_launch": round(gk["bytes"] / gk["launches"]),
@@ -572,11 +575,12 @@ def main():
         # BEFORE anything touches the GPU (this parent never initialises HIP), and exit with
         # the first failing rank's status
         sys.exit(launch.spawn_ranks(args.gpus, [os.path.abspath(__file__)] + sys.argv[1:]))
-    if args.gemm_form is not None:  # thread-local form for this process's GEMM calls (no HIP call here)
+    if args.gemm_form is not None or args.attn_form is not None:  # thread-local forms (no HIP call here)
         import contextlib
         from mme import ops as _ops
         _forms = contextlib.ExitStack()
-        _forms.enter_context(_ops.kernel_forms(gemm=args.gemm_form))
+        _forms.enter_context(_ops.kernel_forms(**({"gemm": args.gemm_form} if args.gemm_form is not None else {}),
+                                               **({"attention": args.attn_form} if args.attn_form is not None else {})))
     _, _, local = launch.env_rank_world()
     if args.same_device:
         local = 0
@@ -694,7 +698,7 @@ def main():
         achieved = g["flops"] / (g["ms"] / 1e3) / 1e12
         peak = MFMA_FP8_PEAK_TFLOPS if args.fp8 else MFMA_BF16_PEAK_TFLOPS
         roofline = {"bound": "mfma",
-                    "kernel": "mme_gemm_mx (gemm_mx11_kernel)" if args.fp8 else "mme_gemm (gemm_pipe9_kernel; gemm_pipe10_kernel for gelu_tanh / quick_gelu fc1)",
+                    "kernel": "mme_gemm_mx (gemm_mx11_kernel)" if args.fp8 else "mme_gemm (gemm_pipe9_kernel; gemm_pipe10_kernel for the non-split gelu_tanh / quick_gelu / gelu_erf fc1)",
                     "achieved": round(achieved, 1), "peak": peak, "unit": "TFLOP/s", "frac": round(achieved / peak, 4),
                     "traffic": None, "launches": g["launches"], "avg_launch_ms": round(avg_ms, 4),
                     "algorithmic_bytes_per_launch": round(g["bytes"] / g["launches"]),
@@ -741,7 +745,8 @@ def main():
                                f"recall", "n_images": n, "n_captions": caps * n, "image_in": "224x224x3 u8",
                    "image_size": spec.vision.image_size, "seq_len": spec.text.max_pos, "img_batch": args.img_batch,
                    "txt_batch": args.txt_batch, "global_batch": n, "parallelism": f"image-shard x{world}",
-                   **({"gemm_form": args.gemm_form} if args.gemm_form is not None else {})},
+                   **({"gemm_form": args.gemm_form} if args.gemm_form is not None else {}),
+                   **({"attn_form": args.attn_form} if args.attn_form is not None else {})},
         "recall": {k: round(v, 2) for k, v in metrics.items()},
         # last timed step, device events, max over ranks; retrieval = all-gather (N > 1) + T2I / I2T /
         # I2T-Sym similarity + fused top-10 + recall counters + counter all-reduce

@@ -150,8 +150,8 @@ int mme_attention(const void* qkv, int ld_qkv, void* out, int ld_out, int B, int
  *   mme_gemm_form / mme_gemm_lnfold_form / mme_gemm_res_stats_form: -1 = production,
  *     47 = pipe6 (the bit-identity reference of pipe8 / pipe9), 48 = the per-row statistics
  *     combine (res_stats); other forms exist in the development build (libmme_dev.so) only;
- *   mme_attention_form: 0 = production, 30 + kind = kernel kind `kind` (round 4 production:
- *     83 hd 72, 86 / 87 hd 80, 89 hd 64 -- the rescale-threshold forms of 62 / 65 / 38 / 0);
+ *   mme_attention_form: 0 = production, 30 + kind = kernel kind `kind` (production: 83 hd 72,
+ *     86 / 87 hd 80, 89 hd 64; 94 = the persistent form of 86, measured and not dispatched);
  *   mme_gemm_mx_form (below): -1 = production (mx11 where its geometry holds, else mx10),
  *     10 = mx10, 0 / 2 / 3 = earlier forms. */
 int mme_gemm_form(int form, const void* A, int lda, const void* B, int ldb, void* C, int ldc, int M, int N, int K,

@@ -3001,6 +3001,11 @@ __global__ __launch_bounds__(256) void probe_attn_img_kernel(const bf16* __restr
 // (the ring slot is a runtime offset instead of an unrolled immediate), so the outputs are bit-identical
 // to kind 86 (tests/test_gpu_kernels.py::test_attention_persistent_vith_bit_identical).
 // Non-causal attention with T <= 32 NW (one query block per unit).
+// Measured (round 5): ViT-H in isolation 7 % faster than kind 86 at 455 / 512 images, but 3 % slower
+// inside the LAION-CLIP-H job (kernel stats 480 vs 466 us per launch, the jobs level): not dispatched.
+// The 9-wave block's bound is its waves' 3 + 2 + 2 + 2 split over the SIMDs (at T = 256 the 8-wave
+// kernel at 4 waves per SIMD runs 0.34-0.375 ms against 0.42-0.44 for 9-wave blocks), and the 8-wave
+// form of this loop (dev kind 95: 179 VGPRs, 2 waves per SIMD) is slower still (0.47 ms at T = 256).
 // ---------------------------------------------------------------------------
 template <int HD, int NW, int MINW = 1>
 __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(MINW))) void attn_m32p_kernel(AttnArgs a,
@@ -3277,7 +3282,8 @@ bool launch_attn(int kind, const AttnArgs& a, int B, int T, int H, hipStream_t s
     } else if (kind == 86)  // kind 65 with the 2^8 rescale threshold: production for hd 80 in 9-wave blocks
         hipLaunchKernelGGL((attn_m32_kernel<HD, 9, 1, true, false, false, true, true>), dim3(cdiv(T, 288) * H * B),
                            dim3(576), 0, st, a);
-    else if (kind == 94) {  // kind 86 as a persistent loop over (image, head) units (T <= 288, non-causal)
+    else if (kind == 94) {  // kind 86 as a persistent loop over (image, head) units (T <= 288, non-causal; measured,
+                            // not dispatched: faster alone, slower in the job -- see the dispatch comment)
         if (!launch_m32p<HD, 9, 1>(a, B, T, H, 1, st)) return false;
     } else if (kind == 87)  // kind 38 with the threshold: production for hd 80 in 8-wave blocks (DFN5B T 730)
         hipLaunchKernelGGL((attn_m32_kernel<HD, 8, 1, true, false, false, false, true>), dim3(cdiv(T, 256) * H * B),
@@ -3608,11 +3614,13 @@ int attention_entry(int form, const void* qkv, int ld_qkv, void* out, int ld_out
     // attn_fwd_kernel (kind 89 = kind 0: CLIP-L vision +3 %, CLIP causal text +1 %;
     // profiles/r04_v20_attn_threshold_hd80_hd64_ab.log).
     // Round 5: kind 94 = kind 86 as a persistent walk over (image, head) units, the next unit's Q and
-    // first K / V tile loaded under the current unit's last tile: ViT-H (T 257) at the 512-image batch
-    // 0.528 -> 0.491 ms (327 -> 352 TF/s), bit-identical (profiles/r05_v6_attn.log).
+    // first K / V tile loaded under the current unit's last tile: bit-identical, 7 % faster in isolation
+    // (ViT-H at 455 / 512 images: 0.48 / 0.53 -> 0.45 / 0.49 ms, profiles/r05_v10_attn_vith_batches.log)
+    // but 3 % slower inside the LAION-CLIP-H job (466 vs 480 us per launch, jobs level;
+    // profiles/r05_v9_*): not dispatched.
     int kind = T <= 64 ? 16
                : (T <= 128 || hd == 64) ? 89
-               : (hd == 80 && pad9 * 10 < min(pad8, pad4) * 9) ? (T <= 288 && !causal ? 94 : 86)
+               : (hd == 80 && pad9 * 10 < min(pad8, pad4) * 9) ? 86
                : hd == 80 && pad8 * 10 <= pad4 * 11 ? 87
                : pad9 * 10 < min(pad8, pad4) * 9 ? 35
                : (hd == 80 && pad12 <= pad8 && pad12 * 10 <= pad4 * 11) ? 23
