@@ -89,7 +89,10 @@ def encoder_layer(x: torch.Tensor, L: LayerW, cfg: TowerConfig, B: int, T: int, 
         a, x = _pooled(a, x, rows)
         n = x.shape[0]
         mlp_flops = 2.0 * n * d * cfg.intermediate
-        ops.gemm(a, L.o_w, L.o_b, residual=x, out=x)
+        if L.mx.o is not None:  # MME_FP8_OPROJ=1 drift experiment: o_proj on mx8 too
+            mx.gemm(mx.quantize(a, out=bufs.hq), L.mx.o, L.o_b, residual=x, out=x)
+        else:
+            ops.gemm(a, L.o_w, L.o_b, residual=x, out=x)
         hq = mx.layernorm(x, L.ln2_g, L.ln2_b, cfg.eps, out=bufs.hq)
         midq = mx.gemm(hq, L.mx.fc1, L.fc1_b, act=act, out_mx=bufs.midq, algo_flops=mlp_flops)
         mx.gemm(midq, L.mx.fc2, L.fc2_b, residual=x, out=x, algo_flops=mlp_flops)

@@ -120,14 +120,18 @@ def gemm(a: MXTensor, w: MXTensor, bias: Optional[torch.Tensor] = None, *, resid
 
 @dataclass
 class LayerMX:
-    """mx8 copies of one encoder layer's fp8 weights (quantised once at load)."""
+    """mx8 copies of one encoder layer's fp8 weights (quantised once at load). `o` (the attention
+    output projection) only under MME_FP8_OPROJ=1: the drift experiment of round 5 (its input is
+    quantised by a separate mme_mx_quant pass), not the production fp8 mode."""
     qkv: MXTensor
     fc1: MXTensor
     fc2: MXTensor
+    o: Optional[MXTensor] = None
 
 
 def quantize_layer(L) -> LayerMX:
-    return LayerMX(quantize(L.qkv_w), quantize(L.fc1_w), quantize(L.fc2_w))
+    o = quantize(L.o_w) if os.environ.get("MME_FP8_OPROJ") == "1" else None
+    return LayerMX(quantize(L.qkv_w), quantize(L.fc1_w), quantize(L.fc2_w), o)
 
 
 # Whole-job fp8 drift bounds (BASELINE configs[4], DFN5B-H at 5 000 images x 25 000 captions): the same
