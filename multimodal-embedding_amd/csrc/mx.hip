@@ -206,14 +206,25 @@ __device__ __forceinline__ i32x4v mx_rsrc(const void* base, unsigned bytes) {
     r[3] = 0x00020000;
     return r;
 }
+// PAD (mx12): five wait states open the statement -- an "s" operand may come straight from a v_readlane
+// (an SGPR spill reload: a VALU write of an SGPR that a VMEM instruction then reads needs 5 wait states,
+// which hipcc does not insert for an inline-asm consumer)
+template <bool PAD = false>
 __device__ __forceinline__ void mx_dma4(unsigned m0base, const unsigned (&voff)[4], i32x4v rsrc, unsigned soff) {
-    asm volatile(
-        "s_mov_b32 m0, %0\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %5, %6 offen lds\n\t"
-        "s_add_u32 m0, m0, 0x400\n\ts_nop 0\n\tbuffer_load_dwordx4 %2, %5, %6 offen lds\n\t"
-        "s_add_u32 m0, m0, 0x400\n\ts_nop 0\n\tbuffer_load_dwordx4 %3, %5, %6 offen lds\n\t"
-        "s_add_u32 m0, m0, 0x400\n\ts_nop 0\n\tbuffer_load_dwordx4 %4, %5, %6 offen lds"
-        ::"s"(m0base), "v"(voff[0]), "v"(voff[1]), "v"(voff[2]), "v"(voff[3]), "s"(rsrc), "s"(soff)
-        : "memory", "m0", "scc");  // s_add_u32 writes SCC
+#define MX_DMA4_BODY                                                                                          \
+    "s_mov_b32 m0, %0\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %5, %6 offen lds\n\t"                          \
+    "s_add_u32 m0, m0, 0x400\n\ts_nop 0\n\tbuffer_load_dwordx4 %2, %5, %6 offen lds\n\t"                   \
+    "s_add_u32 m0, m0, 0x400\n\ts_nop 0\n\tbuffer_load_dwordx4 %3, %5, %6 offen lds\n\t"                   \
+    "s_add_u32 m0, m0, 0x400\n\ts_nop 0\n\tbuffer_load_dwordx4 %4, %5, %6 offen lds"
+    if constexpr (PAD)
+        asm volatile("s_nop 4\n\t" MX_DMA4_BODY::"s"(m0base), "v"(voff[0]), "v"(voff[1]), "v"(voff[2]), "v"(voff[3]),
+                     "s"(rsrc), "s"(soff)
+                     : "memory", "m0", "scc");  // s_add_u32 writes SCC
+    else
+        asm volatile(MX_DMA4_BODY::"s"(m0base), "v"(voff[0]), "v"(voff[1]), "v"(voff[2]), "v"(voff[3]), "s"(rsrc),
+                     "s"(soff)
+                     : "memory", "m0", "scc");  // s_add_u32 writes SCC
+#undef MX_DMA4_BODY
 }
 __device__ __forceinline__ void mx_dma1(unsigned m0base, unsigned voff, i32x4v rsrc, unsigned soff) {
     asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, %3 offen lds"
@@ -232,15 +243,22 @@ __device__ __forceinline__ void mx_dma1(unsigned m0base, unsigned voff, i32x4v r
 constexpr int MXW_PITCH = 144, MXW_LDS = 8 * 128 * MXW_PITCH;
 // SB (mx11): a scheduling barrier after each staged column quad keeps the unrolled staging loop
 // from interleaving (and holding live) all 32 quads' activations at once.
-template <int ACT, bool SWZ = true, bool SB = false>
+// PASSES (mx12, round 5): the sub-tile staged and stored in PASSES row bands through a region of
+// 128 / PASSES rows per wave (2: 8 KiB per wave, two of the five ring units), as pipe10's epilogue.
+template <int ACT, bool SWZ = true, bool SB = false, int PASSES = 1>
 __device__ __forceinline__ void mx_epilogue_wave(const MxArgs& p, char* lds, f32x16 (&acc)[4][2], int m0, int n0,
                                                  int wave, int lane) {
-    constexpr int TM = 128, TN = 64, MX9_PITCH = SWZ ? 128 : MXW_PITCH;
+    static_assert(PASSES == 1 || (PASSES == 2 && SWZ), "one or two staging passes");
+    constexpr int TM = 128, TN = 64, MX9_PITCH = SWZ ? 128 : MXW_PITCH, BAND = TM / PASSES;
     const int wm = wave / 4, wn = wave % 4;
     const int h = lane >> 5, r32 = lane & 31;
     // lane (r32, h) holds row i*32 + r32, columns j*32 + 8q + 4h + (0..3)
-    char* reg = lds + wave * (128 * MX9_PITCH);
+    char* reg = lds + wave * (BAND * MX9_PITCH);
     const int rm0 = m0 + wm * TM, cn0 = n0 + wn * TN;
+    const int rr = lane >> 3, cc = lane & 7;
+#pragma unroll
+    for (int ps = 0; ps < PASSES; ++ps) {
+    if (ps > 0) lgkm_wait<0>();  // the previous band's read-back done before its region is rewritten
 #pragma unroll
     for (int j = 0; j < 2; ++j)
 #pragma unroll
@@ -252,32 +270,34 @@ __device__ __forceinline__ void mx_epilogue_wave(const MxArgs& p, char* lds, f32
                 for (int r = 0; r < 4; ++r) bv[r] = bf2f(p.bias[min(cn0 + nl + r, p.N - 1)]);
             }
 #pragma unroll
-            for (int i = 0; i < 4; ++i) {
+            for (int i = ps * (4 / PASSES); i < (ps + 1) * (4 / PASSES); ++i) {
                 bf16x4 o;
 #pragma unroll
                 for (int r = 0; r < 4; ++r) o[r] = f2bf(apply_act(acc[i][j][4 * qd + r] + bv[r], ACT));
+                const int lrow = i * 32 + r32 - ps * BAND;
                 if constexpr (SWZ)  // chunk 4 j + qd ^ (row & 7), half h ^ (row >> 3 & 1); row & 31 = r32
-                    *reinterpret_cast<bf16x4*>(reg + (i * 32 + r32) * MX9_PITCH + (((4 * j + qd) ^ (r32 & 7)) << 4) +
+                    *reinterpret_cast<bf16x4*>(reg + lrow * MX9_PITCH + (((4 * j + qd) ^ (r32 & 7)) << 4) +
                                                ((h ^ ((r32 >> 3) & 1)) << 3)) = o;
                 else
-                    *reinterpret_cast<bf16x4*>(reg + (i * 32 + r32) * MX9_PITCH + nl * 2) = o;
+                    *reinterpret_cast<bf16x4*>(reg + lrow * MX9_PITCH + nl * 2) = o;
             }
             if (SB) __builtin_amdgcn_sched_barrier(0);
         }
     // the wave's own LDS writes precede its reads
-    const int rr = lane >> 3, cc = lane & 7;
     auto rd = [&](int q, int row) __attribute__((always_inline)) -> u16x8 {
+        const int lrow = row - ps * BAND;
         if constexpr (SWZ) {  // row & 7 = rr, bit 3 of the row = q & 1
-            const u16x8 w = *reinterpret_cast<const u16x8*>(reg + row * MX9_PITCH + ((cc ^ rr) << 4));
+            const u16x8 w = *reinterpret_cast<const u16x8*>(reg + lrow * MX9_PITCH + ((cc ^ rr) << 4));
             return (q & 1) ? u16x8{w[4], w[5], w[6], w[7], w[0], w[1], w[2], w[3]} : w;
         } else {
-            return *reinterpret_cast<const u16x8*>(reg + row * MX9_PITCH + cc * 16);
+            return *reinterpret_cast<const u16x8*>(reg + lrow * MX9_PITCH + cc * 16);
         }
     };
+    constexpr int QN = 16 / PASSES;
     if (!p.out_mx) {
         bf16* Cout = reinterpret_cast<bf16*>(p.C);
 #pragma unroll 4
-        for (int q = 0; q < 16; ++q) {
+        for (int q = ps * QN; q < (ps + 1) * QN; ++q) {
             const int row = q * 8 + rr, gr = rm0 + row, gc = cn0 + cc * 8;
             const u16x8 v = rd(q, row);
             if (gr >= p.M || gc >= p.N) continue;
@@ -296,7 +316,7 @@ __device__ __forceinline__ void mx_epilogue_wave(const MxArgs& p, char* lds, f32
         // mx8 output: lanes cc = 0..3 / 4..7 of a row hold its two 32-column blocks
         uint8_t* Cq = reinterpret_cast<uint8_t*>(p.C);
 #pragma unroll 4
-        for (int q = 0; q < 16; ++q) {  // same trip count for every lane (shuffles)
+        for (int q = ps * QN; q < (ps + 1) * QN; ++q) {  // same trip count for every lane (shuffles)
             const int row = q * 8 + rr, gr = rm0 + row, gc = cn0 + cc * 8;
             const u16x8 v = rd(q, row);
             float f[8];
@@ -313,6 +333,7 @@ __device__ __forceinline__ void mx_epilogue_wave(const MxArgs& p, char* lds, f32
             }
         }
     }
+    }  // passes
 }
 
 // WEPI (round 3): the per-wave epilogue above instead of the whole-tile LDS epilogue below; the
@@ -724,9 +745,13 @@ int launch_mx10(const MxArgs& a, hipStream_t s) {
 // scale op_sel picks the byte (A: i; B: j after a 16-bit shift for odd wn).
 // Needs K % 128 == 0, K >= 384 (three stages) and operands < 4 GiB (32-bit offsets).
 // ---------------------------------------------------------------------------
+template <bool PAD = false>
 __device__ __forceinline__ unsigned mx_sload(unsigned voff, i32x4v rsrc, unsigned soff) {
     unsigned v;
-    asm volatile("buffer_load_dword %0, %1, %2, %3 offen" : "=v"(v) : "v"(voff), "s"(rsrc), "s"(soff) : "memory");
+    if (PAD)  // mx_dma4's PAD: the nops inside the statement, so nothing is scheduled between them and the load
+        asm volatile("s_nop 4\n\tbuffer_load_dword %0, %1, %2, %3 offen" : "=v"(v) : "v"(voff), "s"(rsrc), "s"(soff) : "memory");
+    else
+        asm volatile("buffer_load_dword %0, %1, %2, %3 offen" : "=v"(v) : "v"(voff), "s"(rsrc), "s"(soff) : "memory");
     return v;
 }
 // counted vmcnt that also marks the scale registers loaded by inline asm as written here, so no
@@ -954,6 +979,274 @@ int launch_mx11(const MxArgs& a, hipStream_t s) {
     return mme_check_launch("mme_gemm_mx");
 }
 
+
+// ---------------------------------------------------------------------------
+// mx12 (round 5): persistent mx11, as pipe10 is persistent pipe9 (gemm.hip). One workgroup per CU
+// walks mx11's tile order (xcd_remap of the same ids: every tile on the XCD it would run on as an
+// mx11 block) with mx11's main loop, K order, MFMAs and epilogue arithmetic per tile (bit-identical
+// outputs). At the seam between tiles the next tile's first three ring units (A0 B0 A1) are DMA'd
+// as soon as this tile's last fragment reads are done, i.e. under its epilogue, which stages through
+// slots 3-4 only (two 64-row passes); after it every wave waits for its own loads, one barrier frees
+// slots 3-4, and the next tile's scales and units B1 A2 follow.
+// Measured (round 5, profiles/r05_v12_mx12_gemm.log, r05_v12_fp8_*): bit-identical to mx11 but slower on
+// every DFN5B-H shape with the job's epilogues (QKV 1.45 -> 1.49, fc1 2.30 -> 2.35-2.40, fc2 1.74 ->
+// 1.78-1.81 ms; the fp8 job 1 172-1 174 -> 1 160-1 162 img/s): the persistent loop holds 255 VGPRs and
+// spills 25-40 SGPRs, whose reloads feed the asm loads (next paragraph), so the seam it hides costs more
+// than it saves. Not dispatched (form 12; form 14 = no DMA under the epilogue).
+// Hazard found building it: the SGPR-spill reloads are v_readlane writes of the SGPRs that the inline-asm
+// buffer loads read as soffset; the hardware needs 5 wait states between the two, hipcc pads only
+// instructions it generates, and unpadded the scale loads read stale offsets -- the early wave row's
+// outputs came out wrong on some tiles of some launches (profiles/r05_v15_*, r05_v16_*). mx12's asm loads
+// open with s_nop 4 (PAD); tools/asm_hazard_audit.py checks every kernel of the library for the pattern
+// (tests/test_abi.py::test_no_unpadded_sgpr_vmem_hazards; 12 of 12 runs identical after the fix,
+// profiles/r05_v17_mx12_hazard_fixed_debug.log).
+// ---------------------------------------------------------------------------
+// SEAM (dev A/B): 0 = as described; 2 = no DMA under the epilogue (every tile's A0 B0 A1 at its prologue).
+template <int GROUP_M, int ACT, bool LATE, int SEAM = 0>
+__device__ __forceinline__ void mx12_run(const MxArgs& p, char* lds, const int wave) {
+    constexpr int UNIT = 32768;
+    const int lane = threadIdx.x & 63;
+    const int wm = wave / 4, wn = wave % 4;
+    const int h = lane >> 5, r32 = lane & 31;
+    const int nbm = (p.M + 255) / 256, nbn = (p.N + 255) / 256, ntiles = nbm * nbn;
+
+    const i32x4v rA = mx_rsrc(p.A, (unsigned)((size_t)p.M * p.lda));
+    const i32x4v rB = mx_rsrc(p.B, (unsigned)((size_t)p.N * p.ldb));
+    const i32x4v rSA = mx_rsrc(p.sa, (unsigned)((size_t)(p.K / 32) * p.sa_rows));
+    const i32x4v rSB = mx_rsrc(p.sb, (unsigned)((size_t)(p.K / 32) * p.sb_rows));
+    const unsigned sstepA = 4u * p.sa_rows, sstepB = 4u * p.sb_rows, bshift = (wn & 1) * 16;
+    const unsigned s2A = 2u * p.sa_rows, s2B = 2u * p.sb_rows;
+    const unsigned lds0 = (unsigned)(uintptr_t)(LDS_AS char*)lds;
+    const unsigned lw = __builtin_amdgcn_readfirstlane(lds0 + wave * 4096);
+    const int sw = (r32 >> 1) & 7;
+    const unsigned a_x = lds0 + (wm * 128 + r32) * 128 + ((h ^ sw) << 4);
+    const unsigned b_x = lds0 + (wn * 64 + r32) * 128 + ((h ^ sw) << 4);
+    const int nk = p.K / 128;
+
+    unsigned offA[4], offB[4], vsa = 0, vsb = 0;
+    auto set_off = [&](int m0, int n0) __attribute__((always_inline)) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int prow = (wave * 4 + q) * 8 + (lane >> 3);
+            const int logical = swz(prow, lane & 7);
+            offA[q] = (unsigned)min(m0 + prow, p.M - 1) * (unsigned)p.lda + logical * 16;
+            offB[q] = (unsigned)min(n0 + prow, p.N - 1) * (unsigned)p.ldb + logical * 16;
+        }
+        vsa = (unsigned)(h * p.sa_rows + m0 + wm * 128 + 4 * r32);
+        vsb = (unsigned)(h * p.sb_rows + n0 + (wn >> 1) * 128 + 4 * r32);
+    };
+    auto coords = [&](int v, int& m0, int& n0) __attribute__((always_inline)) {
+        int bm, bn;
+        tile_coords<GROUP_M>(xcd_remap(v, ntiles), nbm, nbn, bm, bn);
+        m0 = bm * 256;
+        n0 = bn * 256;
+    };
+
+    f32x16 acc[4][2];
+    unsigned cur[4], nxt[4];
+    unsigned kscA = 0, kscB = 0;
+    auto load_sc = [&](unsigned (&d)[4]) __attribute__((always_inline)) {
+        d[0] = mx_sload<true>(vsa, rSA, kscA);
+        d[1] = mx_sload<true>(vsa, rSA, kscA + s2A);
+        d[2] = mx_sload<true>(vsb, rSB, kscB);
+        d[3] = mx_sload<true>(vsb, rSB, kscB + s2B);
+        kscA += sstepA;
+        kscB += sstepB;
+    };
+    // mx11's k-step and stage (mx11_tile), unchanged
+    auto step = [&](unsigned aa0, unsigned aa1, unsigned bb0, unsigned bb1, unsigned sa, unsigned sb, bool scl,
+                    bool dma, unsigned m0base, const unsigned (&voff)[4], i32x4v rs, unsigned soff, int wm_, int wc_,
+                    bool end_barrier) __attribute__((always_inline)) {
+        bf16x8 a[4][2], b[2][2];
+        ds_read16<0>(b[0][0], bb0);
+        ds_read16<0>(b[0][1], bb1);
+        ds_read16<4096>(b[1][0], bb0);
+        ds_read16<4096>(b[1][1], bb1);
+        ds_read16<0>(a[0][0], aa0);
+        ds_read16<0>(a[0][1], aa1);
+        ds_read16<4096>(a[1][0], aa0);
+        ds_read16<4096>(a[1][1], aa1);
+        ds_read16<8192>(a[2][0], aa0);
+        ds_read16<8192>(a[2][1], aa1);
+        ds_read16<12288>(a[3][0], aa0);
+        ds_read16<12288>(a[3][1], aa1);
+        if (scl) load_sc(nxt);
+        if (dma) mx_dma4<true>(m0base, voff, rs, soff);
+        if (wm_ == 0) vm_wait_sc<0>(nxt);
+        else if (wm_ == 4) vm_wait_sc<4>(nxt);
+        lgkm_wait<0>();
+        __builtin_amdgcn_s_barrier();
+        __builtin_amdgcn_s_setprio(1);
+        const unsigned sbs = sb >> bshift;
+        mx11_mfma<0, 0>(acc[0][0], a[0], b[0], sa, sbs);
+        mx11_mfma<0, 1>(acc[0][1], a[0], b[1], sa, sbs);
+        mx11_mfma<1, 0>(acc[1][0], a[1], b[0], sa, sbs);
+        mx11_mfma<1, 1>(acc[1][1], a[1], b[1], sa, sbs);
+        mx11_mfma<2, 0>(acc[2][0], a[2], b[0], sa, sbs);
+        mx11_mfma<2, 1>(acc[2][1], a[2], b[1], sa, sbs);
+        mx11_mfma<3, 0>(acc[3][0], a[3], b[0], sa, sbs);
+        mx11_mfma<3, 1>(acc[3][1], a[3], b[1], sa, sbs);
+        __builtin_amdgcn_s_setprio(0);
+        __builtin_amdgcn_sched_barrier(0);
+        if (wc_ == 0) vm_wait_sc<0>(nxt);
+        else if (wc_ == 4) vm_wait_sc<4>(nxt);
+        if (end_barrier) __builtin_amdgcn_s_barrier();
+    };
+    unsigned kB, kA;
+    auto stage = [&](int sa, bool dB, bool scl, bool dA, int need, bool last) __attribute__((always_inline)) {
+        const int sb = sa == 4 ? 0 : sa + 1;
+        const int iB = sa + 3 >= 5 ? sa - 2 : sa + 3, iA = sa + 4 >= 5 ? sa - 1 : sa + 4;
+        const unsigned as = a_x + sa * UNIT, bs = b_x + sb * UNIT;
+        step(as, as ^ (2u << 4), bs, bs ^ (2u << 4), cur[0], cur[2], scl, dB, lw + iB * UNIT, offB, rB, kB, -1, -1,
+             true);
+        step(as ^ (4u << 4), as ^ (6u << 4), bs ^ (4u << 4), bs ^ (6u << 4), cur[1], cur[3], false, dA,
+             lw + iA * UNIT, offA, rA, kA, LATE ? need : -1, LATE ? -1 : need, !(LATE && last));
+        kB += 128;
+        kA += 128;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) cur[q] = nxt[q];
+    };
+
+    int v = blockIdx.x;
+    if (v >= ntiles) return;  // whole workgroup
+    int m0, n0;
+    coords(v, m0, n0);
+    bool primed = false;  // this tile's A0 B0 A1 issued (and landed) under the previous tile's epilogue
+    while (true) {
+        // one prologue path for every tile (as pipe10): units A0 B0 A1 unless primed, then the scales of
+        // stages 0 and 1 and units B1 A2; one counted wait covers both paths (A0..A1, scales landed)
+        set_off(m0, n0);
+        kscA = kscB = 0;
+        if (SEAM == 2 || !primed) {
+            mx_dma4<true>(lw + 0 * UNIT, offA, rA, 0);
+            mx_dma4<true>(lw + 1 * UNIT, offB, rB, 0);
+            mx_dma4<true>(lw + 2 * UNIT, offA, rA, 128);
+        }
+        load_sc(cur);
+        load_sc(nxt);
+        mx_dma4<true>(lw + 3 * UNIT, offB, rB, 128);
+        mx_dma4<true>(lw + 4 * UNIT, offA, rA, 256);
+        vm_wait_sc<8>(cur);
+        vm_wait_sc<8>(nxt);
+        __builtin_amdgcn_s_barrier();
+        if (LATE) __builtin_amdgcn_s_barrier();
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int j = 0; j < 2; ++j)
+#pragma unroll
+                for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
+        {  // stage 0: its successors' units were issued before it; cur <- stage 1's scales
+            const unsigned c0 = cur[0], c1 = cur[1], c2 = cur[2], c3 = cur[3];
+            const unsigned bs = b_x + UNIT;
+            step(a_x, a_x ^ (2u << 4), bs, bs ^ (2u << 4), c0, c2, false, false, 0, offB, rB, 0, -1, -1, true);
+            step(a_x ^ (4u << 4), a_x ^ (6u << 4), bs ^ (4u << 4), bs ^ (6u << 4), c1, c3, false, false, 0, offA, rA,
+                 0, LATE ? 4 : -1, LATE ? -1 : 4, true);
+#pragma unroll
+            for (int q = 0; q < 4; ++q) cur[q] = nxt[q];
+        }
+        kB = 256;
+        kA = 384;
+        int s = 1;
+        for (; s + 5 <= nk - 2; s += 5) {
+            stage(2, true, true, true, 4, false);
+            stage(4, true, true, true, 4, false);
+            stage(1, true, true, true, 4, false);
+            stage(3, true, true, true, 4, false);
+            stage(0, true, true, true, 4, false);
+        }
+        if (s < nk - 2) {
+            stage(2, true, true, true, 4, false);
+            if (++s < nk - 2) {
+                stage(4, true, true, true, 4, false);
+                if (++s < nk - 2) {
+                    stage(1, true, true, true, 4, false);
+                    if (++s < nk - 2) {
+                        stage(3, true, true, true, 4, false);
+                        ++s;
+                    }
+                }
+            }
+        }
+        const int sa2 = (2 * s) % 5, sa1 = sa2 >= 3 ? sa2 - 3 : sa2 + 2;
+        stage(sa2, true, true, false, 0, false);
+        stage(sa1, false, false, false, -1, true);
+        vm_wait<0>();
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int j = 0; j < 2; ++j) asm volatile("" : "+v"(acc[i][j]));
+        // every wave's fragment reads of this tile precede the barrier closing the late row's last
+        // memory phase, which this wave has passed: the whole ring is free of reads
+        const int vn = v + gridDim.x;
+        const bool has_next = vn < ntiles;
+        int m1 = 0, n1 = 0;
+        if (has_next) coords(vn, m1, n1);
+        const bool prime = SEAM != 2 && has_next;
+        if (prime) {  // the next tile's A0 B0 A1 under this tile's epilogue
+            set_off(m1, n1);
+            mx_dma4<true>(lw + 0 * UNIT, offA, rA, 0);
+            mx_dma4<true>(lw + 1 * UNIT, offB, rB, 0);
+            mx_dma4<true>(lw + 2 * UNIT, offA, rA, 128);
+        }
+        {  // lane id from a volatile asm (pipe10: lane-derived epilogue addresses not hoisted and spilled)
+            int ln;
+            asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(ln));
+            mx_epilogue_wave<ACT, true, true, 2>(p, lds + 3 * UNIT, acc, m0, n0, wave, ln);
+        }
+        vm_wait<0>();  // own pieces of the next A0 B0 A1 landed (and this wave's stores retired)
+        __builtin_amdgcn_s_barrier();  // staging reads of every wave done: slots 3-4 free
+        if (!has_next) break;
+        v = vn;
+        m0 = m1;
+        n0 = n1;
+        primed = prime;
+    }
+}
+
+template <int GROUP_M, int ACT, int SEAM = 0>
+__global__ __launch_bounds__(512, 2) void gemm_mx12_kernel(MxArgs p) {
+    __shared__ __attribute__((aligned(16))) char lds[5 * 32768];
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    if (wave >= 4)
+        mx12_run<GROUP_M, ACT, true, SEAM>(p, lds, wave);
+    else
+        mx12_run<GROUP_M, ACT, false, SEAM>(p, lds, wave);
+}
+
+// one persistent workgroup per CU, a multiple of the 8 XCDs (the device's own CU count, read once)
+int mx_persistent_grid(int ntiles) {
+    static int cus[64] = {0};
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) dev = 0;
+    if (cus[dev] == 0) {
+        int n = 0;
+        if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
+        cus[dev] = n >= 8 ? n / 8 * 8 : n;
+    }
+    return ntiles < cus[dev] ? ntiles : cus[dev];
+}
+
+template <int GROUP_M, int SEAM = 0>
+int launch_mx12(const MxArgs& a, hipStream_t s) {
+    const dim3 grid(mx_persistent_grid(((a.M + 255) / 256) * ((a.N + 255) / 256))), block(512);
+    switch (a.act) {
+        case MME_ACT_GELU_TANH:
+            hipLaunchKernelGGL((gemm_mx12_kernel<GROUP_M, MME_ACT_GELU_TANH, SEAM>), grid, block, 0, s, a);
+            break;
+        case MME_ACT_QUICK_GELU:
+            hipLaunchKernelGGL((gemm_mx12_kernel<GROUP_M, MME_ACT_QUICK_GELU, SEAM>), grid, block, 0, s, a);
+            break;
+        case MME_ACT_GELU_ERF:
+            hipLaunchKernelGGL((gemm_mx12_kernel<GROUP_M, MME_ACT_GELU_ERF, SEAM>), grid, block, 0, s, a);
+            break;
+        default:
+            hipLaunchKernelGGL((gemm_mx12_kernel<GROUP_M, MME_ACT_NONE, SEAM>), grid, block, 0, s, a);
+            break;
+    }
+    return mme_check_launch("mme_gemm_mx");
+}
+
 #ifdef MME_DEV
 // ---------------------------------------------------------------------------
 // mx9 (dev variant 9, round 3; MME_DEV builds only): the block-scaled fp8 GEMM on
@@ -1149,9 +1442,9 @@ inline int mx_default_form() { return -1; }
 #endif
 inline bool mx_form_ok(int v) {
 #ifdef MME_DEV
-    return v == -1 || v == 0 || v == 2 || v == 3 || v == 4 || v == 9 || v == 10;
+    return v == -1 || v == 0 || v == 2 || v == 3 || v == 4 || v == 9 || v == 10 || v == 11 || v == 12 || v == 14;
 #else
-    return v == -1 || v == 0 || v == 2 || v == 3 || v == 10;
+    return v == -1 || v == 0 || v == 2 || v == 3 || v == 10 || v == 11 || v == 12 || v == 14;
 #endif
 }
 
@@ -1290,6 +1583,8 @@ int gemm_mx_entry(int form, const void* A, int lda, const void* sa, int sa_rows,
     // form 10 = mx10 (the bit-identity reference and A/B baseline)
     const bool mx11_ok = K % 128 == 0 && K >= 384 &&
                          (size_t)(K / 32) * (sa_rows > sb_rows ? sa_rows : sb_rows) < (1ull << 32);
+    if (form == 12 && mx11_ok) return launch_mx12<4>(a, as_stream(stream));
+    if (form == 14 && mx11_ok) return launch_mx12<4, 2>(a, as_stream(stream));
     if (form != 10 && mx11_ok) return launch_mx11<4>(a, as_stream(stream));
     return launch_mx10<4>(a, as_stream(stream));
 }

@@ -79,3 +79,21 @@ def test_production_library_holds_no_dev_forms():
     mx_args = [None, 64, None, 256, None, 64, None, 256, None, 64, None, 0, 16, 16, 64, None, None, 0, 0, 0, 0, None]
     assert lib.mme_gemm_mx_form(9, *mx_args) != 0 and b"development form" in lib.mme_last_error()
     assert lib.mme_attention_form(7, None, 8, None, 8, 1, 1, 1, 64, None, 0, 1.0, None) != 0
+
+
+def test_no_unpadded_sgpr_vmem_hazards():
+    """Round 5 (mx12): a v_readlane / v_readfirstlane that writes an SGPR, followed within 5 wait states by a
+    VMEM instruction reading it, loads from a stale offset on some waves of some launches; hipcc pads its own
+    instructions but not inline-asm loads, whose "s" operands can come straight from an SGPR-spill reload.
+    tools/asm_hazard_audit.py disassembles the library's gfx950 code objects: no such pair may remain."""
+    import shutil
+    import sys
+    if not os.path.exists("/opt/rocm/lib/llvm/bin/llvm-objdump") or shutil.which("python3") is None:
+        pytest.skip("llvm-objdump not available")
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import asm_hazard_audit
+    for name in ("libmme.so", "libmme_dev.so"):
+        lib = os.path.join(ROOT, "multimodal-embedding_amd", "mme", name)
+        if os.path.exists(lib):
+            hits = asm_hazard_audit.audit_lib(lib)
+            assert not hits, f"{name}: {len(hits)} unpadded pairs, first: {hits[0]}"

@@ -248,7 +248,7 @@ def test_gemm_mx_wave_epilogue_bit_identical(cuda, M, N, K, kind):
     bias = rnd(N, scale=0.1, gen=g)
     res0 = rnd(M, N, gen=g)
     outs = []
-    for v in (0, 2, 3, 10, -1):  # round-2 form, + per-wave epilogue, + single-wave scale DMA, mx10, production
+    for v in (0, 2, 3, 10, -1, 12):  # round-2 form, + per-wave epilogue, + scale DMA, mx10, production, mx12
         with ops.kernel_forms(mx=v):
             if kind == "mx_out":
                 o = mx.MXTensor.empty(M, N, "cuda")
@@ -262,6 +262,35 @@ def test_gemm_mx_wave_epilogue_bit_identical(cuda, M, N, K, kind):
     for o in outs[1:]:
         for p, q in zip(outs[0], o):
             assert torch.equal(p, q), f"mx GEMM form differs from the round-2 kernel ({kind}, {M}x{N}x{K})"
+
+
+@pytest.mark.parametrize("M,N,K,kind", [(304410, 5120, 1280, "mx_out"), (304410, 1280, 5120, "res"),
+                                         (304410, 3840, 1280, "bias"), (5000, 1280, 384, "res"), (100, 256, 512, "mx_out")])
+def test_gemm_mx12_bit_identical_to_mx11(cuda, M, N, K, kind):
+    """Forms 12 / 14 (mx12: persistent mx11, the next tile's first DMA units under the epilogue or not,
+    two-pass staging; measured slower, not dispatched) against form 11 (mx11) at DFN5B-H's execution batch (417 images x 730 tokens: many tiles per
+    CU) for the three fp8 encoder GEMMs with their job epilogues, the minimum K and fewer tiles than CUs:
+    bit-identical outputs and scales."""
+    g = torch.Generator(device="cuda").manual_seed(M + N + K)
+    a = mx.quantize(rnd(M, K, gen=g))
+    w = mx.quantize(rnd(N, K, scale=1 / math.sqrt(K), gen=g))
+    bias = rnd(N, scale=0.1, gen=g)
+    res0 = rnd(M, N, gen=g)
+    outs = []
+    for v in (11, 12, 14):
+        with ops.kernel_forms(mx=v):
+            if kind == "mx_out":
+                o = mx.MXTensor.empty(M, N, "cuda")
+                mx.gemm(a, w, bias, act=_lib.ACT_QUICK_GELU, out_mx=o)
+                outs.append((o.q[:M, :N].clone(), o.scales[:, torch.from_numpy(omx.srow(np.arange(M))).cuda()].clone()))
+            else:
+                x = res0.clone()
+                y = mx.gemm(a, w, bias, residual=x if kind == "res" else None, out=x)
+                outs.append((y.clone(),))
+        torch.cuda.synchronize()
+    for o in outs[1:]:
+        for p, q in zip(outs[0], o):
+            assert torch.equal(p, q), f"mx12 differs from mx11 ({kind}, {M}x{N}x{K})"
 
 
 @pytest.mark.slow
