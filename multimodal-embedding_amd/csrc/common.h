@@ -127,7 +127,8 @@ __device__ __forceinline__ void wait_vmcnt0() { asm volatile("s_waitcnt vmcnt(0)
 // wait + barrier before the bytes are read. `lds_base` must be wave-uniform (M0).
 __device__ __forceinline__ void glds16_asm(const void* gsrc, void* lds_base) {
     const unsigned m0 = __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)(LDS_AS char*)lds_base);
-    asm volatile("s_mov_b32 m0, %1\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(gsrc), "s"(m0) : "memory", "m0");
+    // s_nop 0: the M0 write -> LDS-DMA wait state (hipcc pads no hazard inside a statement)
+    asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(gsrc), "s"(m0) : "memory", "m0");
 }
 
 typedef float f32x2 __attribute__((ext_vector_type(2)));

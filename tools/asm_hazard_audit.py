@@ -1,10 +1,11 @@
 #!/usr/bin/env python3
-"""Audit the gfx950 code of libmme.so for the hazard round 5 found in the persistent fp8 GEMM (mx12):
-a VALU write of an SGPR (v_readlane / v_readfirstlane: SGPR-spill reloads, uniform values) followed, within
+"""Audit the gfx950 code of libmme.so for two hazards that hipcc does not pad inside inline asm:
+(1) the one round 5 found in the persistent fp8 GEMM (mx12): a VALU write of an SGPR (v_readlane / v_readfirstlane: SGPR-spill reloads, uniform values) followed, within
 5 wait states, by a VMEM instruction that reads that SGPR (descriptor, soffset or saddr). The hardware needs
 the 5 wait states; hipcc inserts them for the instructions it generates, but not for an inline-asm consumer,
 so a hit in the final code object is always an unpadded inline-asm load (stale soffset -> wrong data, on
-some waves of some launches).
+some waves of some launches); (2) an SALU write of M0 immediately followed by an LDS-DMA load, which
+takes its LDS destination from M0 and needs one wait state after the write.
 
     python tools/asm_hazard_audit.py [path/to/libmme.so]        # exit 1 on any hit
 """
@@ -49,6 +50,11 @@ def audit_text(text: str):
         lines.append((fn, ins))
     hits = []
     for i, (fn, ins) in enumerate(lines):
+        # an SALU write of M0 directly followed by an LDS-DMA load (which takes its LDS base from M0): 1 wait state
+        if re.match(r"s_(mov|add|sub)_[ub]32 m0\b", ins) and i + 1 < len(lines):
+            nxt = lines[i + 1][1]
+            if re.match(r"(buffer_load_\w+ .* lds$|global_load_lds_)", nxt):
+                hits.append((fn, i, f"{ins}  ->  {nxt}"))
         m = re.match(r"v_read(?:first)?lane_b32 s(\d+)", ins)
         if not m:
             continue
@@ -83,5 +89,5 @@ if __name__ == "__main__":
     hits = audit_lib(lib)
     for fn, i, what in hits[:40]:
         print(f"{fn[:90]}  #{i}: {what}")
-    print(f"{len(hits)} unpadded VALU-SGPR-write -> VMEM-read pairs in {lib}")
+    print(f"{len(hits)} unpadded hazard pairs (VALU SGPR write -> VMEM read, M0 write -> LDS-DMA) in {lib}")
     sys.exit(1 if hits else 0)
