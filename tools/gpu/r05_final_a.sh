@@ -1,4 +1,4 @@
-# Round-5 final measurement set, part A: GPU tests, smoke, the headline bench (+ CPU baseline, parity),
+# Round-5 final measurement set, part A: GPU tests (production and development libraries), smoke, the headline bench (+ CPU baseline, parity),
 # the PMC HBM-traffic passes at the bench geometry (first, so the bench line carries this build's traffic),
 # the bench's rocprofv3 kernel summary + timing check, and the production fc1 GEMM's counters.
 set -o pipefail
@@ -10,6 +10,8 @@ P=gpurun_out/${RUN:-r05_final}
 trap "kill $HB 2>/dev/null" EXIT
 timeout -k 10 900 python -u -m pytest -q -rs --maxfail=5 --timeout 300 --timeout-method thread -m gpu tests/ > ${P}_pytest.log 2>&1
 rc=$?; tail -2 ${P}_pytest.log; [ $rc -ne 0 ] && exit $rc
+MME_DEV=1 timeout -k 10 900 python -u -m pytest -q -rs --maxfail=5 --timeout 300 --timeout-method thread -m gpu tests/ > ${P}_dev_pytest.log 2>&1
+rc=$?; tail -2 ${P}_dev_pytest.log; [ $rc -ne 0 ] && exit $rc
 timeout -k 10 200 python -u -c "import __graft_entry__ as g; g.smoke()" > ${P}_smoke.log 2>&1 || exit $?
 PMC_CONFIG='{"model": "SigLIP-400M", "n_images": 5000, "img_batch": 512, "txt_batch": 8192, "fp8": false}' \
 PMC_BUILD="${RUN:-r05_final}" bash tools/pmc_job.sh > ${P}_pmc.log 2>&1 || { tail -5 ${P}_pmc.log; exit 1; }
