@@ -153,7 +153,9 @@ int mme_attention(const void* qkv, int ld_qkv, void* out, int ld_out, int B, int
  *   mme_attention_form: 0 = production, 30 + kind = kernel kind `kind` (production: 83 hd 72,
  *     86 / 87 hd 80, 89 hd 64; 94 = the persistent form of 86, measured and not dispatched);
  *   mme_gemm_mx_form (below): -1 = production (mx11 where its geometry holds, else mx10),
- *     10 = mx10, 0 / 2 / 3 = earlier forms. */
+ *     11 = mx11, 10 = mx10, 0 / 2 / 3 = earlier forms, 12 / 14 = mx12 (persistent mx11 with / without
+ *     the next tile's DMA under the epilogue; measured slower, not dispatched);
+ *   mme_gemm_form 95 = pipe10 on every non-split GEMM (measured slower, not dispatched). */
 int mme_gemm_form(int form, const void* A, int lda, const void* B, int ldb, void* C, int ldc, int M, int N, int K,
                   const void* bias, const void* residual, int ldr, int res_period, int act, int out_f32,
                   void* stream);
