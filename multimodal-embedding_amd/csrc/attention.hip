@@ -3617,7 +3617,7 @@ int attention_entry(int form, const void* qkv, int ld_qkv, void* out, int ld_out
     // first K / V tile loaded under the current unit's last tile: bit-identical, 7 % faster in isolation
     // (ViT-H at 455 / 512 images: 0.48 / 0.53 -> 0.45 / 0.49 ms, profiles/r05_v10_attn_vith_batches.log)
     // but 3 % slower inside the LAION-CLIP-H job (466 vs 480 us per launch, jobs level;
-    // profiles/r05_v9_*): not dispatched.
+    // profiles/r05_v9_laion_kind94_vs_kind86_ab.log): not dispatched.
     int kind = T <= 64 ? 16
                : (T <= 128 || hd == 64) ? 89
                : (hd == 80 && pad9 * 10 < min(pad8, pad4) * 9) ? 86

@@ -988,7 +988,7 @@ int launch_mx11(const MxArgs& a, hipStream_t s) {
 // as soon as this tile's last fragment reads are done, i.e. under its epilogue, which stages through
 // slots 3-4 only (two 64-row passes); after it every wave waits for its own loads, one barrier frees
 // slots 3-4, and the next tile's scales and units B1 A2 follow.
-// Measured (round 5, profiles/r05_v12_mx12_gemm.log, r05_v12_fp8_*): bit-identical to mx11 but slower on
+// Measured (round 5, profiles/r05_v12_mx12_gemm.log, r05_v12_fp8_mx12_job_ab.log): bit-identical to mx11 but slower on
 // every DFN5B-H shape with the job's epilogues (QKV 1.45 -> 1.49, fc1 2.30 -> 2.35-2.40, fc2 1.74 ->
 // 1.78-1.81 ms; the fp8 job 1 172-1 174 -> 1 160-1 162 img/s): the persistent loop holds 255 VGPRs and
 // spills 25-40 SGPRs, whose reloads feed the asm loads (next paragraph), so the seam it hides costs more

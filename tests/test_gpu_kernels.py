@@ -193,7 +193,7 @@ def test_attention_skip_vs_unskipped(cuda, hd, kind, ref, B, T, H, causal, lens)
     round 5 attention.hip is built with -ffp-contract=off and states its FMAs explicitly (the exp2
     argument fma(s, c, -m c)), so no kernel's arithmetic depends on where the compiler contracts a
     multiply-add: round 4's rare 1-2 ulp differences between these pairs were exactly that
-    (profiles/r05_v1_skip_contract_{on,off}.log: 0 of every output differ with contraction off)."""
+    (profiles/r05_v1_skip_contract_on_off.log: 0 of every output differ with contraction off)."""
     g = torch.Generator(device="cuda").manual_seed(B * T + hd)
     qkv = rnd(B * T, 3 * H * hd, scale=1.5, gen=g)
     sl = None if lens is None else torch.tensor(lens, dtype=torch.int32, device="cuda")
