@@ -161,7 +161,7 @@ __device__ __forceinline__ float row8_sum(float v) {
 // Shared epilogue of the pipelined kernels: bias + activation in registers,
 // bf16 tile staged in LDS (row pitch BN*2+16 B), 16-B stores with the
 // residual / position-table add fused. Starts with a barrier (LDS reuse).
-template <class C, int ACT, int EDIAG = 0>
+template <class C, int ACT, int EDIAG = 0, int FOLD = 0>
 __device__ __forceinline__ void gemm_epilogue_lds(const GemmArgs& p, char* lds, f32x4 (&acc)[C::FM][C::FN], int m0,
                                                   int n0, int wm, int wn, int g, int li, int tid) {
     // EDIAG (dev builds, wrong results): 1 = no global stores, 2 = no epilogue at all
@@ -179,6 +179,9 @@ __device__ __forceinline__ void gemm_epilogue_lds(const GemmArgs& p, char* lds, 
     // features -> out[:, gc/2 + e] = bf16( bf16(gelu_tanh(bf16 gate)) * bf16 up )
     // (GemmaMLP.forward act_fn(gate_proj(x)) * up_proj(x), TF:models/gemma/modeling_gemma.py:95-96).
     constexpr bool GLU = ACT == MME_ACT_GEGLU_TANH;
+    // FOLD: the operand set fixed at compile time, as in gemm_epilogue_wave (1 fold, 2 bias, 3 residual)
+    const bool lnf = FOLD == 1 ? true : FOLD >= 2 ? false : p.ln_stats != nullptr;
+    const bool hres = FOLD == 3 ? true : FOLD != 0 ? false : p.res != nullptr;
     constexpr int RACT = GLU ? MME_ACT_NONE : ACT;
     constexpr int CPR = C::BN / 8;                // 16-B chunks per tile row
     constexpr int NCH = C::BM * CPR / C::NT;      // chunks per thread
@@ -187,7 +190,7 @@ __device__ __forceinline__ void gemm_epilogue_lds(const GemmArgs& p, char* lds, 
     // overlaps the accumulator staging below (the main loop's counted vmcnt is done;
     // these are the only loads in flight). o_proj 186624 x 1152 x 1152 + residual: 0.630 -> 0.589 ms.
     u16x8 rv[NCH];
-    if (!GLU && p.res) {
+    if (!GLU && hres) {
 #pragma unroll
         for (int q = 0; q < NCH; ++q) {
             const int c = tid + q * C::NT;
@@ -199,7 +202,7 @@ __device__ __forceinline__ void gemm_epilogue_lds(const GemmArgs& p, char* lds, 
     __syncthreads();
     // folded LayerNorm: per row (scale, shift) = (rstd, -rstd * mean), per column (cs, b)
     float lr[C::FM], lm[C::FM];
-    if (p.ln_stats) {
+    if (lnf) {
 #pragma unroll
         for (int i = 0; i < C::FM; ++i) {
             const int gr = min(m0 + wm * C::TM + i * 16 + li, p.M - 1);
@@ -212,7 +215,7 @@ __device__ __forceinline__ void gemm_epilogue_lds(const GemmArgs& p, char* lds, 
     for (int j = 0; j < C::FN; ++j) {
         const int nl = wn * C::TN + j * 16 + 4 * g;
         float bv[4] = {0.f, 0.f, 0.f, 0.f}, cs[4] = {0.f, 0.f, 0.f, 0.f};
-        if (p.ln_stats) {  // 4 consecutive columns: one 16-B load each (N % 8 == 0 on this path)
+        if (lnf) {  // 4 consecutive columns: one 16-B load each (N % 8 == 0 on this path)
             const int c4 = min(n0 + nl, p.N - 4);
             const float4 b4 = *reinterpret_cast<const float4*>(p.ln_b + c4);
             const float4 s4 = *reinterpret_cast<const float4*>(p.ln_cs + c4);
@@ -226,7 +229,7 @@ __device__ __forceinline__ void gemm_epilogue_lds(const GemmArgs& p, char* lds, 
         for (int i = 0; i < C::FM; ++i) {
             const int ml = wm * C::TM + i * 16 + li;
             bf16x4 o;
-            if (p.ln_stats) {
+            if (lnf) {
 #pragma unroll
                 for (int r = 0; r < 4; r += 2) {
                     const f32x2 y = apply_act2(
@@ -266,7 +269,7 @@ __device__ __forceinline__ void gemm_epilogue_lds(const GemmArgs& p, char* lds, 
                 o[e] = __builtin_bit_cast(unsigned short,
                                           f2bf(bf2f(f2bf(apply_act(bits2f(v[e]), MME_ACT_GELU_TANH))) * bits2f(v[4 + e])));
             __builtin_nontemporal_store(o, reinterpret_cast<u16x4*>(Cout + (size_t)gr * p.ldc + gc / 2));
-        } else if (p.res) {
+        } else if (hres) {
             u16x8 o;
 #pragma unroll
             for (int e = 0; e < 8; ++e) o[e] = __builtin_bit_cast(unsigned short, f2bf(bits2f(v[e]) + bits2f(rv[q][e])));
@@ -701,7 +704,7 @@ __device__ __forceinline__ void gemm_epilogue_direct(const GemmArgs& p, f32x4 (&
 // entry, main loop done, epilogue issued, epilogue stores retired (tools/gemm_stamps.py)
 __device__ unsigned long long* g_gemm_dbg;
 
-template <class C, int ACT, int STAG, int DIAG>
+template <class C, int ACT, int STAG, int DIAG, int FOLD = 0>
 __device__ __forceinline__ void pipe6_tile(const GemmArgs& p, char* lds, const int m0, const int n0) {
     const int tid = threadIdx.x, lane = tid & 63;
     unsigned long long st0 = 0, st1 = 0;
@@ -813,7 +816,7 @@ __device__ __forceinline__ void pipe6_tile(const GemmArgs& p, char* lds, const i
     if constexpr (DIAG == 11)
         gemm_epilogue_direct<C, ACT>(p, acc, m0, n0, wm, wn, g, li);
     else
-        gemm_epilogue_lds<C, ACT, (DIAG >= 6 && DIAG <= 8 ? DIAG - 5 : 0)>(p, lds, acc, m0, n0, wm, wn, g, li, tid);
+        gemm_epilogue_lds<C, ACT, (DIAG >= 6 && DIAG <= 8 ? DIAG - 5 : 0), FOLD>(p, lds, acc, m0, n0, wm, wn, g, li, tid);
     if (DIAG == 12) {
         const unsigned long long st2 = __builtin_amdgcn_s_memrealtime();
         vm_wait<0>();
@@ -917,11 +920,26 @@ int launch_pipe6(const GemmArgs& a, hipStream_t s) {
 // SQ_LDS_BANK_CONFLICT cycles per fc1 launch (profiles/r03_v12_pmc_gemm_util_fc1.json).
 // PASSES (pipe10, round 4): the sub-tile staged and stored in PASSES row bands through a region of
 // 128 / PASSES rows per wave (2: 8 KiB per wave, 64 KiB for the block, two of the five ring units).
-template <class C, int ACT, bool SWZ = true, int PASSES = 1>
+struct NoHook {
+    __device__ void operator()() const {}
+};
+
+// PRE: every row and column constant of the epilogue (LayerNorm fold: rstd_r, -rstd_r mean_r, b'_n, sum w'_n;
+// else the bias) is loaded and waited for first, then hook() runs (pipe10's SEAM 1 issues the next tile's
+// DMA there), and the passes reuse the registers: no load follows the hook.
+template <class C, int ACT, bool SWZ = true, int PASSES = 1, int PRE = 0, int FOLD = 0,
+          class Hook = NoHook>
 __device__ __forceinline__ void gemm_epilogue_wave(const GemmArgs& p, char* lds, f32x4 (&acc)[C::FM][C::FN], int m0,
-                                                   int n0, int wave, int wm, int wn, int g, int li, int lane) {
+                                                   int n0, int wave, int wm, int wn, int g, int li, int lane,
+                                                   Hook hook = Hook{}) {
     static_assert(C::TM == 128 && C::TN == 64 && C::FM == 8 && C::FN == 4, "per-wave epilogue: 128 x 64 wave tiles");
     static_assert(PASSES == 1 || (PASSES == 2 && SWZ), "one or two staging passes");
+    // FOLD 1: LayerNorm fold, no residual; FOLD 2: bias (or none), no residual, no fold; FOLD 3: residual
+    // (+ row statistics), no fold; FOLD 0: decided per call from p. The compile-time forms let hipcc schedule across the unrolled (i, j) pairs: with the
+    // per-pair runtime branches it padded each pair's transcendental chain with s_nop and waited for every
+    // column pair's constants in turn.
+    const bool lnf = FOLD == 1 ? true : FOLD >= 2 ? false : p.ln_stats != nullptr;
+    const bool hres = FOLD == 3 ? true : FOLD != 0 ? false : p.res != nullptr;
     constexpr bool GLU = ACT == MME_ACT_GEGLU_TANH;
     constexpr int RACT = GLU ? MME_ACT_NONE : ACT;
     constexpr int PITCH = SWZ ? 128 : 144, REGION = 128 * PITCH / PASSES, BAND = 128 / PASSES;
@@ -930,7 +948,7 @@ __device__ __forceinline__ void gemm_epilogue_wave(const GemmArgs& p, char* lds,
     const int rr = lane >> 3, cc = lane & 7;                 // store phase: row rr of 8, 16-B chunk cc
     u16x8 rv[16 / PASSES];  // residual rows of the current pass (all 16 row groups with one pass)
     auto load_res = [&](int ps) __attribute__((always_inline)) {
-        if (!GLU && p.res) {
+        if (!GLU && hres) {
 #pragma unroll
             for (int q = 0; q < 16 / PASSES; ++q) {
                 const int gr = min(rm0 + (ps * (16 / PASSES) + q) * 8 + rr, p.M - 1), gc = min(cn0 + cc * 8, p.N - 8);
@@ -940,7 +958,7 @@ __device__ __forceinline__ void gemm_epilogue_wave(const GemmArgs& p, char* lds,
         }
     };
     if constexpr (PASSES == 1) {
-        if (!GLU && p.res) {  // residual rows first: their latency overlaps the staging below
+        if (!GLU && hres) {  // residual rows first: their latency overlaps the staging below
 #pragma unroll
             for (int q = 0; q < 16; ++q) {
                 const int gr = min(rm0 + q * 8 + rr, p.M - 1), gc = min(cn0 + cc * 8, p.N - 8);
@@ -950,7 +968,7 @@ __device__ __forceinline__ void gemm_epilogue_wave(const GemmArgs& p, char* lds,
         }
     }
     float lr[C::FM], lm[C::FM];
-    if (p.ln_stats) {
+    if (lnf) {
 #pragma unroll
         for (int i = 0; i < C::FM; ++i) {
             const int gr = min(rm0 + i * 16 + li, p.M - 1);
@@ -959,13 +977,49 @@ __device__ __forceinline__ void gemm_epilogue_wave(const GemmArgs& p, char* lds,
             lm[i] = -st.y * st.x;
         }
     }
+    float pbv[PRE ? C::FN : 1][4], pcs[PRE ? C::FN : 1][4];
+    if constexpr (PRE) {
+#pragma unroll
+        for (int j = 0; j < C::FN; ++j) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) pbv[j][r] = pcs[j][r] = 0.f;
+            if (lnf) {
+                const int c4 = min(cn0 + j * 16 + 4 * g, p.N - 4);
+                const float4 b4 = *reinterpret_cast<const float4*>(p.ln_b + c4);
+                const float4 s4 = *reinterpret_cast<const float4*>(p.ln_cs + c4);
+                pbv[j][0] = b4.x, pbv[j][1] = b4.y, pbv[j][2] = b4.z, pbv[j][3] = b4.w;
+                pcs[j][0] = s4.x, pcs[j][1] = s4.y, pcs[j][2] = s4.z, pcs[j][3] = s4.w;
+            } else if (p.bias) {
+#pragma unroll
+                for (int r = 0; r < 4; ++r) pbv[j][r] = bf2f(p.bias[min(cn0 + j * 16 + 4 * g + r, p.N - 1)]);
+            }
+        }
+    }
+    auto preload_done = [&]() __attribute__((always_inline)) {  // every preloaded constant landed, then the hook
+        if (lnf) {
+#pragma unroll
+            for (int i = 0; i < C::FM; ++i) asm volatile("" ::"v"(lr[i]), "v"(lm[i]));
+        }
+#pragma unroll
+        for (int j = 0; j < C::FN; ++j)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) asm volatile("" ::"v"(pbv[j][r]), "v"(pcs[j][r]));
+        hook();
+    };
+    if constexpr (PRE == 1) preload_done();
 #pragma unroll
     for (int ps = 0; ps < PASSES; ++ps) {
+    if constexpr (PRE == 2) {
+        if (ps == 1) preload_done();
+    }
     if constexpr (PASSES > 1) load_res(ps);
 #pragma unroll
     for (int j = 0; j < C::FN; ++j) {
         float bv[4] = {0.f, 0.f, 0.f, 0.f}, cs[4] = {0.f, 0.f, 0.f, 0.f};
-        if (p.ln_stats) {
+        if constexpr (PRE) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) bv[r] = pbv[j][r], cs[r] = pcs[j][r];
+        } else if (lnf) {
             const int c4 = min(cn0 + j * 16 + 4 * g, p.N - 4);
             const float4 b4 = *reinterpret_cast<const float4*>(p.ln_b + c4);
             const float4 s4 = *reinterpret_cast<const float4*>(p.ln_cs + c4);
@@ -978,7 +1032,7 @@ __device__ __forceinline__ void gemm_epilogue_wave(const GemmArgs& p, char* lds,
 #pragma unroll
         for (int i = ps * (C::FM / PASSES); i < (ps + 1) * (C::FM / PASSES); ++i) {
             bf16x4 o;
-            if (p.ln_stats) {
+            if (lnf) {
 #pragma unroll
                 for (int r = 0; r < 4; r += 2) {
                     const f32x2 y = apply_act2(
@@ -1025,7 +1079,7 @@ __device__ __forceinline__ void gemm_epilogue_wave(const GemmArgs& p, char* lds,
                 o[e] = __builtin_bit_cast(unsigned short,
                                           f2bf(bf2f(f2bf(apply_act(bits2f(v[e]), MME_ACT_GELU_TANH))) * bits2f(v[4 + e])));
             __builtin_nontemporal_store(o, reinterpret_cast<u16x4*>(Cout + (size_t)gr * p.ldc + gc / 2));
-        } else if (p.res) {
+        } else if (hres) {
             u16x8 o;
 #pragma unroll
             for (int e = 0; e < 8; ++e)
@@ -1238,7 +1292,7 @@ __device__ __forceinline__ void dma4(unsigned m0base, const unsigned (&voff)[4],
 // PRIO (dev variants 81 / 82): 0 = s_setprio 1 around every compute phase (production);
 // 1 = static priority 1 for the late wave row, no per-phase flips (MI355X_MICROARCH.md, two waves
 // per SIMD, item 4); 2 = no priority changes.
-template <class C, int ACT, bool LATE, int PRIO = 0, bool ESWZ = true>
+template <class C, int ACT, bool LATE, int PRIO = 0, bool ESWZ = true, int FOLD = 0>
 __device__ __forceinline__ void pipe9_tile(const GemmArgs& p, char* lds, const int m0, const int n0, const int wave) {
     static_assert(C::BM == 256 && C::BN == 256 && C::FN == 4 && C::FM == 8 && C::NW == 8, "pipe9: 256 x 256, 8 waves");
     constexpr int UNIT = 32768;
@@ -1358,11 +1412,11 @@ __device__ __forceinline__ void pipe9_tile(const GemmArgs& p, char* lds, const i
     stage(sa2, true, false, 0, false);
     stage(sa1, false, false, -1, true);
     vm_wait<0>();
-    gemm_epilogue_wave<C, ACT, ESWZ>(p, lds, acc, m0, n0, wave, wm, wn, g, li, lane);
+    gemm_epilogue_wave<C, ACT, ESWZ, 1, 0, FOLD>(p, lds, acc, m0, n0, wave, wm, wn, g, li, lane);
 }
 
 // ESWZ: the conflict-free staging layout of gemm_epilogue_wave (round 4); false = pitch 144 (dev form 84)
-template <class C, int GROUP_M, int ACT, bool SPLIT, int PRIO = 0, bool ESWZ = true>
+template <class C, int GROUP_M, int ACT, bool SPLIT, int PRIO = 0, bool ESWZ = true, int FOLD = 0>
 __global__ __launch_bounds__(C::NT, 2) void gemm_pipe9_kernel(GemmArgs p) {
     __shared__ __attribute__((aligned(16))) char lds[5 * 32768];
     const int nbm = (p.M + C::BM - 1) / C::BM;
@@ -1370,7 +1424,7 @@ __global__ __launch_bounds__(C::NT, 2) void gemm_pipe9_kernel(GemmArgs p) {
     int m0, n0;
     if constexpr (SPLIT) {
         if (split_coords(tile, nbm, p.N / C::BN, m0, n0)) {
-            pipe6_tile<Pipe512x128, ACT, 1, 0>(p, lds, m0, n0);
+            pipe6_tile<Pipe512x128, ACT, 1, 0, FOLD>(p, lds, m0, n0);
             return;
         }
     } else {
@@ -1382,9 +1436,9 @@ __global__ __launch_bounds__(C::NT, 2) void gemm_pipe9_kernel(GemmArgs p) {
     }
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     if (wave >= C::NW / 2)
-        pipe9_tile<C, ACT, true, PRIO, ESWZ>(p, lds, m0, n0, wave);
+        pipe9_tile<C, ACT, true, PRIO, ESWZ, FOLD>(p, lds, m0, n0, wave);
     else
-        pipe9_tile<C, ACT, false, PRIO, ESWZ>(p, lds, m0, n0, wave);
+        pipe9_tile<C, ACT, false, PRIO, ESWZ, FOLD>(p, lds, m0, n0, wave);
 }
 
 // ---------------------------------------------------------------------------
@@ -1400,7 +1454,7 @@ __global__ __launch_bounds__(C::NT, 2) void gemm_pipe9_kernel(GemmArgs p) {
 // pipe9's do (pipe6_tile, whole LDS) with a barrier after each and a full prologue for the next.
 // Barrier counts stay equal for the two wave rows: per tile pipe9's, plus one after the epilogue.
 // ---------------------------------------------------------------------------
-template <class C, int GROUP_M, int ACT, bool LATE, bool SPLIT>
+template <class C, int GROUP_M, int ACT, bool LATE, bool SPLIT, int SEAM = 0, int FOLD = 0>
 __device__ __forceinline__ void pipe10_run(const GemmArgs& p, char* lds, const int wave) {
     static_assert(C::BM == 256 && C::BN == 256 && C::FN == 4 && C::FM == 8 && C::NW == 8, "pipe10: 256 x 256, 8 waves");
     constexpr int UNIT = 32768;
@@ -1559,20 +1613,47 @@ __device__ __forceinline__ void pipe10_run(const GemmArgs& p, char* lds, const i
         const bool has_next = vn < ntiles;
         const bool split1 = has_next ? coords(vn, m1, n1) : false;
         const bool prime = has_next && !split1;
-        if (prime) {  // the next tile's A0 B0 A1 under this tile's epilogue (offsets recomputed after it:
-                      // not held live across the epilogue)
-            set_off(m1, n1);
-            dma4(lw + 0 * UNIT, offA, rA, 0);
-            dma4(lw + 1 * UNIT, offB, rB, 0);
-            dma4(lw + 2 * UNIT, offA, rA, 128);
-        }
-        {  // the lane id from a volatile asm: the epilogue's lane-derived addresses are recomputed per
-           // tile instead of being hoisted to kernel entry and spilled around the tile loop
+        if constexpr (SEAM >= 1) {
+            // SEAM 1: the epilogue's row / column constants are loaded and waited for BEFORE the next tile's
+            // DMA is issued (gemm_epilogue_wave's PRE hook): hipcc cannot see the asm DMA, so a wait it places
+            // for a load issued after the DMA counts the DMA too (vmcnt retires in issue order) and holds the
+            // epilogue's first arithmetic until the next tile's three units have landed; and the second
+            // staging pass re-loaded its column constants behind the first pass's stores. The stores are then
+            // the only vector memory operations younger than the DMA, so the wait that retires the DMA leaves
+            // them in flight (vmcnt(16): a full interior wave tile issues 16; a clipped edge tile waits for all).
             int ln;
             asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(ln));
-            gemm_epilogue_wave<C, ACT, true, 2>(p, lds + 3 * UNIT, acc, m0, n0, wave, wm, wn, ln >> 4, ln & 15, ln);
+            auto dma_next = [&]() __attribute__((always_inline)) {
+                if (prime) {
+                    set_off(m1, n1);
+                    dma4(lw + 0 * UNIT, offA, rA, 0);
+                    dma4(lw + 1 * UNIT, offB, rB, 0);
+                    dma4(lw + 2 * UNIT, offA, rA, 128);
+                }
+            };
+            gemm_epilogue_wave<C, ACT, true, 2, SEAM, FOLD>(p, lds + 3 * UNIT, acc, m0, n0, wave, wm, wn, ln >> 4, ln & 15,
+                                                      ln, dma_next);
+            if (m0 + wm * C::TM + C::TM <= p.M && n0 + wn * C::TN + C::TN <= p.N)
+                vm_wait<SEAM == 1 ? 16 : 8>();  // own pieces of units 0-2 landed; this wave's 16 stores may still be in flight
+            else
+                vm_wait<0>();
+        } else {
+            if (prime) {  // the next tile's A0 B0 A1 under this tile's epilogue (offsets recomputed after it:
+                          // not held live across the epilogue)
+                set_off(m1, n1);
+                dma4(lw + 0 * UNIT, offA, rA, 0);
+                dma4(lw + 1 * UNIT, offB, rB, 0);
+                dma4(lw + 2 * UNIT, offA, rA, 128);
+            }
+            {  // the lane id from a volatile asm: the epilogue's lane-derived addresses are recomputed per
+               // tile instead of being hoisted to kernel entry and spilled around the tile loop
+                int ln;
+                asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(ln));
+                gemm_epilogue_wave<C, ACT, true, 2, 0, FOLD>(p, lds + 3 * UNIT, acc, m0, n0, wave, wm, wn, ln >> 4, ln & 15,
+                                                    ln);
+            }
+            vm_wait<0>();  // own pieces of units 0-2 landed (and this wave's stores retired)
         }
-        vm_wait<0>();  // own pieces of units 0-2 landed (and this wave's stores retired)
         __builtin_amdgcn_s_barrier();  // staging reads of every wave done: slots 3-4 free
         if (!has_next) break;
         v = vn;
@@ -1590,15 +1671,15 @@ __device__ __forceinline__ void pipe10_run(const GemmArgs& p, char* lds, const i
     }
 }
 
-template <class C, int GROUP_M, int ACT, bool SPLIT>
+template <class C, int GROUP_M, int ACT, bool SPLIT, int SEAM = 0, int FOLD = 0>
 __global__ __launch_bounds__(C::NT, 2) void gemm_pipe10_kernel(GemmArgs p) {
     __shared__ __attribute__((aligned(16))) char lds[5 * 32768];
     static_assert(Pipe512x128::LDS <= 5 * 32768, "pipe10 LDS");
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     if (wave >= C::NW / 2)
-        pipe10_run<C, GROUP_M, ACT, true, SPLIT>(p, lds, wave);
+        pipe10_run<C, GROUP_M, ACT, true, SPLIT, SEAM, FOLD>(p, lds, wave);
     else
-        pipe10_run<C, GROUP_M, ACT, false, SPLIT>(p, lds, wave);
+        pipe10_run<C, GROUP_M, ACT, false, SPLIT, SEAM, FOLD>(p, lds, wave);
 }
 
 // Workgroups of a persistent GEMM grid: one per CU (160 KiB of LDS each), rounded down to a multiple of
@@ -1616,28 +1697,30 @@ int persistent_grid(int ntiles) {
     return std::min(ntiles, cus[dev]);
 }
 
-template <class C, int GROUP_M, bool SPLIT>
+template <class C, int GROUP_M, bool SPLIT, int SEAM = 0, bool SPEC = false>
 int launch_pipe10(const GemmArgs& a, hipStream_t s) {
     const int nbm = (a.M + C::BM - 1) / C::BM, nbn = (a.N + C::BN - 1) / C::BN;
     const int ntiles = SPLIT ? split_tiles(nbm, a.N / C::BN) : nbm * nbn;
     const dim3 grid(persistent_grid(ntiles)), block(C::NT);
+    // SPEC: the fc1 epilogues compiled for their operands (FOLD 1: LayerNorm fold; FOLD 2: bias), no residual
+    const int fold = !SPEC || a.res ? 0 : a.ln_stats ? 1 : 2;
+#define MME_P10(ACT_)                                                                                          \
+    if (fold == 1)                                                                                            \
+        hipLaunchKernelGGL((gemm_pipe10_kernel<C, GROUP_M, ACT_, SPLIT, SEAM, SPEC ? 1 : 0>), grid, block, 0, s, a); \
+    else if (fold == 2)                                                                                       \
+        hipLaunchKernelGGL((gemm_pipe10_kernel<C, GROUP_M, ACT_, SPLIT, SEAM, SPEC ? 2 : 0>), grid, block, 0, s, a); \
+    else                                                                                                      \
+        hipLaunchKernelGGL((gemm_pipe10_kernel<C, GROUP_M, ACT_, SPLIT, SEAM, 0>), grid, block, 0, s, a);
     switch (a.act) {
-        case MME_ACT_GELU_TANH:
-            hipLaunchKernelGGL((gemm_pipe10_kernel<C, GROUP_M, MME_ACT_GELU_TANH, SPLIT>), grid, block, 0, s, a);
-            break;
-        case MME_ACT_QUICK_GELU:
-            hipLaunchKernelGGL((gemm_pipe10_kernel<C, GROUP_M, MME_ACT_QUICK_GELU, SPLIT>), grid, block, 0, s, a);
-            break;
-        case MME_ACT_GELU_ERF:
-            hipLaunchKernelGGL((gemm_pipe10_kernel<C, GROUP_M, MME_ACT_GELU_ERF, SPLIT>), grid, block, 0, s, a);
-            break;
+        case MME_ACT_GELU_TANH: MME_P10(MME_ACT_GELU_TANH) break;
+        case MME_ACT_QUICK_GELU: MME_P10(MME_ACT_QUICK_GELU) break;
+        case MME_ACT_GELU_ERF: MME_P10(MME_ACT_GELU_ERF) break;
         case MME_ACT_GEGLU_TANH:
-            hipLaunchKernelGGL((gemm_pipe10_kernel<C, GROUP_M, MME_ACT_GEGLU_TANH, SPLIT>), grid, block, 0, s, a);
+            hipLaunchKernelGGL((gemm_pipe10_kernel<C, GROUP_M, MME_ACT_GEGLU_TANH, SPLIT, SEAM>), grid, block, 0, s, a);
             break;
-        default:
-            hipLaunchKernelGGL((gemm_pipe10_kernel<C, GROUP_M, MME_ACT_NONE, SPLIT>), grid, block, 0, s, a);
-            break;
+        default: MME_P10(MME_ACT_NONE) break;
     }
+#undef MME_P10
     return mme_check_launch("mme_gemm");
 }
 
@@ -1726,10 +1809,21 @@ int launch_pipe8(const GemmArgs& a, hipStream_t s) {
     return mme_check_launch("mme_gemm");
 }
 
-template <class C, int GROUP_M, bool SPLIT, int PRIO = 0, bool ESWZ = true>
+template <class C, int GROUP_M, bool SPLIT, int PRIO = 0, bool ESWZ = true, bool SPEC = false>
 int launch_pipe9(const GemmArgs& a, hipStream_t s) {
     const int nbm = (a.M + C::BM - 1) / C::BM, nbn = (a.N + C::BN - 1) / C::BN;
     const dim3 grid(SPLIT ? split_tiles(nbm, a.N / C::BN) : nbm * nbn), block(C::NT);
+    if constexpr (SPEC) {  // the activation-free epilogues compiled for their operands (gemm_epilogue_wave FOLD)
+        if (a.act == MME_ACT_NONE && !(a.res && a.ln_stats)) {
+            if (a.ln_stats)
+                hipLaunchKernelGGL((gemm_pipe9_kernel<C, GROUP_M, MME_ACT_NONE, SPLIT, PRIO, ESWZ, 1>), grid, block, 0, s, a);
+            else if (a.res)
+                hipLaunchKernelGGL((gemm_pipe9_kernel<C, GROUP_M, MME_ACT_NONE, SPLIT, PRIO, ESWZ, 3>), grid, block, 0, s, a);
+            else
+                hipLaunchKernelGGL((gemm_pipe9_kernel<C, GROUP_M, MME_ACT_NONE, SPLIT, PRIO, ESWZ, 2>), grid, block, 0, s, a);
+            return mme_check_launch("mme_gemm");
+        }
+    }
     switch (a.act) {
         case MME_ACT_GELU_TANH:
             hipLaunchKernelGGL((gemm_pipe9_kernel<C, GROUP_M, MME_ACT_GELU_TANH, SPLIT, PRIO, ESWZ>), grid, block, 0, s, a);
@@ -2287,7 +2381,7 @@ inline int default_form() { return g_variant; }
 inline bool form_ok(int) { return true; }
 #else
 inline int default_form() { return -1; }
-inline bool form_ok(int v) { return v == -1 || v == 47 || v == 48 || v == 95; }
+inline bool form_ok(int v) { return v == -1 || v == 47 || v == 48 || v == 95 || v == 96 || v == 97 || v == 98 || v == 99; }
 #endif
 int gemm_dispatch(GemmArgs a, int variant, hipStream_t s);
 
@@ -2407,7 +2501,8 @@ int res_stats_entry(int variant, const void* A, int lda, const void* B, int ldb,
     hipStream_t s = as_stream(stream);
     GemmArgs a{(const bf16*)A, (const bf16*)B, Cp, (const bf16*)bias, (const bf16*)residual,
                lda, ldb, ldc, ldr, M, N, K, 0, MME_ACT_NONE, 0, 0, nullptr, nullptr, nullptr, row_part};
-    const bool fused = (variant < 0 || variant == 47 || variant == 48 || variant == 95) && ldc % 8 == 0 && ((uintptr_t)Cp & 15) == 0 && ldr % 8 == 0 &&
+    const bool fused = (variant < 0 || variant == 47 || variant == 48 || variant == 95 || variant == 96 ||
+                        variant == 97 || variant == 99) && ldc % 8 == 0 && ((uintptr_t)Cp & 15) == 0 && ldr % 8 == 0 &&
                        ((uintptr_t)residual & 15) == 0 && (long)M * N >= 1024L * 1024;
     if (!fused) {  // shapes the pipelined kernel does not take: GEMM, then the row statistics pass
         a.row_part = nullptr;
@@ -2417,6 +2512,10 @@ int res_stats_entry(int variant, const void* A, int lda, const void* B, int ldb,
     }
     if (pipe8_ok(a) && variant == 95 && N % 256 == 0)
         launch_pipe10<Pipe256, 4, false>(a, s);
+    else if (pipe8_ok(a) && variant == 97 && N % 256 == 0)
+        launch_pipe10<Pipe256, 4, false, 1>(a, s);
+    else if (pipe8_ok(a) && variant == 99)
+        N % 256 == 128 ? launch_pipe9<Pipe256, 4, true, 0, true, true>(a, s) : launch_pipe9<Pipe256, 4, false, 0, true, true>(a, s);
     else if (pipe8_ok(a) && variant != 47)  // variant 47: pipe6 (tests: pipe9 / pipe8 are bit-identical to it)
         N % 256 == 128 ? launch_pipe9<Pipe256, 4, true>(a, s) : launch_pipe9<Pipe256, 4, false>(a, s);
     else
@@ -2507,6 +2606,29 @@ int gemm_dispatch(GemmArgs a, int variant, hipStream_t s) {
                   // OpenAI-CLIP-L; profiles/r05_v6_pipe10_everywhere_ab.log): not dispatched
             if (!pipe8_ok(a) || a.N % 256 == 128) break;
             return launch_pipe10<Pipe256, 4, false>(a, s);
+        case 96:  // production dispatch with pipe10's SEAM 1 (epilogue constants loaded before the next tile's
+                  // DMA, stores left in flight across the seam) on the fc1 shapes pipe10 takes
+            if (!pipe8_ok(a) || a.N % 256 == 128 ||
+                !(a.act == MME_ACT_GELU_TANH || a.act == MME_ACT_QUICK_GELU || a.act == MME_ACT_GELU_ERF))
+                break;
+            return launch_pipe10<Pipe256, 4, false, 1>(a, s);
+        case 97:  // pipe10 SEAM 1 on every non-split epilogue (form 95 with the new seam)
+            if (!pipe8_ok(a) || a.N % 256 == 128) break;
+            return launch_pipe10<Pipe256, 4, false, 1>(a, s);
+        case 99:  // production dispatch with the epilogues compiled for their operands (gemm_epilogue_wave FOLD):
+                  // pipe10 fc1 (FOLD 1 / 2) and pipe9's activation-free GEMMs (FOLD 1 / 2 / 3)
+            if (!pipe8_ok(a) || out_f32 || ldc % 8 || ((uintptr_t)Cp & 15) || N % 8 ||
+                (residual && (ldr % 8 || ((uintptr_t)residual & 15))))
+                break;
+            if (N % 256 == 128) return launch_pipe9<Pipe256, 4, true, 0, true, true>(a, s);
+            if (a.act == MME_ACT_GELU_TANH || a.act == MME_ACT_QUICK_GELU || a.act == MME_ACT_GELU_ERF)
+                return launch_pipe10<Pipe256, 4, false, 0, true>(a, s);
+            return launch_pipe9<Pipe256, 4, false, 0, true, true>(a, s);
+        case 98:  // form 96 with SEAM 2 (the next tile's DMA between the two staging passes)
+            if (!pipe8_ok(a) || a.N % 256 == 128 ||
+                !(a.act == MME_ACT_GELU_TANH || a.act == MME_ACT_QUICK_GELU || a.act == MME_ACT_GELU_ERF))
+                break;
+            return launch_pipe10<Pipe256, 4, false, 2>(a, s);
 #ifdef MME_DEV
         case 0: return launch<BigCfg, 1>(a, s);
         case 1: return launch<BigCfg, 4>(a, s);

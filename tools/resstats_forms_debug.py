@@ -1,0 +1,46 @@
+#!/usr/bin/env python3
+"""mme_gemm_res_stats under several GEMM forms: which of output / row_part slices / row stats differ
+from pipe6 (form 47), and by how much. Usage: python tools/resstats_forms_debug.py [--forms 47,-1,95,99]"""
+import argparse
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "multimodal-embedding_amd"))
+import torch  # noqa: E402
+from mme import ops  # noqa: E402
+
+
+def main():
+    p = argparse.ArgumentParser()
+    p.add_argument("--forms", default="47,-1,95,99")
+    p.add_argument("--shapes", default="5000:3840:1280,20000:1152:1152,116935:1280:1280")
+    a = p.parse_args()
+    for sh in a.shapes.split(","):
+        M, N, K = map(int, sh.split(":"))
+        g = torch.Generator(device="cuda").manual_seed(M + N + K)
+        x = torch.randn(M, K, device="cuda", generator=g).to(torch.bfloat16)
+        w = (torch.randn(N, K, device="cuda", generator=g) * K ** -0.5).to(torch.bfloat16)
+        b = (torch.randn(N, device="cuda", generator=g) * 0.1).to(torch.bfloat16)
+        res = torch.randn(M, N, device="cuda", generator=g).to(torch.bfloat16)
+        outs = {}
+        for f in [int(v) for v in a.forms.split(",")]:
+            with ops.kernel_forms(**({} if f == -1 else {"gemm": f})):
+                sr = torch.empty(M, 2, device="cuda", dtype=torch.float32)
+                part = torch.full((M * (N // 64) * 2,), float("nan"), device="cuda", dtype=torch.float32)
+                yr = ops.gemm_res_stats(x, w, b, res, 1e-6, sr, part)
+                y = ops.gemm(x, w, b)
+            torch.cuda.synchronize()
+            outs[f] = (y, yr, sr, part.view(M, N // 64, 2))
+        ref = outs[47] if 47 in outs else next(iter(outs.values()))
+        for f, (y, yr, sr, part) in outs.items():
+            dp = (part - ref[3]).abs()
+            bad = torch.nonzero(dp.amax(-1) > 0)
+            print(f"{M}x{N}x{K} form {f}: y equal {torch.equal(y, ref[0])}, yr equal {torch.equal(yr, ref[1])}, "
+                  f"sr max diff {(sr - ref[2]).abs().max().item():.3g}, part slices differing {bad.shape[0]} "
+                  f"(nan {torch.isnan(part).any().item()}), max {dp.nan_to_num(99).max().item():.3g}, "
+                  f"first {bad[:4].tolist()}", flush=True)
+
+
+if __name__ == "__main__":
+    main()
