@@ -76,7 +76,11 @@ def parse():
                    help="mx8 encoder GEMMs (BASELINE configs[4]: DFN5B-H fp8 weights on the fp8 MFMA)")
     p.add_argument("--gemm-form", type=int, default=None,
                    help="A/B only: run every GEMM call with this libmme kernel form (mme.ops.kernel_forms; "
-                        "47 = pipe6, 95 = pipe10 on every non-split shape); reported on the line")
+                        "47 = pipe6, 93 = the run-time-branched epilogues, 95 = pipe10 on every non-split shape); "
+                        "reported on the line")
+    p.add_argument("--mx-form", type=int, default=None,
+                   help="A/B only: run every mx8 GEMM call with this libmme mx kernel form (mme.ops.kernel_forms; "
+                        "11 = mx11, 15 = mx11 with the bias loaded up front); reported on the line")
     p.add_argument("--attn-form", type=int, default=None,
                    help="A/B only: run every attention call with this libmme kernel form (mme.ops.kernel_forms; "
                         "30 + kind forces a kernel kind); reported on the line")
@@ -575,12 +579,13 @@ def main():
         # BEFORE anything touches the GPU (this parent never initialises HIP), and exit with
         # the first failing rank's status
         sys.exit(launch.spawn_ranks(args.gpus, [os.path.abspath(__file__)] + sys.argv[1:]))
-    if args.gemm_form is not None or args.attn_form is not None:  # thread-local forms (no HIP call here)
+    if args.gemm_form is not None or args.attn_form is not None or args.mx_form is not None:  # thread-local forms
         import contextlib
         from mme import ops as _ops
         _forms = contextlib.ExitStack()
         _forms.enter_context(_ops.kernel_forms(**({"gemm": args.gemm_form} if args.gemm_form is not None else {}),
-                                               **({"attention": args.attn_form} if args.attn_form is not None else {})))
+                                               **({"attention": args.attn_form} if args.attn_form is not None else {}),
+                                               **({"mx": args.mx_form} if args.mx_form is not None else {})))
     _, _, local = launch.env_rank_world()
     if args.same_device:
         local = 0
@@ -746,7 +751,8 @@ def main():
                    "image_size": spec.vision.image_size, "seq_len": spec.text.max_pos, "img_batch": args.img_batch,
                    "txt_batch": args.txt_batch, "global_batch": n, "parallelism": f"image-shard x{world}",
                    **({"gemm_form": args.gemm_form} if args.gemm_form is not None else {}),
-                   **({"attn_form": args.attn_form} if args.attn_form is not None else {})},
+                   **({"attn_form": args.attn_form} if args.attn_form is not None else {}),
+                   **({"mx_form": args.mx_form} if args.mx_form is not None else {})},
         "recall": {k: round(v, 2) for k, v in metrics.items()},
         # last timed step, device events, max over ranks; retrieval = all-gather (N > 1) + T2I / I2T /
         # I2T-Sym similarity + fused top-10 + recall counters + counter all-reduce

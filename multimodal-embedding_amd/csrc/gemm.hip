@@ -284,7 +284,7 @@ __device__ __forceinline__ void gemm_epilogue_lds(const GemmArgs& p, char* lds, 
                 const float mean = row8_sum(sum) * (1.f / 64.f);
                 float m2 = 0.f;
 #pragma unroll
-                for (int e = 0; e < 8; ++e) m2 += (xf[e] - mean) * (xf[e] - mean);
+                for (int e = 0; e < 8; ++e) m2 = __builtin_fmaf(xf[e] - mean, xf[e] - mean, m2);  // pinned: no contraction choice
                 m2 = row8_sum(m2);
                 if ((cc & 7) == 0)
                     *reinterpret_cast<float2*>(p.row_part + 2 * ((size_t)gr * (p.N >> 6) + (gc >> 6))) =
@@ -920,18 +920,9 @@ int launch_pipe6(const GemmArgs& a, hipStream_t s) {
 // SQ_LDS_BANK_CONFLICT cycles per fc1 launch (profiles/r03_v12_pmc_gemm_util_fc1.json).
 // PASSES (pipe10, round 4): the sub-tile staged and stored in PASSES row bands through a region of
 // 128 / PASSES rows per wave (2: 8 KiB per wave, 64 KiB for the block, two of the five ring units).
-struct NoHook {
-    __device__ void operator()() const {}
-};
-
-// PRE: every row and column constant of the epilogue (LayerNorm fold: rstd_r, -rstd_r mean_r, b'_n, sum w'_n;
-// else the bias) is loaded and waited for first, then hook() runs (pipe10's SEAM 1 issues the next tile's
-// DMA there), and the passes reuse the registers: no load follows the hook.
-template <class C, int ACT, bool SWZ = true, int PASSES = 1, int PRE = 0, int FOLD = 0,
-          class Hook = NoHook>
+template <class C, int ACT, bool SWZ = true, int PASSES = 1, int FOLD = 0>
 __device__ __forceinline__ void gemm_epilogue_wave(const GemmArgs& p, char* lds, f32x4 (&acc)[C::FM][C::FN], int m0,
-                                                   int n0, int wave, int wm, int wn, int g, int li, int lane,
-                                                   Hook hook = Hook{}) {
+                                                   int n0, int wave, int wm, int wn, int g, int li, int lane) {
     static_assert(C::TM == 128 && C::TN == 64 && C::FM == 8 && C::FN == 4, "per-wave epilogue: 128 x 64 wave tiles");
     static_assert(PASSES == 1 || (PASSES == 2 && SWZ), "one or two staging passes");
     // FOLD 1: LayerNorm fold, no residual; FOLD 2: bias (or none), no residual, no fold; FOLD 3: residual
@@ -977,49 +968,13 @@ __device__ __forceinline__ void gemm_epilogue_wave(const GemmArgs& p, char* lds,
             lm[i] = -st.y * st.x;
         }
     }
-    float pbv[PRE ? C::FN : 1][4], pcs[PRE ? C::FN : 1][4];
-    if constexpr (PRE) {
-#pragma unroll
-        for (int j = 0; j < C::FN; ++j) {
-#pragma unroll
-            for (int r = 0; r < 4; ++r) pbv[j][r] = pcs[j][r] = 0.f;
-            if (lnf) {
-                const int c4 = min(cn0 + j * 16 + 4 * g, p.N - 4);
-                const float4 b4 = *reinterpret_cast<const float4*>(p.ln_b + c4);
-                const float4 s4 = *reinterpret_cast<const float4*>(p.ln_cs + c4);
-                pbv[j][0] = b4.x, pbv[j][1] = b4.y, pbv[j][2] = b4.z, pbv[j][3] = b4.w;
-                pcs[j][0] = s4.x, pcs[j][1] = s4.y, pcs[j][2] = s4.z, pcs[j][3] = s4.w;
-            } else if (p.bias) {
-#pragma unroll
-                for (int r = 0; r < 4; ++r) pbv[j][r] = bf2f(p.bias[min(cn0 + j * 16 + 4 * g + r, p.N - 1)]);
-            }
-        }
-    }
-    auto preload_done = [&]() __attribute__((always_inline)) {  // every preloaded constant landed, then the hook
-        if (lnf) {
-#pragma unroll
-            for (int i = 0; i < C::FM; ++i) asm volatile("" ::"v"(lr[i]), "v"(lm[i]));
-        }
-#pragma unroll
-        for (int j = 0; j < C::FN; ++j)
-#pragma unroll
-            for (int r = 0; r < 4; ++r) asm volatile("" ::"v"(pbv[j][r]), "v"(pcs[j][r]));
-        hook();
-    };
-    if constexpr (PRE == 1) preload_done();
 #pragma unroll
     for (int ps = 0; ps < PASSES; ++ps) {
-    if constexpr (PRE == 2) {
-        if (ps == 1) preload_done();
-    }
     if constexpr (PASSES > 1) load_res(ps);
 #pragma unroll
     for (int j = 0; j < C::FN; ++j) {
         float bv[4] = {0.f, 0.f, 0.f, 0.f}, cs[4] = {0.f, 0.f, 0.f, 0.f};
-        if constexpr (PRE) {
-#pragma unroll
-            for (int r = 0; r < 4; ++r) bv[r] = pbv[j][r], cs[r] = pcs[j][r];
-        } else if (lnf) {
+        if (lnf) {
             const int c4 = min(cn0 + j * 16 + 4 * g, p.N - 4);
             const float4 b4 = *reinterpret_cast<const float4*>(p.ln_b + c4);
             const float4 s4 = *reinterpret_cast<const float4*>(p.ln_cs + c4);
@@ -1092,7 +1047,7 @@ __device__ __forceinline__ void gemm_epilogue_wave(const GemmArgs& p, char* lds,
                 const float mean = row8_sum(sum) * (1.f / 64.f);
                 float m2 = 0.f;
 #pragma unroll
-                for (int e = 0; e < 8; ++e) m2 += (xf[e] - mean) * (xf[e] - mean);
+                for (int e = 0; e < 8; ++e) m2 = __builtin_fmaf(xf[e] - mean, xf[e] - mean, m2);  // pinned: no contraction choice
                 m2 = row8_sum(m2);
                 if (cc == 0)
                     *reinterpret_cast<float2*>(p.row_part + 2 * ((size_t)gr * (p.N >> 6) + (gc >> 6))) =
@@ -1412,7 +1367,7 @@ __device__ __forceinline__ void pipe9_tile(const GemmArgs& p, char* lds, const i
     stage(sa2, true, false, 0, false);
     stage(sa1, false, false, -1, true);
     vm_wait<0>();
-    gemm_epilogue_wave<C, ACT, ESWZ, 1, 0, FOLD>(p, lds, acc, m0, n0, wave, wm, wn, g, li, lane);
+    gemm_epilogue_wave<C, ACT, ESWZ, 1, FOLD>(p, lds, acc, m0, n0, wave, wm, wn, g, li, lane);
 }
 
 // ESWZ: the conflict-free staging layout of gemm_epilogue_wave (round 4); false = pitch 144 (dev form 84)
@@ -1454,7 +1409,7 @@ __global__ __launch_bounds__(C::NT, 2) void gemm_pipe9_kernel(GemmArgs p) {
 // pipe9's do (pipe6_tile, whole LDS) with a barrier after each and a full prologue for the next.
 // Barrier counts stay equal for the two wave rows: per tile pipe9's, plus one after the epilogue.
 // ---------------------------------------------------------------------------
-template <class C, int GROUP_M, int ACT, bool LATE, bool SPLIT, int SEAM = 0, int FOLD = 0>
+template <class C, int GROUP_M, int ACT, bool LATE, bool SPLIT, int FOLD = 0>
 __device__ __forceinline__ void pipe10_run(const GemmArgs& p, char* lds, const int wave) {
     static_assert(C::BM == 256 && C::BN == 256 && C::FN == 4 && C::FM == 8 && C::NW == 8, "pipe10: 256 x 256, 8 waves");
     constexpr int UNIT = 32768;
@@ -1613,47 +1568,20 @@ __device__ __forceinline__ void pipe10_run(const GemmArgs& p, char* lds, const i
         const bool has_next = vn < ntiles;
         const bool split1 = has_next ? coords(vn, m1, n1) : false;
         const bool prime = has_next && !split1;
-        if constexpr (SEAM >= 1) {
-            // SEAM 1: the epilogue's row / column constants are loaded and waited for BEFORE the next tile's
-            // DMA is issued (gemm_epilogue_wave's PRE hook): hipcc cannot see the asm DMA, so a wait it places
-            // for a load issued after the DMA counts the DMA too (vmcnt retires in issue order) and holds the
-            // epilogue's first arithmetic until the next tile's three units have landed; and the second
-            // staging pass re-loaded its column constants behind the first pass's stores. The stores are then
-            // the only vector memory operations younger than the DMA, so the wait that retires the DMA leaves
-            // them in flight (vmcnt(16): a full interior wave tile issues 16; a clipped edge tile waits for all).
+        if (prime) {  // the next tile's A0 B0 A1 under this tile's epilogue (offsets recomputed after it:
+                      // not held live across the epilogue)
+            set_off(m1, n1);
+            dma4(lw + 0 * UNIT, offA, rA, 0);
+            dma4(lw + 1 * UNIT, offB, rB, 0);
+            dma4(lw + 2 * UNIT, offA, rA, 128);
+        }
+        {  // the lane id from a volatile asm: the epilogue's lane-derived addresses are recomputed per
+           // tile instead of being hoisted to kernel entry and spilled around the tile loop
             int ln;
             asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(ln));
-            auto dma_next = [&]() __attribute__((always_inline)) {
-                if (prime) {
-                    set_off(m1, n1);
-                    dma4(lw + 0 * UNIT, offA, rA, 0);
-                    dma4(lw + 1 * UNIT, offB, rB, 0);
-                    dma4(lw + 2 * UNIT, offA, rA, 128);
-                }
-            };
-            gemm_epilogue_wave<C, ACT, true, 2, SEAM, FOLD>(p, lds + 3 * UNIT, acc, m0, n0, wave, wm, wn, ln >> 4, ln & 15,
-                                                      ln, dma_next);
-            if (m0 + wm * C::TM + C::TM <= p.M && n0 + wn * C::TN + C::TN <= p.N)
-                vm_wait<SEAM == 1 ? 16 : 8>();  // own pieces of units 0-2 landed; this wave's 16 stores may still be in flight
-            else
-                vm_wait<0>();
-        } else {
-            if (prime) {  // the next tile's A0 B0 A1 under this tile's epilogue (offsets recomputed after it:
-                          // not held live across the epilogue)
-                set_off(m1, n1);
-                dma4(lw + 0 * UNIT, offA, rA, 0);
-                dma4(lw + 1 * UNIT, offB, rB, 0);
-                dma4(lw + 2 * UNIT, offA, rA, 128);
-            }
-            {  // the lane id from a volatile asm: the epilogue's lane-derived addresses are recomputed per
-               // tile instead of being hoisted to kernel entry and spilled around the tile loop
-                int ln;
-                asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(ln));
-                gemm_epilogue_wave<C, ACT, true, 2, 0, FOLD>(p, lds + 3 * UNIT, acc, m0, n0, wave, wm, wn, ln >> 4, ln & 15,
-                                                    ln);
-            }
-            vm_wait<0>();  // own pieces of units 0-2 landed (and this wave's stores retired)
+            gemm_epilogue_wave<C, ACT, true, 2, FOLD>(p, lds + 3 * UNIT, acc, m0, n0, wave, wm, wn, ln >> 4, ln & 15, ln);
         }
+        vm_wait<0>();  // own pieces of units 0-2 landed (and this wave's stores retired)
         __builtin_amdgcn_s_barrier();  // staging reads of every wave done: slots 3-4 free
         if (!has_next) break;
         v = vn;
@@ -1671,15 +1599,15 @@ __device__ __forceinline__ void pipe10_run(const GemmArgs& p, char* lds, const i
     }
 }
 
-template <class C, int GROUP_M, int ACT, bool SPLIT, int SEAM = 0, int FOLD = 0>
+template <class C, int GROUP_M, int ACT, bool SPLIT, int FOLD = 0>
 __global__ __launch_bounds__(C::NT, 2) void gemm_pipe10_kernel(GemmArgs p) {
     __shared__ __attribute__((aligned(16))) char lds[5 * 32768];
     static_assert(Pipe512x128::LDS <= 5 * 32768, "pipe10 LDS");
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     if (wave >= C::NW / 2)
-        pipe10_run<C, GROUP_M, ACT, true, SPLIT, SEAM, FOLD>(p, lds, wave);
+        pipe10_run<C, GROUP_M, ACT, true, SPLIT, FOLD>(p, lds, wave);
     else
-        pipe10_run<C, GROUP_M, ACT, false, SPLIT, SEAM, FOLD>(p, lds, wave);
+        pipe10_run<C, GROUP_M, ACT, false, SPLIT, FOLD>(p, lds, wave);
 }
 
 // Workgroups of a persistent GEMM grid: one per CU (160 KiB of LDS each), rounded down to a multiple of
@@ -1697,7 +1625,7 @@ int persistent_grid(int ntiles) {
     return std::min(ntiles, cus[dev]);
 }
 
-template <class C, int GROUP_M, bool SPLIT, int SEAM = 0, bool SPEC = false>
+template <class C, int GROUP_M, bool SPLIT, bool SPEC = true>
 int launch_pipe10(const GemmArgs& a, hipStream_t s) {
     const int nbm = (a.M + C::BM - 1) / C::BM, nbn = (a.N + C::BN - 1) / C::BN;
     const int ntiles = SPLIT ? split_tiles(nbm, a.N / C::BN) : nbm * nbn;
@@ -1706,17 +1634,17 @@ int launch_pipe10(const GemmArgs& a, hipStream_t s) {
     const int fold = !SPEC || a.res ? 0 : a.ln_stats ? 1 : 2;
 #define MME_P10(ACT_)                                                                                          \
     if (fold == 1)                                                                                            \
-        hipLaunchKernelGGL((gemm_pipe10_kernel<C, GROUP_M, ACT_, SPLIT, SEAM, SPEC ? 1 : 0>), grid, block, 0, s, a); \
+        hipLaunchKernelGGL((gemm_pipe10_kernel<C, GROUP_M, ACT_, SPLIT, SPEC ? 1 : 0>), grid, block, 0, s, a); \
     else if (fold == 2)                                                                                       \
-        hipLaunchKernelGGL((gemm_pipe10_kernel<C, GROUP_M, ACT_, SPLIT, SEAM, SPEC ? 2 : 0>), grid, block, 0, s, a); \
+        hipLaunchKernelGGL((gemm_pipe10_kernel<C, GROUP_M, ACT_, SPLIT, SPEC ? 2 : 0>), grid, block, 0, s, a); \
     else                                                                                                      \
-        hipLaunchKernelGGL((gemm_pipe10_kernel<C, GROUP_M, ACT_, SPLIT, SEAM, 0>), grid, block, 0, s, a);
+        hipLaunchKernelGGL((gemm_pipe10_kernel<C, GROUP_M, ACT_, SPLIT, 0>), grid, block, 0, s, a);
     switch (a.act) {
         case MME_ACT_GELU_TANH: MME_P10(MME_ACT_GELU_TANH) break;
         case MME_ACT_QUICK_GELU: MME_P10(MME_ACT_QUICK_GELU) break;
         case MME_ACT_GELU_ERF: MME_P10(MME_ACT_GELU_ERF) break;
         case MME_ACT_GEGLU_TANH:
-            hipLaunchKernelGGL((gemm_pipe10_kernel<C, GROUP_M, MME_ACT_GEGLU_TANH, SPLIT, SEAM>), grid, block, 0, s, a);
+            hipLaunchKernelGGL((gemm_pipe10_kernel<C, GROUP_M, MME_ACT_GEGLU_TANH, SPLIT>), grid, block, 0, s, a);
             break;
         default: MME_P10(MME_ACT_NONE) break;
     }
@@ -1809,7 +1737,7 @@ int launch_pipe8(const GemmArgs& a, hipStream_t s) {
     return mme_check_launch("mme_gemm");
 }
 
-template <class C, int GROUP_M, bool SPLIT, int PRIO = 0, bool ESWZ = true, bool SPEC = false>
+template <class C, int GROUP_M, bool SPLIT, int PRIO = 0, bool ESWZ = true, bool SPEC = true>
 int launch_pipe9(const GemmArgs& a, hipStream_t s) {
     const int nbm = (a.M + C::BM - 1) / C::BM, nbn = (a.N + C::BN - 1) / C::BN;
     const dim3 grid(SPLIT ? split_tiles(nbm, a.N / C::BN) : nbm * nbn), block(C::NT);
@@ -2381,7 +2309,7 @@ inline int default_form() { return g_variant; }
 inline bool form_ok(int) { return true; }
 #else
 inline int default_form() { return -1; }
-inline bool form_ok(int v) { return v == -1 || v == 47 || v == 48 || v == 95 || v == 96 || v == 97 || v == 98 || v == 99; }
+inline bool form_ok(int v) { return v == -1 || v == 47 || v == 48 || v == 93 || v == 95; }
 #endif
 int gemm_dispatch(GemmArgs a, int variant, hipStream_t s);
 
@@ -2501,8 +2429,8 @@ int res_stats_entry(int variant, const void* A, int lda, const void* B, int ldb,
     hipStream_t s = as_stream(stream);
     GemmArgs a{(const bf16*)A, (const bf16*)B, Cp, (const bf16*)bias, (const bf16*)residual,
                lda, ldb, ldc, ldr, M, N, K, 0, MME_ACT_NONE, 0, 0, nullptr, nullptr, nullptr, row_part};
-    const bool fused = (variant < 0 || variant == 47 || variant == 48 || variant == 95 || variant == 96 ||
-                        variant == 97 || variant == 99) && ldc % 8 == 0 && ((uintptr_t)Cp & 15) == 0 && ldr % 8 == 0 &&
+    const bool fused = (variant < 0 || variant == 47 || variant == 48 || variant == 93 ||
+                        variant == 95) && ldc % 8 == 0 && ((uintptr_t)Cp & 15) == 0 && ldr % 8 == 0 &&
                        ((uintptr_t)residual & 15) == 0 && (long)M * N >= 1024L * 1024;
     if (!fused) {  // shapes the pipelined kernel does not take: GEMM, then the row statistics pass
         a.row_part = nullptr;
@@ -2512,10 +2440,9 @@ int res_stats_entry(int variant, const void* A, int lda, const void* B, int ldb,
     }
     if (pipe8_ok(a) && variant == 95 && N % 256 == 0)
         launch_pipe10<Pipe256, 4, false>(a, s);
-    else if (pipe8_ok(a) && variant == 97 && N % 256 == 0)
-        launch_pipe10<Pipe256, 4, false, 1>(a, s);
-    else if (pipe8_ok(a) && variant == 99)
-        N % 256 == 128 ? launch_pipe9<Pipe256, 4, true, 0, true, true>(a, s) : launch_pipe9<Pipe256, 4, false, 0, true, true>(a, s);
+    else if (pipe8_ok(a) && variant == 93)  // the epilogue branching on its operands at run time (A/B)
+        N % 256 == 128 ? launch_pipe9<Pipe256, 4, true, 0, true, false>(a, s)
+                       : launch_pipe9<Pipe256, 4, false, 0, true, false>(a, s);
     else if (pipe8_ok(a) && variant != 47)  // variant 47: pipe6 (tests: pipe9 / pipe8 are bit-identical to it)
         N % 256 == 128 ? launch_pipe9<Pipe256, 4, true>(a, s) : launch_pipe9<Pipe256, 4, false>(a, s);
     else
@@ -2606,29 +2533,16 @@ int gemm_dispatch(GemmArgs a, int variant, hipStream_t s) {
                   // OpenAI-CLIP-L; profiles/r05_v6_pipe10_everywhere_ab.log): not dispatched
             if (!pipe8_ok(a) || a.N % 256 == 128) break;
             return launch_pipe10<Pipe256, 4, false>(a, s);
-        case 96:  // production dispatch with pipe10's SEAM 1 (epilogue constants loaded before the next tile's
-                  // DMA, stores left in flight across the seam) on the fc1 shapes pipe10 takes
-            if (!pipe8_ok(a) || a.N % 256 == 128 ||
-                !(a.act == MME_ACT_GELU_TANH || a.act == MME_ACT_QUICK_GELU || a.act == MME_ACT_GELU_ERF))
-                break;
-            return launch_pipe10<Pipe256, 4, false, 1>(a, s);
-        case 97:  // pipe10 SEAM 1 on every non-split epilogue (form 95 with the new seam)
-            if (!pipe8_ok(a) || a.N % 256 == 128) break;
-            return launch_pipe10<Pipe256, 4, false, 1>(a, s);
-        case 99:  // production dispatch with the epilogues compiled for their operands (gemm_epilogue_wave FOLD):
-                  // pipe10 fc1 (FOLD 1 / 2) and pipe9's activation-free GEMMs (FOLD 1 / 2 / 3)
+        case 93:  // the dispatch before round 5's compiled epilogues: every pipe9 / pipe10 epilogue branching on
+                  // its operands at run time (bit-identical; fc1 1 118 -> 1 198 TF/s, SigLIP-400M job
+                  // 1 088-1 091 -> 1 123 img/s with them, profiles/r05_v19_epilogue_fold_ab.log)
             if (!pipe8_ok(a) || out_f32 || ldc % 8 || ((uintptr_t)Cp & 15) || N % 8 ||
                 (residual && (ldr % 8 || ((uintptr_t)residual & 15))))
                 break;
-            if (N % 256 == 128) return launch_pipe9<Pipe256, 4, true, 0, true, true>(a, s);
+            if (N % 256 == 128) return launch_pipe9<Pipe256, 4, true, 0, true, false>(a, s);
             if (a.act == MME_ACT_GELU_TANH || a.act == MME_ACT_QUICK_GELU || a.act == MME_ACT_GELU_ERF)
-                return launch_pipe10<Pipe256, 4, false, 0, true>(a, s);
-            return launch_pipe9<Pipe256, 4, false, 0, true, true>(a, s);
-        case 98:  // form 96 with SEAM 2 (the next tile's DMA between the two staging passes)
-            if (!pipe8_ok(a) || a.N % 256 == 128 ||
-                !(a.act == MME_ACT_GELU_TANH || a.act == MME_ACT_QUICK_GELU || a.act == MME_ACT_GELU_ERF))
-                break;
-            return launch_pipe10<Pipe256, 4, false, 2>(a, s);
+                return launch_pipe10<Pipe256, 4, false, false>(a, s);
+            return launch_pipe9<Pipe256, 4, false, 0, true, false>(a, s);
 #ifdef MME_DEV
         case 0: return launch<BigCfg, 1>(a, s);
         case 1: return launch<BigCfg, 4>(a, s);
@@ -2761,7 +2675,8 @@ int gemm_dispatch(GemmArgs a, int variant, hipStream_t s) {
         // + gelu_tanh) 1 118 -> 1 135 TF/s, quick_gelu / bias + gelu fc1 +1.0 % (profiles/r04_v10_pipe10_ab.log);
         // the split grid stays on pipe9 (its 512 x 128 tiles inlined into pipe10's loop spill), and so do
         // the epilogues pipe10 was not measured with; round 5: gelu_erf on pipe10 too (the branch-free
-        // erfc form of common.h took it from 22 spilled VGPRs to pipe10's usual 2)
+        // erfc form of common.h took it from 22 spilled VGPRs to pipe10's usual 2), and every epilogue
+        // compiled for its operand set (gemm_epilogue_wave / gemm_epilogue_lds FOLD; form 93 = before)
         if (pipe8_ok(a)) {
             if (N % 256 == 128) return launch_pipe9<Pipe256, 4, true>(a, s);
             if (a.act == MME_ACT_GELU_TANH || a.act == MME_ACT_QUICK_GELU || a.act == MME_ACT_GELU_ERF)

@@ -245,7 +245,10 @@ constexpr int MXW_PITCH = 144, MXW_LDS = 8 * 128 * MXW_PITCH;
 // from interleaving (and holding live) all 32 quads' activations at once.
 // PASSES (mx12, round 5): the sub-tile staged and stored in PASSES row bands through a region of
 // 128 / PASSES rows per wave (2: 8 KiB per wave, two of the five ring units), as pipe10's epilogue.
-template <int ACT, bool SWZ = true, bool SB = false, int PASSES = 1>
+// BPRE (mx form 15, round 5): the wave's 32 bias values loaded up front as eight 8-B loads (one wait)
+// instead of four 2-B loads and a wait per column quad (needs N % 4 == 0 and an 8-B aligned bias:
+// a quad's columns are then all in range or all past N, so clamping the quad start is exact).
+template <int ACT, bool SWZ = true, bool SB = false, int PASSES = 1, bool BPRE = false>
 __device__ __forceinline__ void mx_epilogue_wave(const MxArgs& p, char* lds, f32x16 (&acc)[4][2], int m0, int n0,
                                                  int wave, int lane) {
     static_assert(PASSES == 1 || (PASSES == 2 && SWZ), "one or two staging passes");
@@ -256,6 +259,14 @@ __device__ __forceinline__ void mx_epilogue_wave(const MxArgs& p, char* lds, f32
     char* reg = lds + wave * (BAND * MX9_PITCH);
     const int rm0 = m0 + wm * TM, cn0 = n0 + wn * TN;
     const int rr = lane >> 3, cc = lane & 7;
+    uint2 bq[BPRE ? 8 : 1];
+    if constexpr (BPRE) {
+#pragma unroll
+        for (int jq = 0; jq < 8; ++jq) {
+            const int nl = (jq >> 2) * 32 + 8 * (jq & 3) + 4 * h;
+            bq[jq] = p.bias ? *reinterpret_cast<const uint2*>(p.bias + min(cn0 + nl, p.N - 4)) : uint2{0u, 0u};
+        }
+    }
 #pragma unroll
     for (int ps = 0; ps < PASSES; ++ps) {
     if (ps > 0) lgkm_wait<0>();  // the previous band's read-back done before its region is rewritten
@@ -265,7 +276,11 @@ __device__ __forceinline__ void mx_epilogue_wave(const MxArgs& p, char* lds, f32
         for (int qd = 0; qd < 4; ++qd) {
             const int nl = j * 32 + 8 * qd + 4 * h;
             float bv[4] = {0.f, 0.f, 0.f, 0.f};
-            if (p.bias) {
+            if constexpr (BPRE) {  // bf16 -> f32: the 16 bits as the high half
+                const uint2 w = bq[j * 4 + qd];
+                bv[0] = __uint_as_float(w.x << 16), bv[1] = __uint_as_float(w.x & 0xffff0000u);
+                bv[2] = __uint_as_float(w.y << 16), bv[3] = __uint_as_float(w.y & 0xffff0000u);
+            } else if (p.bias) {
 #pragma unroll
                 for (int r = 0; r < 4; ++r) bv[r] = bf2f(p.bias[min(cn0 + nl + r, p.N - 1)]);
             }
@@ -770,7 +785,7 @@ __device__ __forceinline__ void mx11_mfma(f32x16& acc, const bf16x8 (&a)[2], con
     acc = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(bo, ao, acc, 0, 0, J, (int)sb, I, (int)sa);
 }
 
-template <int ACT, bool LATE>
+template <int ACT, bool LATE, bool BPRE = false>
 __device__ __forceinline__ void mx11_tile(const MxArgs& p, char* lds, const int m0, const int n0, const int wave) {
     constexpr int UNIT = 32768;
     const int lane = threadIdx.x & 63;
@@ -942,10 +957,10 @@ __device__ __forceinline__ void mx11_tile(const MxArgs& p, char* lds, const int 
         for (int j = 0; j < 2; ++j) asm volatile("" : "+v"(acc[i][j]));
     // no LDS hazard: every wave's last fragment reads precede the barrier closing the late row's
     // last memory phase, which the early row passes before it writes its epilogue region
-    mx_epilogue_wave<ACT, true, true>(p, lds, acc, m0, n0, wave, lane);
+    mx_epilogue_wave<ACT, true, true, 1, BPRE>(p, lds, acc, m0, n0, wave, lane);
 }
 
-template <int GROUP_M, int ACT>
+template <int GROUP_M, int ACT, bool BPRE = false>
 __global__ __launch_bounds__(512, 2) void gemm_mx11_kernel(MxArgs p) {
     __shared__ __attribute__((aligned(16))) char lds[5 * 32768];
     const int nbm = (p.M + 255) / 256, nbn = (p.N + 255) / 256;
@@ -954,26 +969,26 @@ __global__ __launch_bounds__(512, 2) void gemm_mx11_kernel(MxArgs p) {
     tile_coords<GROUP_M>(tile, nbm, nbn, bm, bn);
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     if (wave >= 4)
-        mx11_tile<ACT, true>(p, lds, bm * 256, bn * 256, wave);
+        mx11_tile<ACT, true, BPRE>(p, lds, bm * 256, bn * 256, wave);
     else
-        mx11_tile<ACT, false>(p, lds, bm * 256, bn * 256, wave);
+        mx11_tile<ACT, false, BPRE>(p, lds, bm * 256, bn * 256, wave);
 }
 
-template <int GROUP_M>
+template <int GROUP_M, bool BPRE = false>
 int launch_mx11(const MxArgs& a, hipStream_t s) {
     const dim3 grid(((a.M + 255) / 256) * ((a.N + 255) / 256)), block(512);
     switch (a.act) {
         case MME_ACT_GELU_TANH:
-            hipLaunchKernelGGL((gemm_mx11_kernel<GROUP_M, MME_ACT_GELU_TANH>), grid, block, 0, s, a);
+            hipLaunchKernelGGL((gemm_mx11_kernel<GROUP_M, MME_ACT_GELU_TANH, BPRE>), grid, block, 0, s, a);
             break;
         case MME_ACT_QUICK_GELU:
-            hipLaunchKernelGGL((gemm_mx11_kernel<GROUP_M, MME_ACT_QUICK_GELU>), grid, block, 0, s, a);
+            hipLaunchKernelGGL((gemm_mx11_kernel<GROUP_M, MME_ACT_QUICK_GELU, BPRE>), grid, block, 0, s, a);
             break;
         case MME_ACT_GELU_ERF:
-            hipLaunchKernelGGL((gemm_mx11_kernel<GROUP_M, MME_ACT_GELU_ERF>), grid, block, 0, s, a);
+            hipLaunchKernelGGL((gemm_mx11_kernel<GROUP_M, MME_ACT_GELU_ERF, BPRE>), grid, block, 0, s, a);
             break;
         default:
-            hipLaunchKernelGGL((gemm_mx11_kernel<GROUP_M, MME_ACT_NONE>), grid, block, 0, s, a);
+            hipLaunchKernelGGL((gemm_mx11_kernel<GROUP_M, MME_ACT_NONE, BPRE>), grid, block, 0, s, a);
             break;
     }
     return mme_check_launch("mme_gemm_mx");
@@ -1442,9 +1457,9 @@ inline int mx_default_form() { return -1; }
 #endif
 inline bool mx_form_ok(int v) {
 #ifdef MME_DEV
-    return v == -1 || v == 0 || v == 2 || v == 3 || v == 4 || v == 9 || v == 10 || v == 11 || v == 12 || v == 14;
+    return v == -1 || v == 0 || v == 2 || v == 3 || v == 4 || v == 9 || v == 10 || v == 11 || v == 12 || v == 14 || v == 15;
 #else
-    return v == -1 || v == 0 || v == 2 || v == 3 || v == 10 || v == 11 || v == 12 || v == 14;
+    return v == -1 || v == 0 || v == 2 || v == 3 || v == 10 || v == 11 || v == 12 || v == 14 || v == 15;
 #endif
 }
 
@@ -1585,6 +1600,8 @@ int gemm_mx_entry(int form, const void* A, int lda, const void* sa, int sa_rows,
                          (size_t)(K / 32) * (sa_rows > sb_rows ? sa_rows : sb_rows) < (1ull << 32);
     if (form == 12 && mx11_ok) return launch_mx12<4>(a, as_stream(stream));
     if (form == 14 && mx11_ok) return launch_mx12<4, 2>(a, as_stream(stream));
+    if (form == 15 && mx11_ok && N % 4 == 0 && ((uintptr_t)bias & 7) == 0)
+        return launch_mx11<4, true>(a, as_stream(stream));
     if (form != 10 && mx11_ok) return launch_mx11<4>(a, as_stream(stream));
     return launch_mx10<4>(a, as_stream(stream));
 }

@@ -527,11 +527,12 @@ def test_gemm_dispatched_fc1_bit_identical_to_pipe6(cuda, M, N, K, act):
 @pytest.mark.parametrize("M,N,K", [(116935, 1280, 1280), (116935, 1280, 5120), (5000, 3840, 1280), (300, 1024, 1024),
                                    (20000, 1152, 1152), (20000, 3456, 1152)])
 def test_gemm_form95_bit_identical_to_pipe6(cuda, M, N, K):
-    """Form 95 (pipe10, the persistent GEMM, on every non-split epilogue: bias, residual + the next
-    LayerNorm's row statistics, LayerNorm fold), form 97 (the same with SEAM 1) and form 99 (the
-    epilogues compiled for their operands, gemm_epilogue_wave FOLD) against form 47 (pipe6):
-    bit-identical outputs and statistics at ViT-H / CLIP shapes (whole 256-column tiles), SigLIP's
-    split grid (N = 256 k + 128), ragged M, fewer tiles than CUs."""
+    """The production dispatch (pipe9 / pipe10 with every epilogue compiled for its operand set:
+    bias, residual + the next LayerNorm's row statistics, LayerNorm fold), form 93 (the same kernels
+    branching on their operands at run time) and form 95 (pipe10, the persistent GEMM, on every
+    non-split epilogue) against form 47 (pipe6): bit-identical outputs and row statistics at ViT-H /
+    CLIP shapes (whole 256-column tiles), SigLIP's split grid (N = 256 k + 128), ragged M, fewer tiles
+    than CUs."""
     g = torch.Generator(device="cuda").manual_seed(M + N + K)
     x = rnd(M, K, gen=g)
     w = rnd(N, K, scale=K ** -0.5, gen=g)
@@ -543,8 +544,8 @@ def test_gemm_form95_bit_identical_to_pipe6(cuda, M, N, K):
     fold = K <= 2048  # the LayerNorm fold precedes the qkv / fc1 GEMMs (K = the model width)
     st = ops.rowstats(x, 1e-6, d=K) if fold else None
     outs = []
-    for form in (47, 95, 97, 99):
-        with ops.kernel_forms(gemm=form):
+    for form in (47, -1, 93, 95):
+        with ops.kernel_forms(**({} if form == -1 else {"gemm": form})):
             y = ops.gemm(x, w, b)
             yl = ops.gemm_lnfold(x, f, st, act=0) if fold else y
             sr = torch.empty(M, 2, device="cuda", dtype=torch.float32)
@@ -552,19 +553,17 @@ def test_gemm_form95_bit_identical_to_pipe6(cuda, M, N, K):
             yr = ops.gemm_res_stats(x, w, b, res, 1e-6, sr, part)
             outs.append((y, yl, yr, sr))
         torch.cuda.synchronize()
-    for form, o in zip((95, 97, 99), outs[1:]):
+    for form, o in zip((-1, 93, 95), outs[1:]):
         for a_, b_ in zip(outs[0], o):
             assert torch.equal(a_, b_), f"form {form} differs from pipe6 ({M}x{N}x{K})"
 
 
 @pytest.mark.parametrize("M,N,K", [(116935, 5120, 1280), (60001, 4352, 1152), (2000, 1024, 1024), (4100, 768, 512)])
-def test_gemm_pipe10_seams_bit_identical(cuda, M, N, K):
-    """pipe10's seams at the fc1 shapes it is dispatched on: SEAM 1 (form 96: the epilogue's constants
-    loaded before the next tile's DMA, the stores left in flight across the seam) and SEAM 2 (form 98:
-    the DMA between the two staging passes) against pipe6 (form 47) and the production dispatch, for
-    every fc1 activation with the LayerNorm fold and with a bias; form 99: the production seam with
-    the epilogue compiled for its operands (FOLD 1 / 2). Ragged M (clipped edge tiles wait for every
-    store), fewer tiles than CUs; M * N >= 1M throughout (smaller shapes take the generic kernel)."""
+def test_gemm_fc1_compiled_epilogues_bit_identical(cuda, M, N, K):
+    """The fc1 GEMMs as dispatched (pipe10, the epilogue compiled for its operand set: FOLD 1 LayerNorm
+    fold, FOLD 2 bias) against pipe6 (form 47) and the run-time-branched epilogue (form 93), for every
+    fc1 activation: bit-identical. Ragged M, fewer tiles than CUs; M * N >= 1M throughout (smaller
+    shapes take the generic kernel)."""
     g = torch.Generator(device="cuda").manual_seed(M + N + K + 1)
     x = rnd(M, K, gen=g)
     w = rnd(N, K, scale=K ** -0.5, gen=g)
@@ -575,11 +574,11 @@ def test_gemm_pipe10_seams_bit_identical(cuda, M, N, K):
     st = ops.rowstats(x, 1e-6, d=K)
     for act in (_lib.ACT_GELU_TANH, _lib.ACT_QUICK_GELU, _lib.ACT_GELU_ERF):
         outs = []
-        for form in (47, -1, 96, 98, 99):
+        for form in (47, -1, 93):
             with ops.kernel_forms(**({} if form == -1 else {"gemm": form})):
                 outs.append((ops.gemm_lnfold(x, f, st, act=act), ops.gemm(x, w, b, act=act)))
         torch.cuda.synchronize()
-        for form, o in zip((-1, 96, 98, 99), outs[1:]):
+        for form, o in zip((-1, 93), outs[1:]):
             for a_, b_ in zip(outs[0], o):
                 assert torch.equal(a_, b_), f"form {form} act {act} differs from pipe6 ({M}x{N}x{K})"
 

@@ -13,7 +13,7 @@ timeout -k 10 500 python -u -m pytest -q -s --timeout 400 --timeout-method threa
 rc=$?; tail -2 ${P}_pytest.log; [ $rc -ne 0 ] && [ $rc -ne 1 ] && exit $rc  # 1 = a bit-identity assertion: timing still informative
 for e in gelu res none; do
 V=-1,99,-1,99; [ $e = gelu ] && V=-1,99,96,-1,99,96
-timeout -k 10 200 python -u tools/gemm_bench.py --shapes qkv,o_proj,fc1,fc2 --epi $e --variants $V >> ${P}_gemm.log 2>&1 || exit 1
+timeout -k 10 200 python -u tools/gemm_bench.py --shapes qkv,o_proj,fc1,fc2 --epi $e --variants=$V >> ${P}_gemm.log 2>&1 || exit 1
 done
 cat ${P}_gemm.log
 for i in 1 2; do
