@@ -1630,8 +1630,9 @@ int launch_pipe10(const GemmArgs& a, hipStream_t s) {
     const int nbm = (a.M + C::BM - 1) / C::BM, nbn = (a.N + C::BN - 1) / C::BN;
     const int ntiles = SPLIT ? split_tiles(nbm, a.N / C::BN) : nbm * nbn;
     const dim3 grid(persistent_grid(ntiles)), block(C::NT);
-    // SPEC: the fc1 epilogues compiled for their operands (FOLD 1: LayerNorm fold; FOLD 2: bias), no residual
-    const int fold = !SPEC || a.res ? 0 : a.ln_stats ? 1 : 2;
+    // SPEC: the epilogue compiled for its operands (FOLD 1: LayerNorm fold; FOLD 2: bias; FOLD 3: residual,
+    // activation-free only)
+    const int fold = !SPEC ? 0 : a.res ? (a.ln_stats || a.act != MME_ACT_NONE ? 0 : 3) : a.ln_stats ? 1 : 2;
 #define MME_P10(ACT_)                                                                                          \
     if (fold == 1)                                                                                            \
         hipLaunchKernelGGL((gemm_pipe10_kernel<C, GROUP_M, ACT_, SPLIT, SPEC ? 1 : 0>), grid, block, 0, s, a); \
@@ -1639,6 +1640,10 @@ int launch_pipe10(const GemmArgs& a, hipStream_t s) {
         hipLaunchKernelGGL((gemm_pipe10_kernel<C, GROUP_M, ACT_, SPLIT, SPEC ? 2 : 0>), grid, block, 0, s, a); \
     else                                                                                                      \
         hipLaunchKernelGGL((gemm_pipe10_kernel<C, GROUP_M, ACT_, SPLIT, 0>), grid, block, 0, s, a);
+    if (fold == 3) {
+        hipLaunchKernelGGL((gemm_pipe10_kernel<C, GROUP_M, MME_ACT_NONE, SPLIT, 3>), grid, block, 0, s, a);
+        return mme_check_launch("mme_gemm");
+    }
     switch (a.act) {
         case MME_ACT_GELU_TANH: MME_P10(MME_ACT_GELU_TANH) break;
         case MME_ACT_QUICK_GELU: MME_P10(MME_ACT_QUICK_GELU) break;

@@ -1600,7 +1600,9 @@ int gemm_mx_entry(int form, const void* A, int lda, const void* sa, int sa_rows,
                          (size_t)(K / 32) * (sa_rows > sb_rows ? sa_rows : sb_rows) < (1ull << 32);
     if (form == 12 && mx11_ok) return launch_mx12<4>(a, as_stream(stream));
     if (form == 14 && mx11_ok) return launch_mx12<4, 2>(a, as_stream(stream));
-    if (form == 15 && mx11_ok && N % 4 == 0 && ((uintptr_t)bias & 7) == 0)
+    // round 5: the bias loaded up front (form 15, production where N % 4 == 0 and the bias is 8-B aligned):
+    // DFN5B-H fp8 job 1 185-1 187 -> 1 203 img/s, bit-identical (profiles/r05_v20_mx15_ab.log); form 11 = without
+    if (form != 10 && form != 11 && mx11_ok && N % 4 == 0 && ((uintptr_t)bias & 7) == 0)
         return launch_mx11<4, true>(a, as_stream(stream));
     if (form != 10 && mx11_ok) return launch_mx11<4>(a, as_stream(stream));
     return launch_mx10<4>(a, as_stream(stream));

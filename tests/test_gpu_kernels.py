@@ -554,6 +554,8 @@ def test_gemm_form95_bit_identical_to_pipe6(cuda, M, N, K):
             outs.append((y, yl, yr, sr))
         torch.cuda.synchronize()
     for form, o in zip((-1, 93, 95), outs[1:]):
+        if form == -1 and M * N < 1024 * 1024:
+            continue  # production takes the generic kernel below 1M outputs
         for a_, b_ in zip(outs[0], o):
             assert torch.equal(a_, b_), f"form {form} differs from pipe6 ({M}x{N}x{K})"
 
