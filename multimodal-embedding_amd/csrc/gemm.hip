@@ -2535,7 +2535,8 @@ int gemm_dispatch(GemmArgs a, int variant, hipStream_t s) {
             return launch_pipe6<Pipe256, 4, 1>(a, s);
         case 95:  // pipe10 on every non-split epilogue (bias, residual, LayerNorm fold, activations); bit-identical
                   // to pipe6, but the jobs measured 0.2-0.5 % slower than pipe10 on fc1 only (LAION-CLIP-H, DFN5B-H,
-                  // OpenAI-CLIP-L; profiles/r05_v6_pipe10_everywhere_ab.log): not dispatched
+                  // OpenAI-CLIP-L; profiles/r05_v6_pipe10_everywhere_ab.log), and again 0.2-0.6 % slower with the
+                  // compiled epilogues (profiles/r05_v21_pipe10_everywhere_compiled_ab.log): not dispatched
             if (!pipe8_ok(a) || a.N % 256 == 128) break;
             return launch_pipe10<Pipe256, 4, false>(a, s);
         case 93:  // the dispatch before round 5's compiled epilogues: every pipe9 / pipe10 epilogue branching on
