@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """mme_gemm_res_stats under several GEMM forms: which of output / row_part slices / row stats differ
-from pipe6 (form 47), and by how much. Usage: python tools/resstats_forms_debug.py [--forms 47,-1,95,99]"""
+from pipe6 (form 47), and by how much. Usage: python tools/resstats_forms_debug.py [--forms 47,-1,93,95]"""
 import argparse
 import os
 import sys
@@ -13,7 +13,7 @@ from mme import ops  # noqa: E402
 
 def main():
     p = argparse.ArgumentParser()
-    p.add_argument("--forms", default="47,-1,95,99")
+    p.add_argument("--forms", default="47,-1,93,95")
     p.add_argument("--shapes", default="5000:3840:1280,20000:1152:1152,116935:1280:1280")
     a = p.parse_args()
     for sh in a.shapes.split(","):
