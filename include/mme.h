@@ -152,10 +152,11 @@ int mme_attention(const void* qkv, int ld_qkv, void* out, int ld_out, int B, int
  *     combine (res_stats); other forms exist in the development build (libmme_dev.so) only;
  *   mme_attention_form: 0 = production, 30 + kind = kernel kind `kind` (production: 83 hd 72,
  *     86 / 87 hd 80, 89 hd 64; 94 = the persistent form of 86, measured and not dispatched);
- *   mme_gemm_mx_form (below): -1 = production (mx11 where its geometry holds, with the bias loaded up
- *     front where N % 4 == 0, else mx10), 11 = mx11 without the up-front bias, 10 = mx10, 0 / 2 / 3 = earlier forms, 12 / 14 = mx12 (persistent mx11 with / without
+ *   mme_gemm_mx_form (below): -1 = production (mx11 where its geometry holds -- with the bias loaded up
+ *     front, the mx8 block absmax by DPP and quick_gelu in packed f32 where N % 4 == 0 (form 16) -- else
+ *     mx10), 11 = mx11 without those, 10 = mx10, 0 / 2 / 3 = earlier forms, 12 / 14 = mx12 (persistent mx11 with / without
  *     the next tile's DMA under the epilogue; measured slower, not dispatched), 15 = mx11 with the
- *     bias loaded up front (N % 4 == 0, 8-B aligned bias; what production runs there);
+ *     bias loaded up front alone (N % 4 == 0, 8-B aligned bias), 16 = what production runs there;
  *   mme_gemm_form 95 = pipe10 on every non-split GEMM (measured slower, not dispatched); 93 = the
  *     production kernels with their epilogues branching on the operands at run time (the dispatch
  *     before round 5's compiled epilogues; bit-identical, slower). */

@@ -58,6 +58,13 @@ __device__ __forceinline__ float block_amax(float a) {
     a = fmaxf(a, __shfl_xor(a, 2, 64));
     return a;
 }
+// the same by DPP quad permutes ([1,0,3,2], then [2,3,0,1]) instead of two ds_bpermute round trips
+// (max is exact in any order: bit-identical); a >= 0, so a disabled source lane's 0 is harmless
+__device__ __forceinline__ float block_amax_dpp(float a) {
+    a = fmaxf(a, __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(a), 0xB1, 0xF, 0xF, false)));
+    a = fmaxf(a, __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(a), 0x4E, 0xF, 0xF, false)));
+    return a;
+}
 
 // ---------------------------------------------------------------------------
 // bf16 rows -> mx8. One 256-thread block per row; thread t handles 16-B
@@ -248,7 +255,7 @@ constexpr int MXW_PITCH = 144, MXW_LDS = 8 * 128 * MXW_PITCH;
 // BPRE (mx form 15, round 5): the wave's 32 bias values loaded up front as eight 8-B loads (one wait)
 // instead of four 2-B loads and a wait per column quad (needs N % 4 == 0 and an 8-B aligned bias:
 // a quad's columns are then all in range or all past N, so clamping the quad start is exact).
-template <int ACT, bool SWZ = true, bool SB = false, int PASSES = 1, bool BPRE = false>
+template <int ACT, bool SWZ = true, bool SB = false, int PASSES = 1, bool BPRE = false, bool DPPA = false>
 __device__ __forceinline__ void mx_epilogue_wave(const MxArgs& p, char* lds, f32x16 (&acc)[4][2], int m0, int n0,
                                                  int wave, int lane) {
     static_assert(PASSES == 1 || (PASSES == 2 && SWZ), "one or two staging passes");
@@ -287,8 +294,20 @@ __device__ __forceinline__ void mx_epilogue_wave(const MxArgs& p, char* lds, f32
 #pragma unroll
             for (int i = ps * (4 / PASSES); i < (ps + 1) * (4 / PASSES); ++i) {
                 bf16x4 o;
+                if constexpr (DPPA && (ACT == MME_ACT_QUICK_GELU || ACT == MME_ACT_NONE)) {
+                    // packed f32 (form 16): the same operations as apply_act's for these two, so the same bits
 #pragma unroll
-                for (int r = 0; r < 4; ++r) o[r] = f2bf(apply_act(acc[i][j][4 * qd + r] + bv[r], ACT));
+                    for (int r = 0; r < 4; r += 2) {
+                        const f32x2 y = apply_act2(f32x2{acc[i][j][4 * qd + r], acc[i][j][4 * qd + r + 1]} +
+                                                       f32x2{bv[r], bv[r + 1]},
+                                                   ACT);
+                        o[r] = f2bf(y.x);
+                        o[r + 1] = f2bf(y.y);
+                    }
+                } else {
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) o[r] = f2bf(apply_act(acc[i][j][4 * qd + r] + bv[r], ACT));
+                }
                 const int lrow = i * 32 + r32 - ps * BAND;
                 if constexpr (SWZ)  // chunk 4 j + qd ^ (row & 7), half h ^ (row >> 3 & 1); row & 31 = r32
                     *reinterpret_cast<bf16x4*>(reg + lrow * MX9_PITCH + (((4 * j + qd) ^ (r32 & 7)) << 4) +
@@ -341,7 +360,7 @@ __device__ __forceinline__ void mx_epilogue_wave(const MxArgs& p, char* lds, f32
                 f[e] = bits2f(v[e]);
                 a = fmaxf(a, fabsf(f[e]));
             }
-            const int sbyte = mx_scale_byte(block_amax(a));
+            const int sbyte = mx_scale_byte(DPPA ? block_amax_dpp(a) : block_amax(a));
             if (gr < p.M && gc < p.N) {
                 *reinterpret_cast<uint2*>(Cq + (size_t)gr * p.ldc + gc) = mx_pack8(f, sbyte);
                 if ((cc & 3) == 0) p.sc[(size_t)(gc >> 5) * p.sc_rows + mx_srow(gr)] = (uint8_t)sbyte;
@@ -785,7 +804,7 @@ __device__ __forceinline__ void mx11_mfma(f32x16& acc, const bf16x8 (&a)[2], con
     acc = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(bo, ao, acc, 0, 0, J, (int)sb, I, (int)sa);
 }
 
-template <int ACT, bool LATE, bool BPRE = false>
+template <int ACT, bool LATE, bool BPRE = false, bool DPPA = false>
 __device__ __forceinline__ void mx11_tile(const MxArgs& p, char* lds, const int m0, const int n0, const int wave) {
     constexpr int UNIT = 32768;
     const int lane = threadIdx.x & 63;
@@ -957,10 +976,10 @@ __device__ __forceinline__ void mx11_tile(const MxArgs& p, char* lds, const int 
         for (int j = 0; j < 2; ++j) asm volatile("" : "+v"(acc[i][j]));
     // no LDS hazard: every wave's last fragment reads precede the barrier closing the late row's
     // last memory phase, which the early row passes before it writes its epilogue region
-    mx_epilogue_wave<ACT, true, true, 1, BPRE>(p, lds, acc, m0, n0, wave, lane);
+    mx_epilogue_wave<ACT, true, true, 1, BPRE, DPPA>(p, lds, acc, m0, n0, wave, lane);
 }
 
-template <int GROUP_M, int ACT, bool BPRE = false>
+template <int GROUP_M, int ACT, bool BPRE = false, bool DPPA = false>
 __global__ __launch_bounds__(512, 2) void gemm_mx11_kernel(MxArgs p) {
     __shared__ __attribute__((aligned(16))) char lds[5 * 32768];
     const int nbm = (p.M + 255) / 256, nbn = (p.N + 255) / 256;
@@ -969,26 +988,26 @@ __global__ __launch_bounds__(512, 2) void gemm_mx11_kernel(MxArgs p) {
     tile_coords<GROUP_M>(tile, nbm, nbn, bm, bn);
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     if (wave >= 4)
-        mx11_tile<ACT, true, BPRE>(p, lds, bm * 256, bn * 256, wave);
+        mx11_tile<ACT, true, BPRE, DPPA>(p, lds, bm * 256, bn * 256, wave);
     else
-        mx11_tile<ACT, false, BPRE>(p, lds, bm * 256, bn * 256, wave);
+        mx11_tile<ACT, false, BPRE, DPPA>(p, lds, bm * 256, bn * 256, wave);
 }
 
-template <int GROUP_M, bool BPRE = false>
+template <int GROUP_M, bool BPRE = false, bool DPPA = false>
 int launch_mx11(const MxArgs& a, hipStream_t s) {
     const dim3 grid(((a.M + 255) / 256) * ((a.N + 255) / 256)), block(512);
     switch (a.act) {
         case MME_ACT_GELU_TANH:
-            hipLaunchKernelGGL((gemm_mx11_kernel<GROUP_M, MME_ACT_GELU_TANH, BPRE>), grid, block, 0, s, a);
+            hipLaunchKernelGGL((gemm_mx11_kernel<GROUP_M, MME_ACT_GELU_TANH, BPRE, DPPA>), grid, block, 0, s, a);
             break;
         case MME_ACT_QUICK_GELU:
-            hipLaunchKernelGGL((gemm_mx11_kernel<GROUP_M, MME_ACT_QUICK_GELU, BPRE>), grid, block, 0, s, a);
+            hipLaunchKernelGGL((gemm_mx11_kernel<GROUP_M, MME_ACT_QUICK_GELU, BPRE, DPPA>), grid, block, 0, s, a);
             break;
         case MME_ACT_GELU_ERF:
-            hipLaunchKernelGGL((gemm_mx11_kernel<GROUP_M, MME_ACT_GELU_ERF, BPRE>), grid, block, 0, s, a);
+            hipLaunchKernelGGL((gemm_mx11_kernel<GROUP_M, MME_ACT_GELU_ERF, BPRE, DPPA>), grid, block, 0, s, a);
             break;
         default:
-            hipLaunchKernelGGL((gemm_mx11_kernel<GROUP_M, MME_ACT_NONE, BPRE>), grid, block, 0, s, a);
+            hipLaunchKernelGGL((gemm_mx11_kernel<GROUP_M, MME_ACT_NONE, BPRE, DPPA>), grid, block, 0, s, a);
             break;
     }
     return mme_check_launch("mme_gemm_mx");
@@ -1457,9 +1476,9 @@ inline int mx_default_form() { return -1; }
 #endif
 inline bool mx_form_ok(int v) {
 #ifdef MME_DEV
-    return v == -1 || v == 0 || v == 2 || v == 3 || v == 4 || v == 9 || v == 10 || v == 11 || v == 12 || v == 14 || v == 15;
+    return v == -1 || v == 0 || v == 2 || v == 3 || v == 4 || v == 9 || v == 10 || v == 11 || v == 12 || v == 14 || v == 15 || v == 16;
 #else
-    return v == -1 || v == 0 || v == 2 || v == 3 || v == 10 || v == 11 || v == 12 || v == 14 || v == 15;
+    return v == -1 || v == 0 || v == 2 || v == 3 || v == 10 || v == 11 || v == 12 || v == 14 || v == 15 || v == 16;
 #endif
 }
 
@@ -1600,10 +1619,14 @@ int gemm_mx_entry(int form, const void* A, int lda, const void* sa, int sa_rows,
                          (size_t)(K / 32) * (sa_rows > sb_rows ? sa_rows : sb_rows) < (1ull << 32);
     if (form == 12 && mx11_ok) return launch_mx12<4>(a, as_stream(stream));
     if (form == 14 && mx11_ok) return launch_mx12<4, 2>(a, as_stream(stream));
-    // round 5: the bias loaded up front (form 15, production where N % 4 == 0 and the bias is 8-B aligned):
-    // DFN5B-H fp8 job 1 185-1 187 -> 1 203 img/s, bit-identical (profiles/r05_v20_mx15_ab.log); form 11 = without
-    if (form != 10 && form != 11 && mx11_ok && N % 4 == 0 && ((uintptr_t)bias & 7) == 0)
+    // round 5, production where N % 4 == 0 and the bias is 8-B aligned: the bias loaded up front (form 15:
+    // DFN5B-H fp8 job 1 185-1 187 -> 1 203 img/s, profiles/r05_v20_mx15_ab.log), the mx8 output's block absmax
+    // by DPP and quick_gelu in packed f32 (form 16: 1 179-1 181 -> 1 193-1 196 img/s, profiles/r05_v22_mx16_ab.log);
+    // bit-identical throughout; form 11 = mx11 without either, form 15 = the bias alone
+    if (form == 15 && mx11_ok && N % 4 == 0 && ((uintptr_t)bias & 7) == 0)
         return launch_mx11<4, true>(a, as_stream(stream));
+    if (form != 10 && form != 11 && mx11_ok && N % 4 == 0 && ((uintptr_t)bias & 7) == 0)
+        return launch_mx11<4, true, true>(a, as_stream(stream));
     if (form != 10 && mx11_ok) return launch_mx11<4>(a, as_stream(stream));
     return launch_mx10<4>(a, as_stream(stream));
 }

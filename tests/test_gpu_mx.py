@@ -268,7 +268,8 @@ def test_gemm_mx_wave_epilogue_bit_identical(cuda, M, N, K, kind):
                                          (304410, 3840, 1280, "bias"), (5000, 1280, 384, "res"), (100, 256, 512, "mx_out")])
 def test_gemm_mx12_bit_identical_to_mx11(cuda, M, N, K, kind):
     """Forms 12 / 14 (mx12: persistent mx11, the next tile's first DMA units under the epilogue or not,
-    two-pass staging; measured slower, not dispatched) and 15 (mx11 with the bias loaded up front)
+    two-pass staging; measured slower, not dispatched), 15 (mx11 with the bias loaded up front) and 16
+    (+ the mx8 block absmax by DPP, quick_gelu in packed f32)
     against form 11 (mx11) at DFN5B-H's execution batch (417 images x 730 tokens: many tiles per
     CU) for the three fp8 encoder GEMMs with their job epilogues, the minimum K and fewer tiles than CUs:
     bit-identical outputs and scales."""
@@ -278,7 +279,7 @@ def test_gemm_mx12_bit_identical_to_mx11(cuda, M, N, K, kind):
     bias = rnd(N, scale=0.1, gen=g)
     res0 = rnd(M, N, gen=g)
     outs = []
-    for v in (11, 12, 14, 15):
+    for v in (11, 12, 14, 15, 16):
         with ops.kernel_forms(mx=v):
             if kind == "mx_out":
                 o = mx.MXTensor.empty(M, N, "cuda")
