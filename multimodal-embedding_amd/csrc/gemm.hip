@@ -1756,6 +1756,11 @@ int launch_pipe9(const GemmArgs& a, hipStream_t s) {
                 hipLaunchKernelGGL((gemm_pipe9_kernel<C, GROUP_M, MME_ACT_NONE, SPLIT, PRIO, ESWZ, 2>), grid, block, 0, s, a);
             return mme_check_launch("mme_gemm");
         }
+        if (a.act == MME_ACT_GEGLU_TANH && !a.res && !a.ln_stats) {  // ColPali's gate / up GEMM: bias only
+            hipLaunchKernelGGL((gemm_pipe9_kernel<C, GROUP_M, MME_ACT_GEGLU_TANH, SPLIT, PRIO, ESWZ, 2>), grid, block, 0, s,
+                               a);
+            return mme_check_launch("mme_gemm");
+        }
     }
     switch (a.act) {
         case MME_ACT_GELU_TANH:
@@ -2526,6 +2531,7 @@ int gemm_dispatch(GemmArgs a, int variant, hipStream_t s) {
     if (glu) {  // gated epilogue: the pipelined kernel only (its LDS-staged 16-B tile rows pair gate/up)
         MME_REQUIRE(N % 8 == 0 && ldc % 4 == 0 && !out_f32 && !residual && ((uintptr_t)Cp & 7) == 0,
                     "mme_gemm: GeGLU needs N %% 8 == 0, ldc %% 4 == 0, 8-B aligned bf16 C, no residual");
+        if (pipe8_ok(a) && variant == 93) return launch_pipe9<Pipe256, 4, false, 0, true, false>(a, s);
         if (pipe8_ok(a) && variant != 47) return launch_pipe9<Pipe256, 4, false>(a, s);
         return launch_pipe6<Pipe256, 4, 1>(a, s);
     }

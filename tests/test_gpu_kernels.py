@@ -585,6 +585,23 @@ def test_gemm_fc1_compiled_epilogues_bit_identical(cuda, M, N, K):
                 assert torch.equal(a_, b_), f"form {form} act {act} differs from pipe6 ({M}x{N}x{K})"
 
 
+@pytest.mark.parametrize("M,N,K", [(4100, 4096, 1024), (20000, 8192, 2048)])
+def test_gemm_geglu_compiled_epilogue_bit_identical(cuda, M, N, K):
+    """ColPali's gate / up GEMM (GeGLU, bias, no residual) with the epilogue compiled for its
+    operands (FOLD 2) against pipe6 (form 47) and the run-time form (93): bit-identical."""
+    g = torch.Generator(device="cuda").manual_seed(M + N + K + 7)
+    x = rnd(M, K, gen=g)
+    w = rnd(N, K, scale=K ** -0.5, gen=g)
+    b = rnd(N, scale=0.1, gen=g)
+    outs = []
+    for form in (47, -1, 93):
+        with ops.kernel_forms(**({} if form == -1 else {"gemm": form})):
+            outs.append(ops.gemm(x, w, b, act=_lib.ACT_GEGLU_TANH))
+    torch.cuda.synchronize()
+    for form, o in zip((-1, 93), outs[1:]):
+        assert torch.equal(outs[0], o), f"GeGLU form {form} differs from pipe6 ({M}x{N}x{K})"
+
+
 # mme_gemm_res_stats: the residual GEMM's output is bit-identical to mme_gemm's, and the
 # row statistics reduced in its epilogue (64-column slices, Chan-combined) match a separate
 # mme_rowstats pass over that output up to fp32 summation order. Shapes: split grid
