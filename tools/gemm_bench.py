@@ -36,7 +36,7 @@ def main():
                    "bias + quick_gelu to an mx8 output, fc2 bias + residual in place)")
     p.add_argument("--torch", action="store_true", help="also time torch F.linear (hipBLASLt) on each shape")
     p.add_argument("--epi", default="none", help="epilogue: none | bias | res (residual in place) | resstats (res + LayerNorm "
-                   "statistics, mme_gemm_res_stats) | gelu (bias+gelu_tanh)")
+                   "statistics, mme_gemm_res_stats) | gelu (bias+gelu_tanh) | erf (bias+exact GELU) | quick (bias+quick_gelu)")
     a = p.parse_args()
     variants = [int(v) for v in a.variants.split(",")] if a.variants else [-1]
     g = torch.Generator(device="cuda").manual_seed(0)
@@ -51,7 +51,8 @@ def main():
         R256 = C[:256].clone()  # "resper": residual rows r % 256 (an L2-resident residual table)
         kw = {"none": {}, "bias": {"bias": bias}, "res": {"bias": bias, "residual": C}, "resstats": {},
               "resper": {"bias": bias, "residual": R256, "res_period": 256},
-              "gelu": {"bias": bias, "act": _lib.ACT_GELU_TANH}}[a.epi]
+              "gelu": {"bias": bias, "act": _lib.ACT_GELU_TANH}, "erf": {"bias": bias, "act": _lib.ACT_GELU_ERF},
+              "quick": {"bias": bias, "act": _lib.ACT_QUICK_GELU}}[a.epi]
         st = torch.empty(M, 2, device="cuda")
         part = torch.empty(M, max(1, N // 64), 2, device="cuda")
 
