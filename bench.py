@@ -217,21 +217,22 @@ def retrieval_parity(tables, metrics, caps_per_image: int = 5):
         _, rsc = R.topk(s, k + 1)
         tied = np.zeros(len(ridx), bool)
         tied[ranked.tie_rows.cpu().numpy()] = True
-        only = []
+        only, missed = [], []
         same, near = R.compare_topk(ranked.idx.cpu().numpy(), ridx, rsc, exact_rows=tied,
-                                    dev_score=ranked.score.cpu().numpy(), oracle_only=only)
+                                    dev_score=ranked.score.cpu().numpy(), oracle_only=only, unflagged=missed)
         rows[name] = {"rows_identical": f"{int(same.sum())}/{len(same)}", "near_tie_rows": int(near.sum()),
                       "decisive_rows_differing": int((~same & ~near).sum()),
                       "exact_tie_rows_torch_order": int(ranked.tie_rows.numel()),
-                      "oracle_only_exact_tie_rows": len(only)}
+                      "oracle_only_exact_tie_rows": len(only), "device_ties_unflagged": len(missed)}
         for kr, h in zip((1, 5, 10), R.hits(s, tc).sum(0)):
             ref_metrics[f"{name}_R@{kr}"] = 100.0 * h / n
     return {"recall_identical": all(ref_metrics[k] == metrics[k] for k in ref_metrics),
             "oracle_recall": {k: round(v, 2) for k, v in ref_metrics.items()}, "rows": rows,
             "near_tie_rule": "neighbouring oracle scores among the top 11 within 1e-5*|s1|; exact ties are not "
                              "exempt on rows the device finds tied too (torch.topk's order, replayed on both "
-                             "sides); an oracle-only exact tie is a near tie only where the device's own "
-                             "scores differ at that place (counted in oracle_only_exact_tie_rows)",
+                             "sides); an oracle-only exact tie is a near tie (counted in oracle_only_exact_tie_rows); "
+                             "a device row whose own top-11 scores tie must be flagged by tie_rows "
+                             "(device_ties_unflagged, 0 expected)",
             "checker": "oracle/retrieval.py on the job's own embeddings (numpy fp32 + torch.topk order, host)",
             "seconds": round(time.time() - t0, 2)}
 
@@ -239,10 +240,11 @@ def retrieval_parity(tables, metrics, caps_per_image: int = 5):
 def fp8_drift(model_name, dev, imgs, t2i_ids, cap_ids, fp8_tables, img_batch, txt_batch, caps: int = 5):
     """fp8 against bf16 over the WHOLE job (checker; after the timed region, --fp8 only): the same
     weights (seed 0) loaded without the mx8 GEMMs encode the job's images and captions, and the
-    job's fp8 tables are compared with them (mme.mx.job_drift: per-row cosine of the embeddings, the
-    I2T ranking -- every image against all 5n captions, mme_sim_topk -- as top-1 agreement and top-10
-    overlap, and `drift_ok` against mme.mx.JOB_DRIFT_BOUNDS, which tests/test_gpu_mx.py asserts on the
-    same job)."""
+    job's fp8 tables are compared with them (mme.mx.job_drift: per-row cosine of the embeddings; the
+    I2T ranking -- every image against all 5n captions, mme_sim_topk -- as top-1 agreement on the rows
+    decided beyond the measured fp8 score perturbation (gated, with the decided count), and over all rows
+    plus top-10 overlap (reported); `drift_ok` against mme.mx.JOB_DRIFT_BOUNDS, which tests/test_gpu_mx.py
+    asserts on the same job)."""
     from mme import mx
     from mme.models import load_model
     t0 = time.time()
@@ -678,16 +680,24 @@ def main():
     gev = last["tables"].get("gather_events")
     gather_ms = gev[0].elapsed_time(gev[1]) if gev is not None else 0.0
     allgather_per_rank = [round(gather_ms / 1e3, 5)]
+    # per-rank record of the last timed step (so an N-GPU line names the rank / phase that limits it):
+    # phases (s), this rank's image count, its wall time of the K timed steps (s), the all-gather (s)
+    per_rank = torch.zeros(world, 7, dtype=torch.float64, device=dev)
+    per_rank[rank] = torch.tensor([phases[0] / 1e3, phases[1] / 1e3, phases[2] / 1e3, hi - lo, my_caps.shape[0],
+                                   dt, gather_ms / 1e3], dtype=torch.float64)
     if world > 1:
         t = torch.tensor([dt], device=dev)
         all_reduce_(t, dist.ReduceOp.MAX)
         dt = float(t.item())
         all_reduce_(phases, dist.ReduceOp.MAX)
-        g_all = torch.zeros(world, dtype=torch.float64, device=dev)
-        g_all[rank] = gather_ms / 1e3
-        all_reduce_(g_all, dist.ReduceOp.SUM)
-        allgather_per_rank = [round(x, 5) for x in g_all.tolist()]
+        all_reduce_(per_rank, dist.ReduceOp.SUM)
+        allgather_per_rank = [round(x, 5) for x in per_rank[:, 6].tolist()]
     phases = phases.tolist()
+    pr = per_rank.tolist()
+    per_rank_line = {"encode_images_s": [round(r[0], 4) for r in pr], "encode_texts_s": [round(r[1], 4) for r in pr],
+                     "retrieval_s": [round(r[2], 4) for r in pr], "n_images": [int(r[3]) for r in pr],
+                     "n_captions": [int(r[4]) for r in pr], "timed_s": [round(r[5], 4) for r in pr],
+                     "slowest_rank": max(range(world), key=lambda i: pr[i][0] + pr[i][1] + pr[i][2])}
     kt = ops.KernelTimer.summary() if not args.no_kernel_timer else {}
 
     roofline = None
@@ -761,6 +771,8 @@ def main():
         # per rank, last timed step: the RCCL all-gathers of the image / T2I / caption tables
         # (device events around them; 0 at N = 1 where nothing is gathered)
         "allgather_s_per_rank": allgather_per_rank,
+        # the same phases per rank (index = rank), with each rank's share and its own timed wall clock
+        "per_rank": per_rank_line,
         "roofline": roofline,
         "parity": None,
         "cpu_baseline": None,

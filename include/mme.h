@@ -154,12 +154,15 @@ int mme_attention(const void* qkv, int ld_qkv, void* out, int ld_out, int B, int
  *     86 / 87 hd 80, 89 hd 64; 94 = the persistent form of 86, measured and not dispatched);
  *   mme_gemm_mx_form (below): -1 = production (mx11 where its geometry holds -- with the bias loaded up
  *     front, the mx8 block absmax by DPP and quick_gelu in packed f32 where N % 4 == 0 (form 16) -- else
- *     mx10), 11 = mx11 without those, 10 = mx10, 0 / 2 / 3 = earlier forms, 12 / 14 = mx12 (persistent mx11 with / without
- *     the next tile's DMA under the epilogue; measured slower, not dispatched), 15 = mx11 with the
+ *     mx10), 11 = mx11 without those, 10 = mx10, 0 / 2 / 3 = earlier forms, 15 = mx11 with the
  *     bias loaded up front alone (N % 4 == 0, 8-B aligned bias), 16 = what production runs there;
- *   mme_gemm_form 95 = pipe10 on every non-split GEMM (measured slower, not dispatched); 93 = the
- *     production kernels with their epilogues branching on the operands at run time (the dispatch
- *     before round 5's compiled epilogues; bit-identical, slower). */
+ *     12 / 14 = mx12 (persistent mx11 with / without the next tile's DMA under the epilogue; measured
+ *     slower, not dispatched) exist in the development build only;
+ *   two NON-dispatched GEMM forms stay in the production build on purpose, because production-suite
+ *     bit-identity tests and A/B runs select them: mme_gemm_form 95 = pipe10 on every non-split GEMM
+ *     (measured slower) and 93 = the production kernels with their epilogues branching on the operands
+ *     at run time (the dispatch before round 5's compiled epilogues; bit-identical, slower). The plain
+ *     entry points never run them. */
 int mme_gemm_form(int form, const void* A, int lda, const void* B, int ldb, void* C, int ldc, int M, int N, int K,
                   const void* bias, const void* residual, int ldr, int res_period, int act, int out_f32,
                   void* stream);

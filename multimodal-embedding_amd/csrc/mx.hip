@@ -1478,7 +1478,7 @@ inline bool mx_form_ok(int v) {
 #ifdef MME_DEV
     return v == -1 || v == 0 || v == 2 || v == 3 || v == 4 || v == 9 || v == 10 || v == 11 || v == 12 || v == 14 || v == 15 || v == 16;
 #else
-    return v == -1 || v == 0 || v == 2 || v == 3 || v == 10 || v == 11 || v == 12 || v == 14 || v == 15 || v == 16;
+    return v == -1 || v == 0 || v == 2 || v == 3 || v == 10 || v == 11 || v == 15 || v == 16;  // mx12: dev only
 #endif
 }
 

@@ -332,11 +332,14 @@ class ColPaliProcessor:
     """process_images / process_queries / score (main.py:403,423,467) over the device path.
 
     Images: u8 arrays / PIL -> pixel_values by the PIL-exact preprocess kernel (448 square).
-    Queries: pre-tokenized id lists, or strings through the checkpoint's tokenizer (`tokenizer=`:
-    an HF-compatible callable, asked for the caption body only, `add_special_tokens=False`; the
-    ColPali layout adds bos, the query prefix, the augmentation pads and the newline); without
-    one, strings raise unless `allow_hash_tokenizer=True` selects the offline word-hash stand-in.
-    ColPali layout, left padding to the batch-longest."""
+    Queries: pre-tokenized id lists (the spec adds bos, the query prefix ids, the augmentation pads and
+    the newline), or strings through the checkpoint's tokenizer (`tokenizer=`: an HF-compatible
+    callable). A string is laid out the way ColPaliProcessor.__call__ does it,
+    f"{bos_token}{query_prefix}{query}{pad_token * 10}\n" (TF:models/colpali/processing_colpali.py,
+    __call__), and that WHOLE string is tokenized in one call (`add_special_tokens=False`: the bos is
+    in the text), so SentencePiece merges across the prefix / query seam exactly as for the reference.
+    Without a tokenizer, strings raise unless `allow_hash_tokenizer=True` selects the offline
+    word-hash stand-in (body hashed, spec layout). Left padding to the batch-longest."""
 
     def __init__(self, spec: ColPaliSpec, device="cuda", tokenizer=None, allow_hash_tokenizer: bool = False):
         from .colpali import ColPaliScorer
@@ -374,15 +377,23 @@ class ColPaliProcessor:
     def process_queries(self, queries, **_):
         from .processor import _as_rows, _ids, no_string_tokenizer
         strs = [q for q in queries if isinstance(q, str)]
-        body = iter(())
+        full = iter(())
         if strs and self.text_tokenizer is not None:
-            body = iter(_as_rows(_ids(self.text_tokenizer(strs, add_special_tokens=False, padding=False,
-                                                          truncation=False))))
+            full = iter(_as_rows(_ids(self.text_tokenizer([self.query_string(q) for q in strs],
+                                                          add_special_tokens=False, padding=False, truncation=False))))
         elif strs and self.tokenizer is None:
             raise no_string_tokenizer("ColPaliProcessor.process_queries")
-        toks = [(next(body) if self.text_tokenizer is not None else self.tokenizer.encode(q))
-                if isinstance(q, str) else [int(x) for x in q] for q in queries]
-        return self._batch([self.spec.query_tokens(t) for t in toks])
+        rows = [(list(next(full)) if self.text_tokenizer is not None else
+                 self.spec.query_tokens(self.tokenizer.encode(q)))
+                if isinstance(q, str) else self.spec.query_tokens([int(x) for x in q]) for q in queries]
+        return self._batch(rows)
+
+    def query_string(self, query: str) -> str:
+        """ColPaliProcessor.__call__'s text layout: bos + query prefix + query + 10 augmentation pads + newline."""
+        tok = self.text_tokenizer
+        bos = getattr(tok, "bos_token", None) or "<bos>"
+        pad = getattr(tok, "pad_token", None) or "<pad>"
+        return f"{bos}{self.spec.query_prefix}{query}{pad * self.spec.n_aug}\n"
 
     def score(self, qs, ps, **kw):
         return self._scorer.score(qs, ps, **kw)

@@ -197,6 +197,7 @@ class ColPaliSpec:
     newline_id: int = 108
     prompt_ids: Tuple[int, ...] = (50721, 573, 2416, 235265)   # synthetic "Describe the image."
     query_prefix_ids: Tuple[int, ...] = (9413, 235292, 235248)  # synthetic "Question: "
+    query_prefix: str = "Question: "   # the text layout of string queries (ColPaliProcessor.query_prefix)
     n_aug: int = 10
     dim: int = 128
     batch_size: int = 4   # main.py:130

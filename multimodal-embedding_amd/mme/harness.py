@@ -73,9 +73,8 @@ def run_benchmark(model, images_u8: torch.Tensor, caption_ids: torch.Tensor, cap
     name = model.spec.name
     _sync()
     t_start = clock()  # main.py:534: the clock starts before the warmup
-    if warmup:  # main.py:537-543: two items through the same encode path
-        encode_job(model, images_u8[:2], caption_ids[: 2 * caps_per_image], None if caption_lens is None else
-                   caption_lens[: 2 * caps_per_image], caps_per_image, **kw)
+    if warmup:  # main.py:537-541: ONE encode_data call on 2 copies of image 0 and 2 of T2I caption 0
+        warmup_encode(model, images_u8, caption_ids, caption_lens)
     _sync()
     t_warm = clock()
     img, t2i, all_txt = encode_job(model, images_u8, caption_ids, caption_lens, caps_per_image, **kw)
@@ -86,6 +85,8 @@ def run_benchmark(model, images_u8: torch.Tensor, caption_ids: torch.Tensor, cap
     if n_iterations > 0:
         from . import bootstrap as mb
         s_t2i, s_i2t = mb.full_scores(img, t2i, all_txt)
+        _sync()
+        t_scored = clock()
         hits = mb.bootstrap_hits(s_t2i, s_i2t, mb.sample_indices(n, n_iterations, seed, img.device), caps_per_image)
         row.update(mb.bootstrap_row(hits, n, seed=seed))
     else:
@@ -95,12 +96,27 @@ def run_benchmark(model, images_u8: torch.Tensor, caption_ids: torch.Tensor, cap
             row[f"{k}_mean"], row[f"{k}_lower"], row[f"{k}_upper"], row[f"{k}_std"] = v, v, v, 0.0
     _sync()
     t_done = clock()
+    if n_iterations <= 0:
+        t_scored = t_done
     row.update(timing_columns(n, t_start, t_encoded, t_done))
     row["_failure_analysis"] = {}
-    if timings is not None:
-        timings.update(warmup_s=t_warm - t_start, encode_s=t_encoded - t_warm, retrieval_s=t_done - t_encoded,
-                       e2e_img_per_sec=n / (t_done - t_warm))
+    if timings is not None:  # the v28 rate excludes the bootstrap resampling (reported as bootstrap_s)
+        timings.update(warmup_s=t_warm - t_start, encode_s=t_encoded - t_warm, retrieval_s=t_scored - t_encoded,
+                       bootstrap_s=t_done - t_scored, e2e_img_per_sec=n / (t_scored - t_warm))
     return row
+
+
+def warmup_encode(model, images_u8: torch.Tensor, caption_ids: torch.Tensor, caption_lens=None):
+    """main.py:537-541: dummy_img = [images[0]] * min(2, n), dummy_txt = [t2i_captions[0]] * min(2, n),
+    one encode_data call (images, then texts). T2I caption 0 is all_captions[0] (main.py:520)."""
+    n = images_u8.shape[0]
+    if n == 0:
+        return
+    w = min(2, n)
+    model.encode_images(images_u8[:1].expand(w, *images_u8.shape[1:]).contiguous())
+    ids = caption_ids[:1].expand(w, *caption_ids.shape[1:]).contiguous()
+    lens = None if caption_lens is None else caption_lens[:1].expand(w).contiguous()
+    model.encode_texts(ids, lens)
 
 
 def write_csv(rows: List[Dict[str, object]], path: str) -> None:

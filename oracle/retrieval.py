@@ -100,34 +100,37 @@ def hits(s: np.ndarray, tgt_count: int, ks: Sequence[int] = KS, row_offset: int 
 
 
 def compare_topk(idx: np.ndarray, ref_idx: np.ndarray, ref_score: np.ndarray, rel_tol: float = 1e-5,
-                 exact_rows: np.ndarray = None, dev_score: np.ndarray = None, oracle_only: list = None):
+                 exact_rows: np.ndarray = None, dev_score: np.ndarray = None, oracle_only: list = None,
+                 unflagged: list = None):
     """Row-wise parity of a top-k index table against the reference's.
 
     ref_idx / ref_score hold the reference's top-(k+1) per row (score desc). A row is a
     near-tie when two neighbouring scores among those k+1 differ by <= rel_tol·|s_1| but are
     not equal: a different fp32 summation order may legitimately swap them (SURVEY §7,
-    "exact-index parity"). EXACT ties are not exempt: their order is torch.topk's, which the
-    device replays. exact_rows (bool per row, optional): the rows the compared side itself found
-    exactly tied (mme.retrieval.Ranked.tie_rows), with dev_score, its own top-(k+1) scores: a
-    reference exact tie on any OTHER row is a near tie only where the compared side's scores at
-    that place really differ (its summation order did not produce the tie); where they are equal
-    too, the compared side missed a tie and the row is NOT exempt. Without dev_score every such
-    row is exempt (the round-4 rule). oracle_only (a list, optional) receives the indices of the
-    rows holding a reference-only exact tie. Returns (identical [rows] bool, near_tie [rows]
-    bool); every row that is not a near-tie must be identical. With no (k+1)-th reference column
-    (fewer columns than k + 1) only the gaps that exist are compared."""
+    "exact-index parity"). EXACT ties are not exempt on rows the compared side found tied too
+    (exact_rows, bool per row: mme.retrieval.Ranked.tie_rows): their order is torch.topk's, which
+    the device replays. A reference exact tie on a row the compared side did NOT flag is a near tie
+    (its summation order separated the pair); oracle_only (a list, optional) receives those rows.
+    dev_score (optional), the compared side's own top-(k+1) scores, checks the flags themselves:
+    a row whose own scores hold an exact tie must be flagged; unflagged (a list, optional)
+    receives the rows that are not (a tie_rows defect; callers assert it stays empty). Returns
+    (identical [rows] bool, near_tie [rows] bool); every row that is not a near-tie must be
+    identical. With no (k+1)-th reference column (fewer columns than k + 1) only the gaps that
+    exist are compared."""
     k = idx.shape[1]
     same = (idx == ref_idx[:, :k]).all(1)
     kk = min(k + 1, ref_score.shape[1])
     gaps = ref_score[:, :kk - 1] - ref_score[:, 1:kk]
     unequal = gaps != 0
     if exact_rows is not None:
-        only = ~np.asarray(exact_rows, bool)[:, None] & (gaps == 0)
+        flagged = np.asarray(exact_rows, bool)
+        only = ~flagged[:, None] & (gaps == 0)
         if oracle_only is not None:
             oracle_only.extend(np.nonzero(only.any(1))[0].tolist())
-        if dev_score is not None:
-            dgaps = dev_score[:, :kk - 1] - dev_score[:, 1:kk]
-            only &= dgaps != 0
+        if dev_score is not None and unflagged is not None:
+            kd = min(kk, dev_score.shape[1])
+            dtied = (dev_score[:, :kd - 1] == dev_score[:, 1:kd]).any(1)
+            unflagged.extend(np.nonzero(dtied & ~flagged)[0].tolist())
         unequal = unequal | only
     near = ((gaps <= rel_tol * np.abs(ref_score[:, :1])) & unequal).any(1)
     return same, near

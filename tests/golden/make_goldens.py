@@ -127,7 +127,7 @@ class RefProcessor:
         return BatchFeature({"input_ids": ids, "attention_mask": mask})
 
 
-def hf_model(spec, dtype):
+def hf_model(spec, dtype, overrides=None):
     from transformers import CLIPConfig, CLIPModel, SiglipConfig, SiglipModel
     v, t = spec.vision, spec.text
     vc = dict(hidden_size=v.hidden, intermediate_size=v.intermediate, num_hidden_layers=v.layers,
@@ -145,6 +145,9 @@ def hf_model(spec, dtype):
         cfg = CLIPConfig(text_config=tc, vision_config=vc, projection_dim=spec.proj_dim)
         m = CLIPModel(cfg)
     sd = torch_state_dict(spec, seed=0)
+    for k, v in (overrides or {}).items():
+        assert k in sd and sd[k].shape == v.shape, k
+        sd[k] = torch.from_numpy(np.ascontiguousarray(v, np.float32))
     missing, unexpected = m.load_state_dict(sd, strict=False)
     missing = [k for k in missing if not k.endswith(("position_ids", "logit_scale", "logit_bias"))]
     assert not missing and not unexpected, (missing, unexpected)
@@ -241,6 +244,154 @@ def make_config0(main):
         del hf
     np.savez_compressed(os.path.join(HERE, "config0_clip_l.npz"), **out)
     print("config0_clip_l.npz:", {k: v.shape for k, v in out.items()})
+
+
+# ------------------------------------------------------------------ end-to-end (encode -> rank) with fitted heads
+def _fit_factors(F: np.ndarray, T: np.ndarray):
+    """Minimum-norm W [D, d] with F W^T = T (F [m, d] float64 features of rank m <= d), as bf16 factors
+    W = A B: B = bf16(V^T) [m, d] from F = U S V^T, then A = ((F B^T)^-1 T)^T [D, m] solved against the
+    ROUNDED B (F W^T = (F B^T) A^T = T), so A's own rounding costs one bf16 ulp of the targets (A's column i scales like 1/s_i and
+    multiplies back s_i), not the condition number of F."""
+    _, _, Vt = np.linalg.svd(F, full_matrices=False)
+    B = bf16_bits(torch.from_numpy(Vt.astype(np.float32)))
+    Bf = (B.astype(np.uint32) << 16).view(np.float32).astype(np.float64)
+    A = np.linalg.solve(F @ Bf.T, T).T
+    return bf16_bits(torch.from_numpy(A.astype(np.float32))), B
+
+
+def make_e2e(main):
+    """End-to-end parity fixture: the reference's own encode_data (main.py:386-438)
+    -> compute_similarity_scores (main.py:440-475) -> compute_metrics_detailed (main.py:305-383, v28 I2T
+    orientation) on inputs whose ranking is DECIDED beyond bf16 noise.
+
+    With random weights every embedding clusters (pairwise cosine 0.9+), so the top-10 score gaps
+    (~1e-4) sit far below the ~1e-3 score noise of any bf16 tower, on the device or on the CPU. Here
+    the towers keep their seeded random weights except the last linear map into the joint space,
+    which is FITTED in closed form (minimum-norm least squares on the fp32 reference's own pooled
+    features) onto graded targets (planted.graded_targets): every T2I / Sym row and the top of every
+    I2T row then sees 12 distinct levels 0.038 apart, and recall is not chance (R@1 / R@5 50 %, R@10
+    100 %). The fitted maps are the models' weights, used identically by the reference run here and
+    by the device on the GPU box: CLIP visual_projection / text_projection; SigLIP the MAP head's
+    mlp.fc2 (weight + bias, so image = r + fc2(h) hits the target) and text_model.head. They are
+    stored as bf16 factors A [D, m], B [m, d] (weights_gen.factor_product rebuilds W = bf16(A B)
+    bit-identically on any box; SHA-256 stored). The inputs are synthetic noise images and ragged
+    random-id captions (planted.e2e_inputs), encoded at the reference's --batch-size 32."""
+    from PIL import Image
+    from transformers.models.siglip.image_processing_pil_siglip import SiglipImageProcessorPil
+    from transformers.models.clip.image_processing_pil_clip import CLIPImageProcessorPil
+    import hashlib
+    from mme.config import get_spec
+    from planted import E2E_MODELS, e2e_inputs, graded_targets
+    from weights_gen import factor_product
+    caps, bs = 5, 32
+    out = {"models": np.array([m[0] for m in E2E_MODELS]), "caps": np.int64(caps), "batch_size": np.int64(bs)}
+    torch.set_num_threads(os.cpu_count() or 8)
+    for name, n, H in E2E_MODELS:
+        spec = get_spec(name)
+        key = name.replace("-", "_")
+        imgs, rows = e2e_inputs(spec, n, H, caps)
+        S = spec.vision.image_size
+        ip = (SiglipImageProcessorPil(size={"height": S, "width": S}) if spec.family == "siglip" else
+              CLIPImageProcessorPil(size={"shortest_edge": S}, crop_size={"height": S, "width": S}))
+        proc = RefProcessor(ip, spec.text.pad_id)
+        pil = [Image.fromarray(a) for a in imgs]
+        # 1. the fp32 reference's pooled features ahead of the fitted maps, batched as encode_data batches
+        hf = hf_model(spec, torch.float32)
+        fi, fc, ri = [], [], []
+        with torch.no_grad():
+            for s in range(0, n, bs):
+                pv = proc(images=pil[s:s + bs])["pixel_values"]
+                if spec.family == "clip":
+                    fi.append(hf.vision_model(pixel_values=pv).pooler_output)
+                else:
+                    head = hf.vision_model.head
+                    x = hf.vision_model(pixel_values=pv).last_hidden_state
+                    r = head.attention(head.probe.repeat(x.shape[0], 1, 1), x, x)[0]
+                    h = head.mlp.activation_fn(head.mlp.fc1(head.layernorm(r)))
+                    fi.append(h[:, 0])
+                    ri.append(r[:, 0])
+            # SigLIP pools the LAST position, a pad token for shorter rows, so a caption's feature depends on
+            # its batch's padded length: the T2I encode (main.py:554, its own batches) is fitted too
+            t2i_rows = rows[::caps]
+            for rr in ((rows,) if spec.family == "clip" else (rows, t2i_rows)):
+                for s in range(0, len(rr), bs):
+                    b = proc(text=rr[s:s + bs])
+                    if spec.family == "clip":
+                        fc.append(hf.text_model(**b).pooler_output)
+                    else:
+                        fc.append(hf.text_model(**b).last_hidden_state[:, -1])
+        Fi, Fc = torch.cat(fi).double().numpy(), torch.cat(fc).double().numpy()
+        if spec.family != "clip":  # a T2I row padded as in its all-captions batch has the same feature: drop it
+            def padded(rr):
+                return [max(len(r) for r in rr[s:s + bs]) for s in range(0, len(rr), bs) for _ in rr[s:s + bs]]
+            keep = np.array(padded(rows)[::caps]) != np.array(padded(t2i_rows))
+            Fc = np.concatenate([Fc[:len(rows)], Fc[len(rows):][keep]])
+        D = spec.proj_dim if spec.family == "clip" else spec.vision.hidden
+        zi, zc = graded_targets(n, caps, D, seed=0)
+        if spec.family == "clip":
+            Ti, Tc = zi, zc
+        else:  # image = r + fc2(h) + b2 = |r| z  ->  [h, 1] [W2, b2]^T = |r| z - r ; text = head(f) = z
+            R = torch.cat(ri).double().numpy()
+            Ti = np.median(np.linalg.norm(R, axis=1)) * zi - R
+            Tc = np.concatenate([zc, zc[::caps][keep]])
+            Fi = np.concatenate([Fi, np.ones((n, 1))], 1)
+            Fc = np.concatenate([Fc, np.ones((Fc.shape[0], 1))], 1)
+        ov = {}
+        for tag, F, T in (("img", Fi, Ti), ("txt", Fc, Tc)):
+            A, B = _fit_factors(F, T)
+            W = factor_product(A, B)
+            out[f"{key}_{tag}_A"], out[f"{key}_{tag}_B"] = A, B
+            out[f"{key}_{tag}_sha"] = np.array(hashlib.sha256(W.view(np.uint32).tobytes()).hexdigest()[:32])
+            if spec.family == "clip":
+                ov["visual_projection.weight" if tag == "img" else "text_projection.weight"] = W
+            elif tag == "img":
+                ov["vision_model.head.mlp.fc2.weight"], ov["vision_model.head.mlp.fc2.bias"] = W[:, :-1], W[:, -1]
+            else:
+                ov["text_model.head.weight"], ov["text_model.head.bias"] = W[:, :-1], W[:, -1]
+        del hf
+        # 2. the reference's chain with the fitted heads, bf16 (the reference's precision) and fp32
+        m_info = {"name": name, "type": spec.m_info["type"], "batch_size": bs}
+        out[f"{key}_params"] = np.array([n, caps, H, 41], np.int64)
+        out[f"{key}_cap_lens"] = np.array([len(r) for r in rows], np.int64)
+        out[f"{key}_cap_ids"] = np.concatenate(rows).astype(np.int64)
+        for tag, dtype in (("bf16", torch.bfloat16), ("f32", torch.float32)):
+            mdl = RefAdapter(hf_model(spec, dtype, overrides=ov))
+            main.DEVICE, main.DTYPE = "cpu", dtype
+            with torch.no_grad():
+                img_e, all_e = main.encode_data(mdl, proc, m_info, pil, rows)
+                _, t2i_e = main.encode_data(mdl, proc, m_info, [], rows[::caps])
+            if tag == "f32":
+                out[f"{key}_img_f32"], out[f"{key}_all_f32"], out[f"{key}_t2i_f32"] = (
+                    img_e.numpy(), all_e.numpy(), t2i_e.numpy())
+                continue
+            out[f"{key}_img_bf16"], out[f"{key}_all_bf16"], out[f"{key}_t2i_bf16"] = (
+                bf16_bits(img_e), bf16_bits(all_e), bf16_bits(t2i_e))
+            s_t2i = main.compute_similarity_scores(img_e, t2i_e, {"type": "dense"}, None)   # [n, n]  = t2i @ img.T
+            s_i2t = main.compute_similarity_scores(all_e, img_e, {"type": "dense"}, None)   # [n, 5n] = img @ all.T
+            s_sym = s_t2i.t().contiguous()
+            metrics = main.compute_metrics_detailed(s_t2i, s_i2t, s_sym, list(range(n)),
+                                                    {i: list(range(caps * i, caps * i + caps)) for i in range(n)},
+                                                    {i: i for i in range(n)}, [""] * n)
+            for p, s in (("t2i", s_t2i), ("i2t", s_i2t), ("sym", s_sym)):
+                v, _ = torch.topk(s, 11, dim=1)
+                ix = torch.stack([torch.topk(s[i], 10).indices for i in range(n)])  # compute_metrics_detailed's call
+                out[f"{key}_{p}_idx"], out[f"{key}_{p}_score"] = ix.numpy().astype(np.int32), v.numpy()
+                gaps = (v[:, :-1] - v[:, 1:]).min(1).values
+                print(f"e2e {name} {p}: top-11 min gap median {gaps.median():.3e} min {gaps.min():.3e}", flush=True)
+            keys = [k for k in metrics if not k.startswith("_")]
+            out["metric_names"] = np.array(keys)
+            out[f"{key}_metric_values"] = np.array([metrics[k] for k in keys], np.float64)
+            print(f"e2e {name}:", dict(zip(keys, out[f"{key}_metric_values"].round(2))), flush=True)
+        e16 = {k: bits_f32(out[f"{key}_{k}_bf16"]) for k in ("img", "all", "t2i")}
+        for k in ("img", "all", "t2i"):
+            c = (e16[k] * out[f"{key}_{k}_f32"]).sum(1) / np.linalg.norm(e16[k], axis=1)
+            print(f"e2e {name} {k}: bf16 vs fp32 reference cos min {c.min():.5f}", flush=True)
+    np.savez_compressed(os.path.join(HERE, "e2e_fitted.npz"), **out)
+    print("e2e_fitted.npz:", sum(v.nbytes for v in out.values()) / 1e6, "MB raw")
+
+
+def bits_f32(b):
+    return (np.asarray(b, np.uint16).astype(np.uint32) << 16).view(np.float32)
 
 
 # ------------------------------------------------------------------ retrieval
@@ -839,7 +990,7 @@ if __name__ == "__main__":
              "config0": lambda: make_config0(main), "edge": lambda: make_edge(main),
              "winoground": make_winoground, "bootstrap": lambda: make_bootstrap(main),
              "colpali_full": lambda: make_colpali_full(main), "torch_topk": make_torch_topk,
-             "dense_ties": lambda: make_dense_ties(main)}
+             "dense_ties": lambda: make_dense_ties(main), "e2e": lambda: make_e2e(main)}
     for name, fn in steps.items():
         if not only or name in only:
             fn()

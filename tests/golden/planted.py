@@ -124,5 +124,65 @@ def config0_inputs(spec, n_img: int = 64, caps: int = 5, seed: int = 21):
     return imgs, cap_rows
 
 
+E2E_MODELS = (("tiny-clip", 32, 112), ("tiny-siglip", 64, 112), ("OpenAI-CLIP-L", 64, 224), ("SigLIP-400M", 64, 224))
+
+
+def e2e_inputs(spec, n: int, H: int, caps: int = 5, seed: int = 41):
+    """Inputs of the end-to-end fixture (e2e_fitted.npz): n synthetic H x H u8 images and caps*n ragged
+    caption id rows (CLIP: [bos] + 1..L-2 ids + [eos]; SigLIP: 1..L-1 ids + [eos]) in main.py's layout
+    (caption j of image i at caps*i + j, T2I = caption 0)."""
+    from mme.processor import synthetic_images
+    t = spec.text
+    imgs = synthetic_images(n, H, H, seed=seed)
+    rng = np.random.default_rng(seed + 1)
+    if t.bos_id is not None:
+        lens = rng.integers(1, t.max_pos - 1, caps * n)
+        rows = [[t.bos_id] + rng.integers(1, min(t.bos_id, t.eos_id), int(L)).tolist() + [t.eos_id] for L in lens]
+    else:
+        lens = rng.integers(1, t.max_pos, caps * n)
+        rows = [rng.integers(2, t.vocab, int(L)).tolist() + [t.eos_id] for L in lens]
+    return imgs, rows
+
+
+GRADED_OWN_RANK = (0, 7)   # 0-based rank of the own image per caption table (t = l mod 2): R@1 50, R@5 50, R@10 100
+
+
+def graded_targets(n: int, caps: int, D: int, seed: int = 0, K: int = 12, delta: float = 0.038):
+    """Target joint embeddings with a GRADED score structure (the fitted projection heads of the
+    end-to-end fixture map the towers' pooled features onto these; make_goldens.make_e2e).
+
+    Image i -> u_i (orthonormal); caption (l, 0) -> sum_k L[lev_l(k)] u_{(l+k) mod n} + r u_null, so
+    a T2I row, a Sym row and the top of an I2T row see the K distinct levels L = delta*(K..1), spaced
+    delta apart, and every other score is 0. Caption tables t = l mod G (G = len(GRADED_OWN_RANK))
+    place the own image at GRADED_OWN_RANK[t]; the level map lev_t(k) = sigma((k + G*d_t) mod K) keeps
+    every Sym / I2T row a bijection onto the levels (the G residues never collide). Captions j >= 1
+    carry only 0.2*j*delta of their own image (below the I2T top-11) plus u_null. Returns float64
+    (img [n, D], cap [caps*n, D]) of unit norm."""
+    G = len(GRADED_OWN_RANK)
+    assert K % G == 0 and G * G <= K and n % G == 0 and n >= K and D >= n + 1
+    rng = np.random.default_rng(seed)
+    u = np.linalg.qr(rng.standard_normal((D, n + 1)))[0].T        # [n+1, D] orthonormal; u[n] = u_null
+    L = delta * np.arange(K, 0, -1, dtype=np.float64)             # level value by rank 0..K-1
+    assert (L ** 2).sum() < 1.0
+    # sigma: a fixed bijection of level indices with sigma(G*d_t) = own rank of table t
+    d = list(range(G))
+    sigma = {G * dt: GRADED_OWN_RANK[t] for t, dt in enumerate(d)}
+    rest_src = [x for x in range(K) if x not in sigma]
+    rest_dst = [x for x in range(K) if x not in sigma.values()]
+    perm = rng.permutation(len(rest_dst))
+    sigma.update({s: rest_dst[p] for s, p in zip(rest_src, perm)})
+    img = u[:n].copy()
+    cap = np.zeros((caps * n, D))
+    for l in range(n):
+        t = l % G
+        lev = [sigma[(k + G * d[t]) % K] for k in range(K)]
+        v = np.array([L[x] for x in lev])
+        cap[caps * l] = v @ u[(l + np.arange(K)) % n] + np.sqrt(1.0 - (v ** 2).sum()) * u[n]
+        for j in range(1, caps):
+            a = 0.2 * j * delta
+            cap[caps * l + j] = a * u[l] + np.sqrt(1.0 - a * a) * u[n]
+    return img, cap
+
+
 def bf16_sha(t: torch.Tensor) -> str:
     return hashlib.sha256(t.contiguous().view(torch.int16).numpy().tobytes()).hexdigest()[:32]

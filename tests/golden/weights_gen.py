@@ -136,6 +136,39 @@ def np_state_dict_colpali(spec, seed: int = 0) -> Dict[str, np.ndarray]:
     return sd
 
 
+def bf16_bits_to_f32(b: np.ndarray) -> np.ndarray:
+    return (np.asarray(b, np.uint16).astype(np.uint32) << 16).view(np.float32)
+
+
+def factor_product(a_bits: np.ndarray, b_bits: np.ndarray) -> np.ndarray:
+    """W = bf16(A @ B) for bf16 factors A [D, r], B [r, d] (tests/golden/e2e_fitted.npz): float64
+    outer products added in a fixed order with numpy's elementwise ufuncs (each op correctly
+    rounded, no BLAS), so every box rebuilds the same bits; the fixture stores their SHA-256."""
+    a = bf16_bits_to_f32(a_bits).astype(np.float64)
+    b = bf16_bits_to_f32(b_bits).astype(np.float64)
+    w = np.zeros((a.shape[0], b.shape[1]), np.float64)
+    for k in range(a.shape[1]):
+        w += np.multiply.outer(a[:, k], b[k])
+    return bf16_round(w.astype(np.float32))
+
+
+def fitted_overrides(spec, fx, key: str) -> Dict[str, np.ndarray]:
+    """The fitted projection heads of one model of e2e_fitted.npz, as state-dict entries (fp32 arrays of
+    bf16 values). CLIP: visual_projection / text_projection. SigLIP: the MAP head's mlp.fc2 (weight and
+    bias: the last factor column) and text_model.head (weight and bias)."""
+    import hashlib
+    wi = factor_product(fx[f"{key}_img_A"], fx[f"{key}_img_B"])
+    wt = factor_product(fx[f"{key}_txt_A"], fx[f"{key}_txt_B"])
+    for w, tag in ((wi, "img"), (wt, "txt")):
+        sha = hashlib.sha256(w.view(np.uint32).tobytes()).hexdigest()[:32]
+        assert sha == str(fx[f"{key}_{tag}_sha"]), f"{key} {tag} head rebuilt differently ({sha})"
+    if spec.family == "clip":
+        return {"visual_projection.weight": wi, "text_projection.weight": wt}
+    return {"vision_model.head.mlp.fc2.weight": np.ascontiguousarray(wi[:, :-1]),
+            "vision_model.head.mlp.fc2.bias": np.ascontiguousarray(wi[:, -1]),
+            "text_model.head.weight": np.ascontiguousarray(wt[:, :-1]), "text_model.head.bias": np.ascontiguousarray(wt[:, -1])}
+
+
 def torch_state_dict(spec, seed: int = 0, dtype=None):
     import torch
     dtype = dtype or torch.float32

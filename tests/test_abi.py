@@ -97,3 +97,29 @@ def test_no_unpadded_sgpr_vmem_hazards():
         if os.path.exists(lib):
             hits = asm_hazard_audit.audit_lib(lib)
             assert not hits, f"{name}: {len(hits)} unpadded pairs, first: {hits[0]}"
+
+
+def test_asm_hazard_audit_follows_control_flow():
+    """the audit's scanner on synthetic objdump text: straight-line, across a taken conditional
+    branch (objdump offset, pc + 4 + 4 * simm16) and an unconditional one, an SGPR pair written by
+    v_cmp_*_e64, a VOP3b carry-out, padding that suffices, and a target outside the listing (reported)."""
+    import sys
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import asm_hazard_audit as A
+
+    def dis(*ins):
+        return "0000000000001000 <_Zk>:\n" + "\n".join(f"\t{x:50s}// {0x1000 + 4 * i:012X}: 00000000"
+                                                        for i, x in enumerate(ins))
+    load = "buffer_load_dword v1, v2, s[8:11], s5 offen"
+    assert len(A.audit_text(dis("v_readlane_b32 s5, v0, 1", load))) == 1
+    assert not A.audit_text(dis("v_readlane_b32 s5, v0, 1", "s_nop 4", load))
+    assert not A.audit_text(dis("v_readlane_b32 s5, v0, 1", "s_mov_b32 s5, 0", load))        # rewritten first
+    # s_cbranch_scc0 1 at 0x1004 jumps to 0x100c, skipping the s_nop 7 on the taken path
+    assert len(A.audit_text(dis("v_readlane_b32 s5, v0, 1", "s_cbranch_scc0 1", "s_nop 7", load))) == 1
+    # an unconditional s_branch 1 at 0x1004 over the s_nop 7
+    assert len(A.audit_text(dis("v_readfirstlane_b32 s5, v0", "s_branch 1", "s_nop 7", load))) == 1
+    assert len(A.audit_text(dis("v_cmp_eq_u32_e64 s[10:11], v0, v1", load))) == 1               # descriptor pair
+    assert len(A.audit_text(dis("v_add_co_u32_e64 v3, s[4:5], v0, v1", "buffer_load_dword v1, v2, s[4:7], 0 offen"))) == 1
+    assert not A.audit_text(dis("v_cmp_eq_u32_e64 s[10:11], v0, v1", "buffer_load_dword v1, v2, s[12:15], 0 offen"))
+    hits = A.audit_text(dis("v_readlane_b32 s5, v0, 1", "s_cbranch_execz 300", "s_nop 7", "s_endpgm"))
+    assert len(hits) == 1 and "unresolved" in hits[0][2]

@@ -5,9 +5,11 @@ at --batch-size 32, then compute_similarity_scores + compute_metrics_detailed; m
 Embeddings: per-row cosine >= 0.999 against the reference's fp32 run through the
 drop-in surface (processor + get_*_features, mme.encode.encode_data) and the fast paths.
 Retrieval: the reference's own embeddings ranked on the device must reproduce its top-10 order and
-R@k (fp32 near-tie rule). Ranking of the device's own embeddings: rows decided beyond twice the
-score perturbation measured on that row must match; random weights leave few such rows, and the
-count is printed."""
+R@k (fp32 near-tie rule). The ranking of the device's OWN embeddings against the reference's chain is
+tests/test_gpu_e2e.py: with these random weights every embedding clusters and no row's top-11 gap
+exceeds the bf16 score noise (round 5's test here asserted on 0 decided rows), so that test fits the
+towers' last linear maps onto graded targets at this same geometry (OpenAI-CLIP-L, 64 x 320) and
+requires >= 80 % decided rows, all identical, and identical R@k."""
 import numpy as np
 import pytest
 import torch
@@ -68,29 +70,3 @@ def test_config0_retrieval_vs_reference(cuda, golden):
         assert np.abs(sc.cpu().numpy() - g[tag + "_score"][:, :10]).max() < 1e-5
     got = retrieval.compute_metrics(emb["img"], emb["t2i"], emb["all"])
     assert got == dict(zip([str(k) for k in g["metric_names"]], g["metric_values"]))
-
-
-def test_config0_ranking_of_device_embeddings(clip_l, golden):
-    """The device's own embeddings ranked on the device vs the reference's ranking. With random weights
-    the embeddings cluster tightly, so most rows' top-11 score gaps are below the bf16 embedding
-    noise (~1e-3): only rows decided beyond twice the score perturbation measured on that row must
-    match; the rest are reported."""
-    spec, model = clip_l
-    g = golden("config0_clip_l")
-    imgs, rows = config0_inputs(spec)
-    n, caps = imgs.shape[0], len(rows) // imgs.shape[0]
-    ie, ae = encode.encode_data(model, Processor(spec), {"type": "dense", "batch_size": 32}, list(imgs), rows)
-    _, te = encode.encode_data(model, Processor(spec), {"type": "dense", "batch_size": 32}, [], rows[::caps])
-    emb = {"img": ie.cuda(), "all": ae.cuda(), "t2i": te.cuda()}
-    for tag, qk, dk in (("t2i", "t2i", "img"), ("i2t", "img", "all"), ("sym", "img", "t2i")):
-        idx, _ = ops.sim_topk(emb[qk], emb[dk], 10)
-        idx = idx.cpu().numpy()
-        ref_idx, ref_sc = g[tag + "_idx"], g[tag + "_score"]
-        full = (emb[qk].float() @ emb[dk].float().T).cpu().numpy()
-        pert = np.abs(np.take_along_axis(full, ref_idx, 1) - ref_sc).max(1)              # per-row noise
-        gaps = ref_sc[:, :10] - ref_sc[:, 1:]
-        decided = (gaps > 2 * pert[:, None]).all(1)
-        same = (idx == ref_idx[:, :10]).all(1)
-        print(f"{tag}: {int(same.sum())}/{len(same)} rows identical; {int(decided.sum())} rows decided beyond the "
-              f"measured score noise (median {np.median(pert):.2e}), all of which must match")
-        assert same[decided].all()

@@ -1,0 +1,110 @@
+"""End-to-end parity: the device's own encode -> rank chain against the reference's CPU chain.
+
+tests/golden/e2e_fitted.npz holds, per model (tiny-clip, tiny-siglip, OpenAI-CLIP-L = BASELINE
+configs[0], SigLIP-400M = the headline model), the outputs of the reference's own main.encode_data
+(main.py:386-438, --batch-size 32) -> compute_similarity_scores (main.py:440-475) ->
+compute_metrics_detailed (main.py:305-383, v28 I2T orientation) at 64 images x 320 captions (tiny-clip
+32 x 160), with the last linear map of each tower fitted so the ranking is DECIDED beyond bf16 noise
+(make_goldens.make_e2e: graded targets, 12 levels 0.038 apart; R@1 / R@5 50 %, R@10 100 %).
+
+Here the device encodes the same inputs through the drop-in surface (Processor + get_*_features via
+mme.encode.encode_data) and through the fast paths (u8 images resident, id tables + lengths), ranks its
+OWN embeddings on the device (mme_sim_topk) and must reproduce, per protocol:
+  * a row is "decided" when every gap in the reference's top-11 exceeds twice the largest score
+    perturbation measured on that row (device score - reference score over the reference's top-11);
+    at least 80 % of the rows must be decided, and the count is printed;
+  * every decided row's top-10 is identical in order;
+  * R@1 / R@5 / R@10 are identical to the reference's (mme.retrieval.compute_metrics on the device).
+"""
+import numpy as np
+import pytest
+import torch
+
+from helpers import bits_to_f32, row_cos
+from planted import e2e_inputs
+from mme import encode, get_spec, ops, retrieval
+from mme.models import CLIPModel, SiglipModel
+from mme.processor import Processor
+from weights_gen import fitted_overrides, torch_state_dict
+
+pytestmark = pytest.mark.gpu
+
+DECIDED_MIN = 0.8
+
+
+@pytest.fixture(scope="module")
+def fx(golden):
+    return golden("e2e_fitted")
+
+
+def _model(spec, fx, key):
+    sd = torch_state_dict(spec, 0)
+    for k, v in fitted_overrides(spec, fx, key).items():
+        assert sd[k].shape == v.shape, k
+        sd[k] = torch.from_numpy(v)
+    cls = SiglipModel if spec.family == "siglip" else CLIPModel
+    return cls.from_spec(spec, device="cuda", state_dict={k: v.to(torch.bfloat16) for k, v in sd.items()})
+
+
+def _check_ranking(fx, key, emb, label):
+    caps = int(fx["caps"])
+    for tag, qk, dk in (("t2i", "t2i", "img"), ("i2t", "img", "all"), ("sym", "img", "t2i")):
+        idx, _ = ops.sim_topk(emb[qk], emb[dk], 10)
+        idx = idx.cpu().numpy()
+        ref_idx, ref_sc = fx[f"{key}_{tag}_idx"], fx[f"{key}_{tag}_score"]
+        full = (emb[qk].float() @ emb[dk].float().T).cpu().numpy()
+        # the reference's top-11 columns: its own scores recomputed from its bf16 embeddings
+        # (compute_similarity_scores: txt.float() @ img.float().T), checked against the stored scores
+        rq, rd = (torch.from_numpy(bits_to_f32(fx[f"{key}_{k}_bf16"])) for k in (qk, dk))
+        rv, cols = torch.topk(rq @ rd.T, 11, dim=1)
+        assert np.abs(rv.numpy() - ref_sc).max() < 1e-5 and np.array_equal(cols[:, :10].numpy(), ref_idx)
+        cols = cols.numpy()
+        pert = np.abs(np.take_along_axis(full, cols, 1) - ref_sc).max(1)
+        gaps = ref_sc[:, :10] - ref_sc[:, 1:]
+        decided = (gaps > 2 * pert[:, None]).all(1)
+        same = (idx == ref_idx).all(1)
+        n = len(same)
+        print(f"{key} {label} {tag}: {int(decided.sum())}/{n} rows decided (score noise median {np.median(pert):.2e}, "
+              f"max {pert.max():.2e}; reference top-11 gap min {gaps.min():.2e}); {int(same.sum())}/{n} rows identical; "
+              f"decided rows differing: {int((decided & ~same).sum())}")
+        assert decided.mean() >= DECIDED_MIN, f"{key} {tag}: only {int(decided.sum())}/{n} rows decided"
+        assert same[decided].all(), f"{key} {tag}: decided rows {np.nonzero(decided & ~same)[0].tolist()} differ"
+    got = retrieval.compute_metrics(emb["img"], emb["t2i"], emb["all"], caps)
+    want = dict(zip([str(k) for k in fx["metric_names"]], fx[f"{key}_metric_values"]))
+    print(f"{key} {label}: R@k device {got}")
+    assert got == want
+
+
+@pytest.mark.parametrize("name", ["tiny-clip", "tiny-siglip", "OpenAI-CLIP-L", "SigLIP-400M"])
+def test_e2e_device_chain_vs_reference(cuda, fx, name):
+    spec = get_spec(name)
+    key = name.replace("-", "_")
+    n, caps, H, seed = (int(x) for x in fx[f"{key}_params"])
+    bs = int(fx["batch_size"])
+    imgs, rows = e2e_inputs(spec, n, H, caps, seed=seed)
+    lens = fx[f"{key}_cap_lens"]
+    assert [len(r) for r in rows] == lens.tolist() and np.array_equal(np.concatenate(rows), fx[f"{key}_cap_ids"])
+    model = _model(spec, fx, key)
+    m_info = {"name": name, "type": spec.m_info["type"], "batch_size": bs}
+    # 1. the drop-in surface: processor + get_*_features through encode_data (main.py:386-438)
+    ie, ae = encode.encode_data(model, Processor(spec), m_info, list(imgs), rows)
+    _, te = encode.encode_data(model, Processor(spec), m_info, [], rows[::caps])
+    surf = {"img": ie, "all": ae, "t2i": te}
+    for k, got in surf.items():
+        c32 = row_cos(got, torch.from_numpy(fx[f"{key}_{k}_f32"]))
+        c16 = row_cos(got, torch.from_numpy(bits_to_f32(fx[f"{key}_{k}_bf16"])))
+        print(f"{key} {k}: cos vs reference fp32 min {c32.min():.5f}, vs reference bf16 min {c16.min():.5f}")
+        assert c32.min() >= 0.999 and c16.min() >= 0.999
+    _check_ranking(fx, key, {k: v.cuda() for k, v in surf.items()}, "surface")
+    # 2. the fast paths the bench times: u8 images resident, id table + lengths at the reference's batches
+    L = int(lens.max())
+    ids = torch.full((len(rows), L), spec.text.pad_id, dtype=torch.int64)
+    for i, r in enumerate(rows):
+        ids[i, : len(r)] = torch.tensor(r)
+    fast = {"img": model.encode_images(torch.from_numpy(imgs).cuda()),
+            "all": model.encode_texts(ids.cuda(), torch.from_numpy(lens), ref_batch=bs),
+            "t2i": model.encode_texts(ids[::caps].contiguous().cuda(), torch.from_numpy(lens[::caps].copy()),
+                                      ref_batch=bs)}
+    for k in fast:
+        assert row_cos(fast[k].cpu(), surf[k]).min() >= 0.9999, k
+    _check_ranking(fx, key, fast, "fast path")

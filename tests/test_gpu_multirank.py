@@ -35,3 +35,13 @@ def test_multirank_bench_equals_single_rank(cuda, world):
     assert many["n_gpus"] == world and many["process_group"]["ranks"] == world
     assert many["recall"] == one["recall"]
     assert many["parity"]["recall_identical"] and one["parity"]["recall_identical"]
+    # the line names every rank's phases and share (verdict r5 item 6): world 3 shards 203 unevenly
+    pr = many["per_rank"]
+    print(f"world {world}: per-rank phases {json.dumps(pr)}")
+    for key in ("encode_images_s", "encode_texts_s", "retrieval_s", "n_images", "n_captions", "timed_s"):
+        assert len(pr[key]) == world, key
+    assert sum(pr["n_images"]) == 203 and pr["n_captions"] == [5 * k for k in pr["n_images"]]
+    assert all(x > 0 for x in pr["encode_images_s"] + pr["encode_texts_s"] + pr["retrieval_s"])
+    assert max(pr["encode_images_s"]) == pytest.approx(many["encode_images_s"], abs=1e-4)
+    assert 0 <= pr["slowest_rank"] < world
+    assert one["per_rank"]["n_images"] == [203]

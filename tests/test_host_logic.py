@@ -103,20 +103,44 @@ def test_processor_delegates_strings_to_the_tokenizer():
     assert proc.tokenize(["a cat"]) == [[b, 101, 103, e]]
 
 
+class GemmaLikeStub:
+    """Stand-in for Gemma's tokenizer on whole ColPali query strings: <bos> / <pad> / newline map to the
+    spec's special ids, every other whitespace-separated piece to 100 + its length; records the strings."""
+
+    def __init__(self, spec):
+        self.spec, self.calls = spec, []
+        self.bos_token, self.pad_token = "<bos>", "<pad>"
+
+    def __call__(self, batch, add_special_tokens=True, **kw):
+        import re
+        self.calls.append(dict(batch=list(batch), add_special_tokens=add_special_tokens))
+        rows = []
+        for s in batch:
+            r = []
+            for piece in re.findall(r"<bos>|<pad>|\n|[^\s<]+", s):
+                r.append({"<bos>": self.spec.bos_id, "<pad>": self.spec.pad_id,
+                          "\n": self.spec.newline_id}.get(piece, 100 + len(piece)))
+            rows.append(r)
+        return {"input_ids": rows}
+
+
 def test_colpali_processor_tokenizer_contract():
-    """ColPali queries: the tokenizer encodes the caption body only (add_special_tokens=False); the
-    ColPali layout (bos, prefix, augmentation pads, newline) and left padding come from the spec."""
+    """ColPali string queries: laid out as ColPaliProcessor.__call__ does,
+    bos + "Question: " + query + 10 pads + newline, and tokenized as ONE string (so the prefix / query
+    seam merges as the reference's SentencePiece sees it); id lists keep the spec layout; left padding."""
     from mme.colpali_encoder import ColPaliProcessor
     spec = get_spec("tiny-colpali")
     with pytest.raises(ValueError, match="tokenizer"):
         ColPaliProcessor(spec, device="cpu").process_queries(["a cat"])
-    tok = StubTokenizer(bos=spec.bos_id)
+    tok = GemmaLikeStub(spec)
     proc = ColPaliProcessor(spec, device="cpu", tokenizer=tok)
     bf = proc.process_queries(["a cat", [11, 12, 13]])
-    assert tok.calls[-1]["add_special_tokens"] is False and tok.calls[-1]["n"] == 1
-    rows = [list(spec.query_tokens([101, 103])), list(spec.query_tokens([11, 12, 13]))]
+    assert tok.calls[-1] == {"batch": ["<bos>Question: a cat" + "<pad>" * 10 + "\n"], "add_special_tokens": False}
+    rows = [[spec.bos_id, 109, 101, 103] + [spec.pad_id] * 10 + [spec.newline_id],
+            list(spec.query_tokens([11, 12, 13]))]
     L = max(map(len, rows))
     assert bf["input_ids"].tolist() == [[spec.pad_id] * (L - len(r)) + r for r in rows]
+    assert bf["attention_mask"].tolist() == [[0] * (L - len(r)) + [1] * len(r) for r in rows]
     hashed = ColPaliProcessor(spec, device="cpu", allow_hash_tokenizer=True).process_queries(["a cat"])
     assert hashed["input_ids"].shape[0] == 1
 
@@ -172,10 +196,16 @@ def test_csv_timing_columns_follow_main_py(monkeypatch):
     assert harness.timing_columns(10, 100.0, 104.0, 109.0) == {
         "Time": 9.0, "QPS": 2.5, "Encoding_Time": 4.0, "Img_per_sec": 2.5}
     ticks = iter([100.0, 101.0, 104.0, 109.0])  # start, after warmup, after encodes, after metrics
-    calls = []
+    calls, warm = [], []
 
     class Fake:
         spec = types.SimpleNamespace(name="fake")
+
+        def encode_images(self, imgs, **kw):
+            warm.append(("img", imgs.clone()))
+
+        def encode_texts(self, ids, lens=None, **kw):
+            warm.append(("txt", ids.clone()))
 
     def fake_encode(model, imgs, ids, lens, cpi, **kw):
         calls.append(imgs.shape[0])
@@ -184,12 +214,30 @@ def test_csv_timing_columns_follow_main_py(monkeypatch):
     monkeypatch.setattr(harness, "encode_job", fake_encode)
     monkeypatch.setattr(harness, "compute_metrics", lambda *a: {k: 1.0 for k in METRIC_KEYS})
     tm = {}
-    row = harness.run_benchmark(Fake(), torch.zeros(10, 2, 2, 3, dtype=torch.uint8),
-                                torch.zeros(50, 4, dtype=torch.int64), timings=tm, clock=lambda: next(ticks))
-    assert calls == [2, 10]  # warmup on two items, then the job
+    imgs = torch.arange(10 * 2 * 2 * 3, dtype=torch.int64).reshape(10, 2, 2, 3).to(torch.uint8)
+    ids = torch.arange(50 * 4, dtype=torch.int64).reshape(50, 4)
+    row = harness.run_benchmark(Fake(), imgs, ids, timings=tm, clock=lambda: next(ticks))
+    assert calls == [10]  # the job; the warmup is main.py:537-541's, not an encode_job
+    # warmup: [images[0]] * 2 then [t2i_captions[0]] * 2 (T2I caption 0 = all_captions[0])
+    assert [w[0] for w in warm] == ["img", "txt"]
+    assert torch.equal(warm[0][1], imgs[[0, 0]]) and torch.equal(warm[1][1], ids[[0, 0]])
     assert (row["Time"], row["QPS"], row["Encoding_Time"], row["Img_per_sec"]) == (9.0, 2.5, 4.0, 2.5)
-    assert tm == {"warmup_s": 1.0, "encode_s": 3.0, "retrieval_s": 5.0, "e2e_img_per_sec": 10 / 8.0}
+    assert tm == {"warmup_s": 1.0, "encode_s": 3.0, "retrieval_s": 5.0, "bootstrap_s": 0.0,
+                  "e2e_img_per_sec": 10 / 8.0}
     assert list(row)[-5:] == ["Time", "QPS", "Encoding_Time", "Img_per_sec", "_failure_analysis"]
+    # with the bootstrap, the v28 rate stops after the score matrices: bootstrap_s apart
+    from mme import bootstrap as mb
+    ticks = iter([100.0, 101.0, 104.0, 106.0, 120.0])
+    monkeypatch.setattr(mb, "full_scores", lambda *a: (None, None))
+    monkeypatch.setattr(mb, "sample_indices", lambda *a: None)
+    monkeypatch.setattr(mb, "bootstrap_hits", lambda *a: None)
+    monkeypatch.setattr(mb, "bootstrap_row", lambda *a, **k: {})
+    monkeypatch.setattr(harness, "_sync", lambda: None)
+    tm = {}
+    monkeypatch.setattr(harness, "encode_job", lambda *a, **k: (imgs, None, None))
+    harness.run_benchmark(Fake(), imgs, ids, timings=tm, n_iterations=3, clock=lambda: next(ticks))
+    assert tm == {"warmup_s": 1.0, "encode_s": 3.0, "retrieval_s": 2.0, "bootstrap_s": 14.0,
+                  "e2e_img_per_sec": 10 / 5.0}
 
 
 def test_registry_flops_match_survey():
@@ -314,23 +362,23 @@ def test_exec_batch_keeps_gemm_operands_under_4gib(n):
 
 
 def test_compare_topk_oracle_only_exact_ties():
-    """an exact tie in the oracle's top-(k+1) on a row the device did not flag is exempt (a
-    near tie) only where the device's own scores differ at that place; where they are equal too, the
-    device missed a tie and a differing order stays decisive."""
+    """an exact tie in the oracle's top-(k+1) on a row the device did not flag is a near
+    tie (the device's summation order separated the pair) and is reported in oracle_only; rows the device
+    flagged replay torch's order and are never exempt; a row whose OWN device scores tie but which
+    tie_rows did not flag is a tie_rows defect, reported in unflagged."""
     from oracle import retrieval as R
     ref_idx = np.array([[0, 1, 2], [0, 1, 2]])
     ref_sc = np.array([[3.0, 2.0, 2.0], [3.0, 2.0, 2.0]], np.float32)     # exact tie at places 2 / 3
     dev_idx = np.array([[0, 2], [0, 2]])                                    # the tied pair swapped
     dev_sc = np.array([[3.0, 2.0, 1.9999999], [3.0, 2.0, 2.0]], np.float32)
-    only = []
+    only, missed = [], []
     same, near = R.compare_topk(dev_idx, ref_idx, ref_sc, exact_rows=np.zeros(2, bool), dev_score=dev_sc,
-                                oracle_only=only)
-    assert only == [0, 1] and not same.any()
-    assert near.tolist() == [True, False]   # row 1: the device's scores tie too -> not exempt
-    _, near_old = R.compare_topk(dev_idx, ref_idx, ref_sc, exact_rows=np.zeros(2, bool))
-    assert near_old.all()                   # without device scores: the round-4 rule
-    _, near_flagged = R.compare_topk(dev_idx, ref_idx, ref_sc, exact_rows=np.ones(2, bool), dev_score=dev_sc)
-    assert not near_flagged.any()           # rows the device flagged replay torch's order: never exempt
+                                oracle_only=only, unflagged=missed)
+    assert only == [0, 1] and not same.any() and near.all()
+    assert missed == [1]                    # row 1: the device's own scores tie, tie_rows did not flag it
+    _, near_flagged = R.compare_topk(dev_idx, ref_idx, ref_sc, exact_rows=np.ones(2, bool), dev_score=dev_sc,
+                                     unflagged=missed)
+    assert not near_flagged.any() and missed == [1]   # flagged rows: never exempt, nothing unflagged
 
 
 def test_gelu_erfc_fit_accuracy():
