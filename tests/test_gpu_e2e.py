@@ -16,6 +16,8 @@ OWN embeddings on the device (mme_sim_topk) and must reproduce, per protocol:
   * every decided row's top-10 is identical in order;
   * R@1 / R@5 / R@10 are identical to the reference's (mme.retrieval.compute_metrics on the device).
 """
+import warnings
+
 import numpy as np
 import pytest
 import torch
@@ -48,6 +50,7 @@ def _model(spec, fx, key):
 
 def _check_ranking(fx, key, emb, label):
     caps = int(fx["caps"])
+    summary = []
     for tag, qk, dk in (("t2i", "t2i", "img"), ("i2t", "img", "all"), ("sym", "img", "t2i")):
         idx, _ = ops.sim_topk(emb[qk], emb[dk], 10)
         idx = idx.cpu().numpy()
@@ -67,12 +70,16 @@ def _check_ranking(fx, key, emb, label):
         print(f"{key} {label} {tag}: {int(decided.sum())}/{n} rows decided (score noise median {np.median(pert):.2e}, "
               f"max {pert.max():.2e}; reference top-11 gap min {gaps.min():.2e}); {int(same.sum())}/{n} rows identical; "
               f"decided rows differing: {int((decided & ~same).sum())}")
+        summary.append(f"{tag} {int(decided.sum())}/{n} decided, {int(same.sum())}/{n} identical")
         assert decided.mean() >= DECIDED_MIN, f"{key} {tag}: only {int(decided.sum())}/{n} rows decided"
         assert same[decided].all(), f"{key} {tag}: decided rows {np.nonzero(decided & ~same)[0].tolist()} differ"
     got = retrieval.compute_metrics(emb["img"], emb["t2i"], emb["all"], caps)
     want = dict(zip([str(k) for k in fx["metric_names"]], fx[f"{key}_metric_values"]))
     print(f"{key} {label}: R@k device {got}")
     assert got == want
+    # the counts in the suite's own output (pytest's warnings summary shows under -q too)
+    warnings.warn(f"e2e {key} {label}: " + "; ".join(summary) + f"; R@1/5/10 identical ({got['T2I_R@1']:.1f} / "
+                  f"{got['T2I_R@5']:.1f} / {got['T2I_R@10']:.1f} T2I)")
 
 
 @pytest.mark.parametrize("name", ["tiny-clip", "tiny-siglip", "OpenAI-CLIP-L", "SigLIP-400M"])

@@ -474,8 +474,9 @@ def test_gemm_activation_vs_float64(cuda, M, N, act):
     """The epilogue activations on exactly representable pre-activations: A[m, 0] = x_m (bf16), B[n, 0] = 1,
     everything else 0, so acc = x_m exactly and the output is bf16(act(x_m)) (every column the same). Against
     the float64 formula rounded to bf16: gelu_tanh / quick_gelu on v_exp_f32 + v_rcp_f32, gelu_erf
-    (nn.GELU's exact form, LAION-CLIP-H) through the branch-free erfc fit of common.h (round 5; libm erff
-    before): >= 99.5 % bit-identical, the rest one bf16 ulp, over x in [-10, 10] and the tails."""
+    (nn.GELU's exact form, LAION-CLIP-H) through the sigmoid-of-polynomial form of common.h (round 6; an
+    erfc fit in round 5, libm erff before): >= 99.5 % bit-identical, the rest one bf16 ulp, over x in
+    [-10, 10] and the tails (the fp32-level bound: test_gemm_gelu_erf_fp32_accuracy)."""
     K = 64
     x = torch.cat([torch.linspace(-10, 10, M - 64, device="cuda"), torch.logspace(-6, 1.2, 64, device="cuda")])
     xb = x.to(torch.bfloat16)
@@ -499,6 +500,35 @@ def test_gemm_activation_vs_float64(cuda, M, N, act):
     err = (got.float() - rb.float()).abs()
     print(f"act {act}: {same:.5f} bit-identical to the float64 formula, max err / ulp {(err / ulp).max().item():.2f}")
     assert same >= 0.995 and bool((err <= ulp * 1.01).all())
+
+
+def test_gemm_gelu_erf_fp32_accuracy(cuda):
+    """The exact-erf GELU (act 3, csrc/common.h gelu_erf2) at fp32 resolution, through the GEMM's fp32-output
+    epilogue (the same device function every fc1 epilogue inlines): A[m, 0] = x_m exactly (bf16 values over
+    [-12, 12] and a log grid near 0), B[n, 0] = 1. Erf-equivalent absolute error 2 |g - x Phi(x)| / |x| against
+    float64 below 6e-7 (host restatement 3.5e-7 with correctly rounded exp2 / rcp; the device's v_exp_f32 /
+    v_rcp_f32 are 1 ulp), and within 7e-7 of torch's own fp32 0.5 x (1 + erf(x / sqrt2)) on the device."""
+    K = 64
+    xs = torch.cat([torch.linspace(-12, 12, 60000, device="cuda"), torch.logspace(-3, 1.1, 4000, device="cuda"),
+                    -torch.logspace(-3, 1.1, 4000, device="cuda")]).to(torch.bfloat16)
+    xs = xs[xs.float().abs() > 1e-3]
+    M = xs.numel()
+    A = torch.zeros(M, K, device="cuda", dtype=torch.bfloat16)
+    A[:, 0] = xs
+    B = torch.zeros(8, K, device="cuda", dtype=torch.bfloat16)
+    B[:, 0] = 1
+    out = ops.gemm(A, B, None, act=3, out_f32=True)
+    g = out[:, 0].double()
+    xd = xs.double()
+    ref = 0.5 * xd * torch.special.erfc(-xd / math.sqrt(2))
+    xf = xs.float()
+    gt = (xf * 0.5 * (1 + torch.erf(xf * 0.7071067811865476))).double()
+    e_ours = (2 * (g - ref).abs() / xd.abs()).max().item()
+    e_torch = (2 * (gt - ref).abs() / xd.abs()).max().item()
+    e_diff = (2 * (g - gt).abs() / xd.abs()).max().item()
+    print(f"gelu_erf fp32: erf-equivalent abs error {e_ours:.3g} (torch fp32 formula on the device {e_torch:.3g}); "
+          f"difference from torch {e_diff:.3g}")
+    assert e_ours < 6e-7 and e_diff < 7e-7
 
 
 @pytest.mark.parametrize("M,N,K,act", [(303993, 4352, 1152, 1), (70001, 4352, 1152, 2), (5000, 5120, 1280, 2),
