@@ -137,9 +137,10 @@ __device__ __forceinline__ f32x2 pk_fma(f32x2 a, f32x2 b, f32x2 c) { return __bu
 // gelu(x) = x Phi(x) (nn.GELU(approximate="none"), the ViT-H / LAION-CLIP-H / MetaCLIP MLP) as a sigmoid:
 // Phi(x) = 1 / (1 + 2^(x P(x^2))) with x P(x^2) ~= -log2(e) logit(Phi(x)), P of degree 6 in x^2
 // (tools/gelu_erf_fit.py: minimax of |dPhi| on |x| <= 6.2 by linear programming; fit error 1.6e-8 in
-// Phi). Neither tail loses digits to the cancellation of 1 + erf(x / sqrt2): the negative tail is a
-// rcp of a large number. x P(x^2) is monotone, so no clamp: past |x| ~ 6 v_exp_f32 saturates to 0 or
-// +inf and v_rcp_f32(inf) = 0. Cost: the gelu_tanh form (one exp, one add, one rcp, three multiplies)
+// Phi). The error is absolute (minimax in |dPhi|): far in the negative tail, where |gelu| < 1.5e-5 and
+// torch's own 0.5 x (1 + erf) loses its digits to cancellation, the relative error grows (5 % at x = -5);
+// x P(x^2) is monotone, so no clamp: v_exp_f32 saturates to 0 or +inf and v_rcp_f32(inf) = 0 (gelu = x past
+// x ~ 8, -0 below x ~ -8). Cost: the gelu_tanh form (one exp, one add, one rcp, three multiplies)
 // plus five packed FMAs -- round 5's Numerical Recipes erfc fit (t = 1 / (1 + z / 2), nine FMAs of P(t),
 // exp, select) took +19 % over bias-only on LAION's fc1, the tanh form +7 %
 // (profiles/r05_v24_fc1_activation_cost.log). Accuracy in float32 (erf-equivalent absolute error

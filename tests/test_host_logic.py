@@ -391,7 +391,10 @@ def test_gelu_erf_accuracy():
     1 ulp). Against float64 x Phi(x) on [-12, 12]: the erf-equivalent absolute error 2 |g - x Phi(x)| / |x|
     stays below 4e-7 (3.5e-7; round 5's erfc fit 3.9e-7; torch's own fp32 formula 0.5 x (1 + erf(x / sqrt2))
     with a correctly rounded erf 2.1e-7), and our erf-equivalent differs from torch's fp32 one by less
-    than 5e-7 (4 ulp of fp32 at 1.0; the two errors add where their signs differ); both tails exact."""
+    than 5e-7 (4 ulp of fp32 at 1.0; the two errors add where their signs differ). The bound is absolute: the
+    fit is minimax in |dPhi|, so far in the negative tail (x < -4.5, |gelu| < 1.5e-5) the relative error grows
+    (5 % at x = -5, where torch's own fp32 formula is off by ~10 %), and past x ~ -8 the output is -0 (the true
+    value < 1e-14 in magnitude); past x ~ 8 it is exactly x."""
     import re
     import sys
     from scipy.special import erf, ndtr
