@@ -565,7 +565,8 @@ def test_gemm_dispatched_fc1_bit_identical_to_pipe6(cuda, M, N, K, act):
 
 
 @pytest.mark.parametrize("M,N,K", [(116935, 1280, 1280), (116935, 1280, 5120), (5000, 3840, 1280), (300, 1024, 1024),
-                                   (20000, 1152, 1152), (20000, 3456, 1152)])
+                                   (20000, 1152, 1152), (20000, 3456, 1152), (20111, 1152, 4352), (4000, 384, 4352),
+                                   (303993, 1152, 1152)])
 def test_gemm_form95_bit_identical_to_pipe6(cuda, M, N, K):
     """The production dispatch (pipe9 / pipe10 with every epilogue compiled for its operand set:
     bias, residual + the next LayerNorm's row statistics, LayerNorm fold), form 93 (the same kernels
