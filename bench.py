@@ -82,8 +82,9 @@ def parse():
                    help="A/B only: run every mx8 GEMM call with this libmme mx kernel form (mme.ops.kernel_forms; "
                         "11 = mx11, 15 = mx11 with the bias loaded up front); reported on the line")
     p.add_argument("--attn-form", type=int, default=None,
-                   help="A/B only: run every attention call with this libmme kernel form (mme.ops.kernel_forms; "
-                        "30 + kind forces a kernel kind); reported on the line")
+                   help="A/B only: run every attention call with T > 128 (the vision towers; text attention keeps "
+                        "the production dispatch) with this libmme kernel form (mme.ops.kernel_forms "
+                        "attention_long; 30 + kind forces a kernel kind); reported on the line")
     return p.parse_args()
 
 
@@ -586,7 +587,7 @@ def main():
         from mme import ops as _ops
         _forms = contextlib.ExitStack()
         _forms.enter_context(_ops.kernel_forms(**({"gemm": args.gemm_form} if args.gemm_form is not None else {}),
-                                               **({"attention": args.attn_form} if args.attn_form is not None else {}),
+                                               **({"attention_long": args.attn_form} if args.attn_form is not None else {}),
                                                **({"mx": args.mx_form} if args.mx_form is not None else {})))
     _, _, local = launch.env_rank_world()
     if args.same_device:

@@ -35,10 +35,11 @@ extern "C" {
 #define MME_ERR_HIP 2         /* HIP runtime error at launch               */
 #define MME_ERR_UNSUPPORTED 3 /* valid request this build does not handle  */
 
-#define MME_ABI_VERSION 8  /* 6: mme_gemm_res_stats row_part is [M][N / 64][2]; 7: mme_build_flags, mme_topk_rows_torch;
+#define MME_ABI_VERSION 9  /* 6: mme_gemm_res_stats row_part is [M][N / 64][2]; 7: mme_build_flags, mme_topk_rows_torch;
                               8: mme_recall_hits skip mask, mme_sim_scores, mme_tie_rows; per-call kernel
                                  forms (mme_*_form) replace the process-global *_variant switches, which
-                                 remain in the development build only */
+                                 remain in the development build only;
+                              9: mme_attention_qs (+ _form), Q pre-scaled */
 
 /* mme_build_flags() bits */
 #define MME_BUILD_DEV 1 /* development / diagnostic kernel forms compiled in (libmme_dev.so) */
@@ -144,6 +145,14 @@ int mme_layernorm(const void* x, int ldx, const void* gamma, const void* beta, v
 int mme_attention(const void* qkv, int ld_qkv, void* out, int ld_out, int B, int T, int H, int hd,
                   const int32_t* seq_lens, int causal, float scale, void* stream);
 
+/* mme_attention with Q pre-scaled (ABI 9): the Q columns of qkv already hold q * scale * log2(e)
+ * (mme/ops.py LNFolded(row_scale=...) folds the factor into the Q rows of the projection before its
+ * single bf16 rounding), so the kernels compute exp2(Q'K^T - M) and hd 72 runs kind 98, whose QK^T
+ * MFMA also subtracts the running max (Q^T row 72 = -M against a ones row of K): the per-score FMA of
+ * the softmax goes. Same masks, outputs and errors as mme_attention. */
+int mme_attention_qs(const void* qkv, int ld_qkv, void* out, int ld_out, int B, int T, int H, int hd,
+                     const int32_t* seq_lens, int causal, void* stream);
+
 /* Per-call kernel forms (ABI 8; bit-identity tests and A/B measurements). Each takes the
  * arguments of its plain entry point after an int `form`; the library holds no switch
  * (the plain entry points always run the production dispatch):
@@ -174,6 +183,8 @@ int mme_gemm_res_stats_form(int form, const void* A, int lda, const void* B, int
                             float* row_stats, void* stream);
 int mme_attention_form(int form, const void* qkv, int ld_qkv, void* out, int ld_out, int B, int T, int H, int hd,
                        const int32_t* seq_lens, int causal, float scale, void* stream);
+int mme_attention_qs_form(int form, const void* qkv, int ld_qkv, void* out, int ld_out, int B, int T, int H, int hd,
+                          const int32_t* seq_lens, int causal, void* stream);
 
 /* SigLIP MAP pooling-head attention: one probe query per head against the
  * T keys/values of each image. q: bf16 [H*hd] (already projected);

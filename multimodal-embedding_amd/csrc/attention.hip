@@ -1394,12 +1394,18 @@ __global__ __launch_bounds__(256, 2) void attn_short_pf_kernel(AttnArgs a, int u
 // and is not built.
 // THR (round 4, kinds 86-88): rescale O only when a query's running max grows by more than 2^8 in the
 // exp2 domain (attn_hyb_kernel's XT 2; P <= 256 otherwise, the weight sums share the stale max).
-template <int HD, int NW, int MINW, bool PRIO, bool DPV = false, bool PF = false, bool SKIP = false, bool THR = false>
+template <int HD, int NW, int MINW, bool PRIO, bool DPV = false, bool PF = false, bool SKIP = false, bool THR = false,
+          bool BIAS = false>
 __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(MINW))) void attn_m32_kernel(AttnArgs a) {
     constexpr int NSTG = DPV ? 3 : 2;
     constexpr bool ONES = HD % 32 != 0;
     constexpr int NCHL = HD / 8;                    // K / V planes with data
-    constexpr int NKS = (HD + 15) / 16;             // QK^T k-steps of 16
+    // BIAS (round 6, with THR; Q pre-scaled by the caller, mme_attention_qs): attn_hyb_kernel's XT 4 --
+    // Q^T row HD holds -M (the running max as a bf16 value) against a ones row of K, so the QK^T MFMAs
+    // return c s - M. Row HD lies in the zero padding of the last k-step at hd 72; hd 80 adds a k-step.
+    static_assert(!BIAS || (THR && !DPV && !PF && HD % 32 != 0), "BIAS: threshold rescale, plain loop, hd 72 / 80");
+    constexpr int NKS = (HD + 15) / 16 + (BIAS && HD % 16 == 0 ? 1 : 0);  // QK^T k-steps of 16
+    constexpr int KSB = HD / 16, HHB = (HD % 16) / 8;  // BIAS: Q^T row HD = k-step KSB, lane half HHB, element 0
     constexpr int NDB = (HD + (ONES ? 1 : 0) + 31) / 32;  // O^T d-blocks of 32
     constexpr int NVP = 4 * NDB;                    // V planes read (data, ones, zero padding)
     constexpr int TILE = (NCHL + NVP) * 1024;
@@ -1412,6 +1418,7 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(MINW)))
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int r = lane & 31, hh = lane >> 5;
+    float mb = 0.f;  // BIAS: the running max M that Q^T row HD holds as -M
     const int nqb = (a.T + QB - 1) / QB;
     int id;
     {
@@ -1470,6 +1477,9 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(MINW)))
     const unsigned lds0 = (unsigned)(uintptr_t)(LDS_AS char*)lds;
     // K fragment (A operand) of k-step ks, key block kb: plane 2 ks + hh, key 32 kb + r
     const unsigned kb0 = lds0 + hh * 1024 + r * 16;
+    // BIAS: k-step KSB's lanes past the head dim read the ones plane (V plane NCHL = tile plane 2 NCHL)
+    const unsigned kbb = (HD % 16 == 0 || hh == HHB) ? lds0 + 2 * NCHL * 1024 + r * 16 : kb0 + KSB * 2048;
+    auto kaddr = [&](int ks) { return (BIAS && ks == KSB) ? kbb : kb0 + ks * 2048; };
     // V^T fragment (A operand) of d-block db, key step (kb, s'): two transposed reads,
     // keys 32 kb + 16 s' + 8 j + 4 hh + q (j = 0, 1) at d = 32 db + 16 half + 4 p .. + 3
     unsigned vbj[2];
@@ -1526,7 +1536,7 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(MINW)))
             }
 #pragma unroll
             for (int ks = 0; ks < NKS; ++ks) {
-                const bf16x8 kf = *reinterpret_cast<const LDS_AS bf16x8*>((uintptr_t)(kb0 + so + kb * 512 + ks * 2048));
+                const bf16x8 kf = *reinterpret_cast<const LDS_AS bf16x8*>((uintptr_t)(kaddr(ks) + so + kb * 512));
                 z = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[ks], z, 0, 0, 0);
             }
             sc[kb] = z;
@@ -1544,12 +1554,44 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(MINW)))
     };
     // online softmax of one tile's scores: running max, lazy O rescale, P packed to bf16
     // (pk[2 kb + s'] = registers 8 s' .. 8 s' + 7 of key block kb)
-    auto softmax = [&](f32x16(&sc)[2], bf16x8(&pk)[4]) {
+    auto softmax = [&](f32x16(&sc)[2], bf16x8(&pk)[4], int t = 0) {
         float mloc = fmaxf(sc[0][0], sc[0][1]);
 #pragma unroll
         for (int e = 2; e < 16; ++e) mloc = fmaxf(mloc, sc[0][e]);
 #pragma unroll
         for (int e = 0; e < 16; ++e) mloc = fmaxf(mloc, sc[1][e]);
+        if constexpr (BIAS) {  // scores are c s - M: attn_hyb_kernel's XT 4 rescale
+            if (t == 0 || __builtin_amdgcn_ballot_w64(mloc > 8.0f)) {
+                const float mq = xmax32(mloc);
+                const float mn = bf2f(f2bf(mb + (t == 0 ? mq : fmaxf(mq, 0.f))));
+                const float d = mn - mb;  // exact: both bf16 values
+                if (t > 0) {
+                    const float alpha = __builtin_amdgcn_exp2f(-d);
+#pragma unroll
+                    for (int i = 0; i < NDB; ++i) o[i] *= alpha;
+                }
+#pragma unroll
+                for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+                    for (int e = 0; e < 16; ++e) sc[kb][e] -= d;
+                mb = mn;
+                uint4 w = __builtin_bit_cast(uint4, qf[KSB]);
+                const unsigned nb = __builtin_bit_cast(unsigned short, f2bf(-mn));
+                w.x = hh == HHB ? nb : w.x;  // Q^T row HD (row HD + 1 stays 0)
+                qf[KSB] = __builtin_bit_cast(bf16x8, w);
+            }
+#pragma unroll
+            for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+                for (int e = 0; e < 16; ++e) sc[kb][e] = __builtin_amdgcn_exp2f(sc[kb][e]);
+#pragma unroll
+            for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+                for (int sp = 0; sp < 2; ++sp)
+#pragma unroll
+                    for (int j = 0; j < 8; ++j) pk[2 * kb + sp][j] = f2bf(sc[kb][8 * sp + j]);
+            return;
+        }
         mloc = xmax32(mloc);
         const float mnew = fmaxf(m, mloc);
         if (__builtin_amdgcn_ballot_w64(THR ? (mloc - m) * c > 8.0f : mnew != m)) {
@@ -1646,14 +1688,14 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(MINW)))
             __builtin_amdgcn_s_barrier();
             if (t + 1 < nkt) issue(t + 1);
             qk(t, 0, sc);
-            softmax(sc, pk);
+            softmax(sc, pk, t);
             pv(0, pk, SKIP && t * 64 + 32 >= Tk);
             if (t + 1 < nkt) {
                 vm_wait<0>();
                 __builtin_amdgcn_s_barrier();
                 if (t + 2 < nkt) issue(t + 2);
                 qk(t + 1, TILE, sc);
-                softmax(sc, pk);
+                softmax(sc, pk, t + 1);
                 pv(TILE, pk, SKIP && (t + 1) * 64 + 32 >= Tk);
             }
         }
@@ -2099,6 +2141,12 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(2))) vo
 // XT (dev kinds 80-83): VALU trims. 1 = exp2 arguments as packed FMAs (RING 4's qks only; the same
 // per-element fma); 2 = rescale O only when some query's max grows by more than 2^8 in the exp2
 // domain (P <= 256 otherwise; the weight sums use the same stale max: not bit-identical to kind 62).
+// 4 (round 6, with 2; RING 2, hd 72) = the exp2 argument straight out of the QK^T MFMA: Q carries
+// the factor c = scale * log2(e) (8: the caller folded it into the Q projection; else multiplied in
+// here, one extra bf16 rounding of Q), and Q^T row 72 carries -M, the query's running max in that
+// domain held as a bf16 value, against a ones row of K (the hh = 1 lanes of the last k-step read the
+// ones plane instead of V plane 0), so the MFMA yields c s - M and the per-element FMA goes. The
+// threshold test is lane-local (max of the lane's 32 scores > 8); the first tile always sets M.
 template <int HD, int NW, int MINW, bool PRIO, int SKIP = 0, bool DBG = false, int RING = 2, int XT = 0>
 __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(MINW))) void attn_hyb_kernel(AttnArgs a) {
     static_assert(RING >= 2 && RING <= 4, "two to four ring slots");
@@ -2150,8 +2198,14 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(MINW)))
                 qf[ks] = *reinterpret_cast<const bf16x8*>(qrow + col);
             else
                 qf[ks] = bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
+            if constexpr ((XT & 4) && !(XT & 8)) {
+#pragma unroll
+                for (int j = 0; j < 8; ++j) qf[ks][j] = f2bf(bf2f(qf[ks][j]) * c);
+            }
         }
     }
+    static_assert(!(XT & 4) || (HD == 72 && RING == 2 && (XT & 2)), "the MFMA bias form: hd 72, RING 2, XT 2");
+    float mb = 0.f;  // XT 4: the running max M (bf16 value) that Q^T row 72 holds as -M
 
     int nkt = (Tk + 63) / 64;
     if (a.causal) nkt = min(nkt, (min(T, qb * QB + QB) + 63) / 64);
@@ -2179,6 +2233,9 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(MINW)))
 
     const unsigned lds0 = (unsigned)(uintptr_t)(LDS_AS char*)lds;
     const unsigned kb0 = lds0 + hh * 1024 + r * 16;  // K fragment: plane 2 ks + hh, key 32 kb + r
+    // XT 4: the last k-step's hh = 1 lanes (K dims 72..79) read the ones plane (plane 2 NCHL)
+    const unsigned kb4 = kb0 + (NKS - 1) * 2048 + ((XT & 4) ? hh * (2 * NCHL - 2 * NKS + 1) * 1024 : 0);
+    auto kaddr = [&](int ks) { return ((XT & 4) && ks == NKS - 1) ? kb4 : kb0 + ks * 2048; };
     unsigned vbj[2];
     {
         const int q = li >> 2, p = li & 3, pc = p >> 1;
@@ -2220,7 +2277,7 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(MINW)))
 #pragma unroll
                     for (int ks = 0; ks < NKS; ++ks) {
                         const bf16x8 kf =
-                            *reinterpret_cast<const LDS_AS bf16x8*>((uintptr_t)(kb0 + so + kb * 512 + ks * 2048));
+                            *reinterpret_cast<const LDS_AS bf16x8*>((uintptr_t)(kaddr(ks) + so + kb * 512));
                         z = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[ks], z, 0, 0, 0);
                     }
                     sc[kb] = z;
@@ -2238,7 +2295,7 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(MINW)))
             }
 #pragma unroll
             for (int ks = 0; ks < NKS; ++ks) {
-                const bf16x8 kf = *reinterpret_cast<const LDS_AS bf16x8*>((uintptr_t)(kb0 + so + kb * 512 + ks * 2048));
+                const bf16x8 kf = *reinterpret_cast<const LDS_AS bf16x8*>((uintptr_t)(kaddr(ks) + so + kb * 512));
                 z = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[ks], z, 0, 0, 0);
             }
             sc[kb] = z;
@@ -2263,6 +2320,37 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(MINW)))
         for (int e = 2; e < 16; ++e) mloc = fmaxf(mloc, sc[0][e]);
 #pragma unroll
         for (int e = 0; e < 16; ++e) mloc = fmaxf(mloc, sc[1][e]);
+        if constexpr (XT & 4) {
+            // scores are c s - M already; the first tile sets M (O is still zero), later tiles move
+            // it only when some lane's score exceeds 8 (P <= 256 otherwise)
+            if (t == 0 || __builtin_amdgcn_ballot_w64(mloc > 8.0f)) {
+                const float mq = xmax32(mloc);
+                const float mn = bf2f(f2bf(mb + (t == 0 ? mq : fmaxf(mq, 0.f))));  // >= mb for t > 0
+                const float d = mn - mb;  // exact: both bf16 values
+                if (t > 0) {
+                    const float alpha = __builtin_amdgcn_exp2f(-d);
+#pragma unroll
+                    for (int u = 0; u < 2; ++u) {
+                        const float au = __shfl(alpha, 16 * u + li, 64);
+#pragma unroll
+                        for (int i = 0; i < NDT; ++i) o[u][i] *= au;
+                    }
+                }
+#pragma unroll
+                for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+                    for (int e = 0; e < 16; ++e) sc[kb][e] -= d;
+                mb = mn;
+                uint4 w = __builtin_bit_cast(uint4, qf[NKS - 1]);
+                const unsigned nb = __builtin_bit_cast(unsigned short, f2bf(-mn));
+                w.x = hh ? nb : w.x;  // Q^T row 72 (row 73 stays 0)
+                qf[NKS - 1] = __builtin_bit_cast(bf16x8, w);
+            }
+#pragma unroll
+            for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+                for (int e = 0; e < 16; ++e) sc[kb][e] = __builtin_amdgcn_exp2f(sc[kb][e]);
+        } else {
         mloc = xmax32(mloc);
         const float mnew = fmaxf(m, mloc);
         if (__builtin_amdgcn_ballot_w64((XT & 2) ? (mloc - m) * c > 8.0f : mnew != m)) {
@@ -2289,6 +2377,7 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(MINW)))
                 if (!ONES) psum += sc[kb][e];
             }
         if (!ONES) lsum += psum;
+        }
         if (DBG && b == 1 && h == 8 && qb == 1 && wave == 2 && t == 1 && (lane == 14 || lane == 46))
             for (int kb = 0; kb < 2; ++kb)
                 printf("K%d E lane %d kb %d: %a %a %a %a %a %a %a %a %a %a %a %a %a %a %a %a\n", SKIP, lane, kb,
@@ -2353,7 +2442,7 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(MINW)))
 #pragma unroll
                 for (int ks = 0; ks < NKS; ++ks) {
                     const bf16x8 kf =
-                        *reinterpret_cast<const LDS_AS bf16x8*>((uintptr_t)(kb0 + so + kb * 512 + ks * 2048));
+                        *reinterpret_cast<const LDS_AS bf16x8*>((uintptr_t)(kaddr(ks) + so + kb * 512));
                     z = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[ks], z, 0, 0, 0);
                 }
                 sc[kb] = z;
@@ -3306,6 +3395,28 @@ bool launch_attn(int kind, const AttnArgs& a, int B, int T, int H, hipStream_t s
         } else {
             hipLaunchKernelGGL((attn_m32_kernel<HD, 8, 1, true>), dim3(cdiv(T, 256) * H * B), dim3(512), 0, st, a);
         }
+    } else if (kind == 99 || kind == 100 || kind == 101) {  // attn_m32_kernel with the exp2 argument from the
+                                                         // MFMA (BIAS; Q pre-scaled, mme_attention_qs only):
+                                                         // 99 / 100 = kind 87 (8 waves), 101 = kind 86 (9 waves, skip)
+        if constexpr (HD == 64)
+            return false;
+        else if (kind == 101)
+            hipLaunchKernelGGL((attn_m32_kernel<HD, 9, 1, true, false, false, true, true, true>),
+                               dim3(cdiv(T, 288) * H * B), dim3(576), 0, st, a);
+        else
+            hipLaunchKernelGGL((attn_m32_kernel<HD, 8, 1, true, false, false, false, true, true>),
+                               dim3(cdiv(T, 256) * H * B), dim3(512), 0, st, a);
+    } else if (kind == 97 || kind == 98) {  // kind 83 with the exp2 argument from the MFMA (XT 4): 97 scales Q
+                                            // here (one more bf16 rounding of Q), 98 takes Q pre-scaled
+                                            // (mme_attention_qs: production for hd 72 since round 6)
+        if constexpr (HD != 72)
+            return false;
+        else if (kind == 97)
+            hipLaunchKernelGGL((attn_hyb_kernel<HD, 8, 4, true, 2, false, 2, 6>), dim3(cdiv(T, 256) * H * B),
+                               dim3(512), 0, st, a);
+        else
+            hipLaunchKernelGGL((attn_hyb_kernel<HD, 8, 4, true, 2, false, 2, 14>), dim3(cdiv(T, 256) * H * B),
+                               dim3(512), 0, st, a);
     } else
         return launch_attn_dev<HD>(kind, a, B, T, H, st);
     return true;
@@ -3542,7 +3653,7 @@ inline int attn_default_form() { return 0; }
 #endif
 
 int attention_entry(int form, const void* qkv, int ld_qkv, void* out, int ld_out, int B, int T, int H, int hd,
-                    const int32_t* seq_lens, int causal, float scale, void* stream);
+                    const int32_t* seq_lens, int causal, float scale, bool qs, void* stream);
 }  // namespace
 
 #ifdef MME_DEV
@@ -3554,18 +3665,31 @@ extern "C" int mme_attention_variant(int v) {  // development build only
 
 extern "C" int mme_attention(const void* qkv, int ld_qkv, void* out, int ld_out, int B, int T, int H, int hd,
                              const int32_t* seq_lens, int causal, float scale, void* stream) {
-    return attention_entry(attn_default_form(), qkv, ld_qkv, out, ld_out, B, T, H, hd, seq_lens, causal, scale, stream);
+    return attention_entry(attn_default_form(), qkv, ld_qkv, out, ld_out, B, T, H, hd, seq_lens, causal, scale, false,
+                           stream);
 }
 
 extern "C" int mme_attention_form(int form, const void* qkv, int ld_qkv, void* out, int ld_out, int B, int T, int H,
                                   int hd, const int32_t* seq_lens, int causal, float scale, void* stream) {
     MME_REQUIRE(form == 0 || (form >= 30 && form <= 199), "mme_attention_form: form %d (0 or 30 + kind)", form);
-    return attention_entry(form, qkv, ld_qkv, out, ld_out, B, T, H, hd, seq_lens, causal, scale, stream);
+    return attention_entry(form, qkv, ld_qkv, out, ld_out, B, T, H, hd, seq_lens, causal, scale, false, stream);
+}
+
+extern "C" int mme_attention_qs(const void* qkv, int ld_qkv, void* out, int ld_out, int B, int T, int H, int hd,
+                                const int32_t* seq_lens, int causal, void* stream) {
+    return attention_entry(attn_default_form(), qkv, ld_qkv, out, ld_out, B, T, H, hd, seq_lens, causal, 0.f, true,
+                           stream);
+}
+
+extern "C" int mme_attention_qs_form(int form, const void* qkv, int ld_qkv, void* out, int ld_out, int B, int T,
+                                     int H, int hd, const int32_t* seq_lens, int causal, void* stream) {
+    MME_REQUIRE(form == 0 || (form >= 30 && form <= 199), "mme_attention_qs_form: form %d (0 or 30 + kind)", form);
+    return attention_entry(form, qkv, ld_qkv, out, ld_out, B, T, H, hd, seq_lens, causal, 0.f, true, stream);
 }
 
 namespace {
 int attention_entry(int form, const void* qkv, int ld_qkv, void* out, int ld_out, int B, int T, int H, int hd,
-                    const int32_t* seq_lens, int causal, float scale, void* stream) {
+                    const int32_t* seq_lens, int causal, float scale, bool qs, void* stream) {
     MME_REQUIRE(qkv && out, "mme_attention: null pointer");
     MME_REQUIRE(B >= 0 && T > 0 && H > 0, "mme_attention: bad shape");
     MME_REQUIRE(hd == 64 || hd == 72 || hd == 80, "mme_attention: head_dim %d unsupported (64/72/80)", hd);
@@ -3573,8 +3697,9 @@ int attention_entry(int form, const void* qkv, int ld_qkv, void* out, int ld_out
     MME_REQUIRE(ld_out % 4 == 0 && ld_out >= H * hd, "mme_attention: bad ld_out");
     MME_REQUIRE(((uintptr_t)qkv & 15) == 0 && ((uintptr_t)out & 7) == 0, "mme_attention: misaligned");
     if (B == 0) return MME_OK;
+    // exp(x*scale) = exp2(x*scale*log2 e); qs (mme_attention_qs): Q already carries scale*log2 e
     AttnArgs a{(const bf16*)qkv, (bf16*)out, seq_lens, ld_qkv, ld_out, T, H, hd, causal ? 1 : 0,
-               scale * 1.4426950408889634f};  // exp(x*scale) = exp2(x*scale*log2 e)
+               qs ? 1.0f : scale * 1.4426950408889634f};
     // kernel choice (tools/attn_bench.py): short sequences (T <= 128: one or two key tiles)
     // and head dim 64 (3 waves/SIMD already) -> register-staged attn_fwd_kernel; otherwise
     // LDS-DMA staging, 8 waves (256 queries) per block unless that pads the query range by
@@ -3618,6 +3743,9 @@ int attention_entry(int form, const void* qkv, int ld_qkv, void* out, int ld_out
     // (ViT-H at 455 / 512 images: 0.48 / 0.53 -> 0.45 / 0.49 ms, profiles/r05_v10_attn_vith_batches.log)
     // but 3 % slower inside the LAION-CLIP-H job (466 vs 480 us per launch, jobs level;
     // profiles/r05_v9_laion_kind94_vs_kind86_ab.log): not dispatched.
+    // Round 6: kind 98 = kind 83 with the exp2 argument c s - M out of the QK^T MFMA (mme_attention_qs: Q
+    // pre-scaled by c in the projection, Q^T row 72 = -M against a ones row of K): 1.48 -> 1.40 ms per
+    // 417-image launch, SigLIP job +0.8 % (profiles/r06_v5_*); chosen below when qs.
     int kind = T <= 64 ? 16
                : (T <= 128 || hd == 64) ? 89
                : (hd == 80 && pad9 * 10 < min(pad8, pad4) * 9) ? 86
@@ -3637,9 +3765,17 @@ int attention_entry(int form, const void* qkv, int ld_qkv, void* out, int ld_out
         return mme_check_launch("mme_attention");
     }
 #endif
+    // hd 72 with Q pre-scaled: kind 83's loop with the exp2 argument from the MFMA (kind 98, round 6: the
+    // per-score FMA goes); a forced kind 83 keeps its own loop (c = 1), the A/B and accuracy reference
+    if (qs && kind == 83) kind = 98;
     if (form >= 9 && form <= 16) kind = form - 9;  // dev: force a kernel
     if (form >= 30 && form <= 199) kind = form - 30;  // dev: force a kernel
     if ((kind == 16 || kind == 19 || kind == 66) && T > 64) kind = 0;  // the short kernels hold one 64-key tile
+    // kinds 97 / 98 are one kernel scaling Q itself / taking it pre-scaled
+    if (qs && kind == 97) kind = 98;
+    if (!qs && kind == 98) kind = 97;
+    MME_REQUIRE(qs || (kind != 99 && kind != 100 && kind != 101), "mme_attention: kind %d needs Q pre-scaled "
+                "(mme_attention_qs)", kind);
 #ifdef MME_DEV
     if (form >= 21 && form <= 26 && hd == 72) {  // dev: attn_dma_kernel<72,8,2> diagnostics
         const dim3 grid(cdiv(T, 256) * H * B), blk(512);

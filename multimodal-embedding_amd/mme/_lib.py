@@ -18,7 +18,7 @@ LIB_PATH = os.environ.get("MME_LIB", os.path.join(_HERE, "libmme_dev.so" if DEV 
 # MME_ACT_* / MME_PIX_* from include/mme.h
 ACT_NONE, ACT_GELU_TANH, ACT_QUICK_GELU, ACT_GELU_ERF, ACT_GEGLU_TANH = 0, 1, 2, 3, 4
 PIX_F32_NCHW, PIX_PATCHES = 0, 1
-ABI_VERSION = 8
+ABI_VERSION = 9
 BUILD_DEV = 1  # MME_BUILD_DEV
 
 # name -> (restype, argtypes)
@@ -39,6 +39,7 @@ SIGNATURES = {
                                    _P, _P]),
     "mme_layernorm": (c_int, [_P, c_int, _P, _P, _P, c_int, c_int, c_int, c_float, _P, _P]),
     "mme_attention": (c_int, [_P, c_int, _P, c_int, c_int, c_int, c_int, c_int, _P, c_int, c_float, _P]),
+    "mme_attention_qs": (c_int, [_P, c_int, _P, c_int, c_int, c_int, c_int, c_int, _P, c_int, _P]),
     "mme_probe_attention": (c_int, [_P, _P, c_int, _P, c_int, c_int, c_int, c_int, c_int, c_float, _P]),
     "mme_map_pool": (c_int, [_P, c_int, _P, c_int, _P, c_int, c_int, c_int, c_int, c_int, _P]),
     "mme_token_embed": (c_int, [_P, c_int, c_int, _P, _P, c_int, _P, c_int, _P]),
@@ -70,7 +71,7 @@ SIGNATURES = {
     "mme_attention_mqa": (c_int, [_P, c_int, _P, c_int, c_int, c_int, c_int, c_int, _P, _P, c_float, _P]),
 }
 # per-call kernel forms (ABI 8; mme.ops.kernel_forms): the entry point's arguments after an int form
-for _name in ("mme_gemm", "mme_gemm_lnfold", "mme_gemm_res_stats", "mme_attention", "mme_gemm_mx"):
+for _name in ("mme_gemm", "mme_gemm_lnfold", "mme_gemm_res_stats", "mme_attention", "mme_attention_qs", "mme_gemm_mx"):
     SIGNATURES[_name + "_form"] = (c_int, [c_int] + SIGNATURES[_name][1])
 
 

@@ -38,6 +38,10 @@ PRUNE_LAST = os.environ.get("MME_PRUNE_LAST", "1") != "0"
 # SigLIP's MAP head with the probe query absorbed into the key projection (mme_map_pool):
 # no [B*T, 2d] K / V projection; MME_MAP_ABSORB=0 runs the K / V GEMM + mme_probe_attention.
 MAP_ABSORB = os.environ.get("MME_MAP_ABSORB", "1") != "0"
+# Head dim 72 with T > 128 (SigLIP vision towers; round 6): the attention's scale * log2(e) folded into
+# the Q rows of the LayerNorm-folded QKV projection, attention through mme_attention_qs (kind 98: the
+# softmax's exp2 argument straight out of the QK^T MFMA). MME_Q_PRESCALE=0 keeps the plain entry.
+Q_PRESCALE = os.environ.get("MME_Q_PRESCALE", "1") != "0"
 
 
 class _Bufs:
@@ -99,11 +103,18 @@ def encoder_layer(x: torch.Tensor, L: LayerW, cfg: TowerConfig, B: int, T: int, 
         return False, x
     if LN_FOLD:  # layer_norm1 -> qkv and layer_norm2 -> fc1 folded (mme.h mme_gemm_lnfold)
         if L.fold is None:
-            L.fold = (ops.LNFolded(L.qkv_w, L.qkv_b, L.ln1_g, L.ln1_b), ops.LNFolded(L.fc1_w, L.fc1_b, L.ln2_g, L.ln2_b))
+            qs = None
+            if Q_PRESCALE and hd == 72 and T > 128:  # Q rows carry the attention's scale * log2(e)
+                qs = torch.ones(3 * d, dtype=torch.float32)
+                qs[:d] = ops.attention_q_scale(hd)
+            L.fold = (ops.LNFolded(L.qkv_w, L.qkv_b, L.ln1_g, L.ln1_b, row_scale=qs),
+                      ops.LNFolded(L.fc1_w, L.fc1_b, L.ln2_g, L.ln2_b))
+            L.q_prescaled = qs is not None
         fused = bufs.part is not None
         st = bufs.stats if (stats_in and fused) else ops.rowstats(x, cfg.eps, d=d, out=bufs.stats)
         qkv = ops.gemm_lnfold(x, L.fold[0], st, out=bufs.wide[:, : 3 * d])
-        a = ops.attention(qkv, B, T, H, hd, seq_lens=seq_lens, causal=causal, out=bufs.h)
+        a = ops.attention(qkv, B, T, H, hd, seq_lens=seq_lens, causal=causal, out=bufs.h,
+                          q_prescaled=L.q_prescaled)
         a, x = _pooled(a, x, rows)
         n = x.shape[0]
         mlp_flops = 2.0 * n * d * cfg.intermediate  # unpadded intermediate width

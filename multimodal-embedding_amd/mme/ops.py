@@ -26,7 +26,8 @@ _forms = threading.local()
 def kernel_forms(**forms: int):
     """Kernel forms for the calls this thread makes inside the block (bit-identity tests, A/B):
     gemm=47 (pipe6) / 48 (per-row statistics combine), mx=0 / 2 / 3 / 10 (earlier mx GEMM forms),
-    attention=30 + kind (force an attention kernel kind). Each call passes its form to the library
+    attention=30 + kind (force an attention kernel kind), attention_long=30 + kind (the same for calls
+    with T > 128 only, i.e. the vision towers: a job A/B that leaves text attention alone). Each call passes its form to the library
     through the mme_*_form entry points; the library itself holds no switch."""
     old = dict(getattr(_forms, "d", {}))
     _forms.d = {**old, **forms}
@@ -256,22 +257,35 @@ def gemm_lnfold(x: torch.Tensor, folded: "LNFolded", stats: torch.Tensor, *, act
     return out
 
 
+def attention_q_scale(hd: int, scale: Optional[float] = None) -> float:
+    """The factor mme_attention_qs expects in the Q columns: scale * log2(e) (scale = hd^-0.5)."""
+    return (hd ** -0.5 if scale is None else scale) * 1.4426950408889634
+
+
 class LNFolded:
     """nn.LayerNorm(gamma, beta) followed by nn.Linear(w, bias), folded for mme_gemm_lnfold:
-    w' = bf16(w * gamma) (per input column), cs = sum_k w'[n, k] (fp32), b' = bias + w . beta (fp32)."""
+    w' = bf16(w * gamma) (per input column), cs = sum_k w'[n, k] (fp32), b' = bias + w . beta (fp32).
+    row_scale (fp32 [N], optional) multiplies output row n of the linear map before w' is rounded
+    (the attention's Q rows by attention_q_scale: one bf16 rounding, as without it)."""
 
-    def __init__(self, w: torch.Tensor, bias: Optional[torch.Tensor], gamma: torch.Tensor, beta: torch.Tensor):
+    def __init__(self, w: torch.Tensor, bias: Optional[torch.Tensor], gamma: torch.Tensor, beta: torch.Tensor,
+                 row_scale: Optional[torch.Tensor] = None):
         K = w.shape[1]
         g = torch.zeros(K, dtype=torch.float32, device=w.device)
         bt = torch.zeros(K, dtype=torch.float32, device=w.device)
         g[: gamma.numel()] = gamma.float()  # K may be zero-padded past the LayerNorm width
         bt[: beta.numel()] = beta.float()
         wf = w.float()
+        bf = bias.float() if bias is not None else None
+        if row_scale is not None:
+            rs = row_scale.float().to(w.device)
+            wf = wf * rs[:, None]
+            bf = bf * rs[: bf.numel()] if bf is not None else None
         self.w = (wf * g).to(BF16).contiguous()
         self.cs = self.w.float().sum(dim=1).contiguous()
         b = wf @ bt
-        if bias is not None:
-            b[: bias.numel()] += bias.float()[: b.numel()]
+        if bf is not None:
+            b[: bf.numel()] += bf[: b.numel()]
         self.b = b.contiguous()
 
 
@@ -307,7 +321,11 @@ def l2norm(x: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
 
 # ---------------------------------------------------------------- attention
 def attention(qkv: torch.Tensor, B: int, T: int, H: int, hd: int, *, seq_lens: Optional[torch.Tensor] = None,
-              causal: bool = False, scale: Optional[float] = None, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+              causal: bool = False, scale: Optional[float] = None, out: Optional[torch.Tensor] = None,
+              q_prescaled: bool = False) -> torch.Tensor:
+    """softmax(Q K^T scale + mask) V per head (mme_attention). q_prescaled: the Q columns already hold
+    q * scale * log2(e) (LNFolded(row_scale=attention_q_scale(hd)) on the projection; mme_attention_qs),
+    and `scale` is not used."""
     _dev(qkv, seq_lens, out)
     if qkv.shape[0] != B * T:
         raise ValueError(f"attention: qkv has {qkv.shape[0]} rows, expected B*T={B * T}")
@@ -317,8 +335,14 @@ def attention(qkv: torch.Tensor, B: int, T: int, H: int, hd: int, *, seq_lens: O
         raise ValueError("attention: seq_lens must be int32 [B]")
     scale = hd ** -0.5 if scale is None else scale
     ev = KernelTimer.begin()
-    _call_form("mme_attention", "attention", qkv.data_ptr(), _rowmajor(qkv, "qkv"), out.data_ptr(),
-               _rowmajor(out, "out"), B, T, H, hd, _ptr(seq_lens), int(causal), float(scale), _stream())
+    fl = _form("attention_long") if T > 128 else None  # a job A/B of the long-sequence (vision) kernel only
+    entry = "mme_attention_qs" if q_prescaled else "mme_attention"
+    args = (qkv.data_ptr(), _rowmajor(qkv, "qkv"), out.data_ptr(), _rowmajor(out, "out"), B, T, H, hd,
+            _ptr(seq_lens), int(causal)) + (() if q_prescaled else (float(scale),)) + (_stream(),)
+    if fl is not None:
+        call(entry + "_form", int(fl), *args)
+    else:
+        _call_form(entry, "attention", *args)
     # T <= 64 (SigLIP text) runs attn_short_kernel: one key tile per (batch, head), HBM-bound (Q, K, V in, O out)
     KernelTimer.end(ev, "attention_short" if T <= 64 else "attention",
                     4.0 * B * H * T * T * hd * (0.5 if causal else 1.0), 8.0 * B * T * H * hd)

@@ -42,6 +42,7 @@ class LayerW:
     fc2_b: torch.Tensor
     mx: Optional[object] = None  # mme.mx.LayerMX: fp8 copies of qkv/fc1/fc2 (opt-in precision mode)
     fold: Optional[tuple] = None  # (ops.LNFolded qkv, ops.LNFolded fc1): LayerNorms folded into the weights
+    q_prescaled: bool = False  # fold[0]'s Q rows carry the attention's scale * log2(e) (mme_attention_qs)
 
 
 @dataclass

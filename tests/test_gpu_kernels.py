@@ -129,7 +129,7 @@ def test_attention(cuda, B, T, H, hd, causal, lens):
     torch.testing.assert_close(out.float(), ref, atol=2e-2, rtol=2e-2)
 
 
-PROD_ATTN_KINDS = (38, 41, 58, 62, 65, 83, 84, 86, 87, 88, 89, 94)  # in the production library; the rest are development forms (libmme_dev.so)
+PROD_ATTN_KINDS = (38, 41, 58, 62, 65, 83, 84, 86, 87, 88, 89, 94, 97)  # in the production library; the rest are development forms (libmme_dev.so)
 
 
 @pytest.mark.parametrize("kind", [k if k in PROD_ATTN_KINDS else pytest.param(k, marks=pytest.mark.dev)
@@ -340,6 +340,129 @@ def test_attention_threshold_vs_exact_rescale(cuda, hd, T, exact, thr):
           f"(kind {thr}); max {e_ex.max().item():.3g} / {e_th.max().item():.3g}")
     assert e_th.mean().item() <= 1.3 * e_ex.mean().item()
     assert e_th.max().item() <= 1.5 * e_ex.max().item() + 2.0 ** -7
+
+
+def _qs_inputs(B, T, H, hd, amp, g):
+    """fp32 Q / K / V draws; qkv = their bf16 roundings, qkv_s the same with Q rounded from
+    q * attention_q_scale(hd) (what the Q-scaled projection produces: one rounding either way)."""
+    q32, k32, v32 = (torch.randn(B * T, H * hd, device="cuda", generator=g) * amp for _ in range(3))
+    kb, vb = k32.to(torch.bfloat16), v32.to(torch.bfloat16)
+    qkv = torch.cat([q32.to(torch.bfloat16), kb, vb], 1)
+    qkv_s = torch.cat([(q32 * ops.attention_q_scale(hd)).to(torch.bfloat16), kb, vb], 1)
+    return q32, kb, vb, qkv, qkv_s
+
+
+def _hd72_production_kind(T):
+    """mme_attention's dispatch at head dim 72 (attention.hip attention_entry)."""
+    if T <= 64:
+        return 16
+    if T <= 128:
+        return 89
+    pad8, pad4, pad9 = -(-T // 256) * 256, -(-T // 128) * 128, -(-T // 288) * 288
+    if pad9 * 10 < min(pad8, pad4) * 9:
+        return 35
+    return 83 if pad8 * 10 <= pad4 * 11 else 14
+
+
+def _attn_f64(q32, kb, vb, B, T, H, hd, sl, causal):
+    q, k, v = (t.double().view(B, T, H, hd).transpose(1, 2) for t in (q32, kb, vb))
+    s = (q @ k.transpose(-1, -2)) * hd ** -0.5
+    mask = torch.zeros(B, 1, T, T, dtype=torch.bool, device="cuda")
+    if sl is not None:
+        mask |= (torch.arange(T, device="cuda")[None, :] >= sl[:, None].long())[:, None, None, :]
+    if causal:
+        mask |= torch.triu(torch.ones(T, T, dtype=torch.bool, device="cuda"), 1)
+    return (torch.softmax(s.masked_fill(mask, float("-inf")), -1) @ v).transpose(1, 2).reshape(B * T, H * hd)
+
+
+@pytest.mark.parametrize("B,T,H,causal,lens", [(8, 729, 16, False, None), (2, 520, 3, False, [520, 301]),
+                                                 (2, 200, 3, True, None), (3, 64, 2, False, [64, 1, 30]),
+                                                 (2, 65, 2, False, None), (2, 300, 3, True, [300, 280]),
+                                                 (1, 32, 2, False, None), (2, 769, 2, False, [769, 700]),
+                                                 (2, 1024, 4, False, None)])
+def test_attention_mfma_bias_vs_fp64(cuda, B, T, H, causal, lens):
+    """Kind 98 (round 6, production for hd 72 through mme_attention_qs): kind 83's loop with the exp2
+    argument c s - M produced by the QK^T MFMA -- Q arrives multiplied by c = scale log2 e (folded into
+    the Q projection before its one bf16 rounding), Q^T row 72 = -M against a ones row of K, M the
+    query's running max held as a bf16 value. Against an fp64 reference of the unrounded fp32 Q its
+    error stays at that of kind 83's loop on the same pre-scaled Q (mean within 1.15x, max within 1.5x
+    + 2^-7) and, where the sample is large, within 1.15x of kind 83 on the plain Q (one rounding of Q
+    either way), on the SigLIP and ColPali (T 1024) geometries and on padded, causal, one- and two-tile
+    sequences, with scores scaled up 4x as well (more rescales, larger M). Kind 97 (the same loop
+    scaling Q in the kernel: a second rounding of Q, 1.3x kind 83's mean error) is reported only."""
+    hd = 72
+    g = torch.Generator(device="cuda").manual_seed(B * T + 97)
+    sl = None if lens is None else torch.tensor(lens, dtype=torch.int32, device="cuda")
+    for amp in (1.5, 6.0):
+        q32, kb, vb, qkv, qkv_s = _qs_inputs(B, T, H, hd, amp, g)
+        ref = _attn_f64(q32, kb, vb, B, T, H, hd, sl, causal)
+        outs = {}
+        for kind in (83, 97):
+            with ops.kernel_forms(attention=30 + kind):
+                outs[kind] = ops.attention(qkv, B, T, H, hd, seq_lens=sl, causal=causal).double()
+        for kind in (83, 98):  # the same pre-scaled Q: kind 83's own loop at c = 1, and kind 98
+            with ops.kernel_forms(attention=30 + kind):
+                outs[f"{kind}qs"] = ops.attention(qkv_s, B, T, H, hd, seq_lens=sl, causal=causal,
+                                                  q_prescaled=True).double()
+        prod = ops.attention(qkv_s, B, T, H, hd, seq_lens=sl, causal=causal, q_prescaled=True).double()
+        torch.cuda.synchronize()
+        if _hd72_production_kind(T) == 83:  # where the plain entry runs kind 83, the qs entry runs kind 98
+            assert torch.equal(prod, outs["98qs"]), "the qs production dispatch is not kind 98"
+        assert torch.isfinite(outs["98qs"]).all()
+        e = {k: (o - ref).abs() for k, o in outs.items()}
+        print(f"B {B} T {T} amp {amp}: mean err " + " / ".join(f"{e[k].mean().item():.3g} ({k})" for k in e) +
+              "; max " + " / ".join(f"{e[k].max().item():.3g}" for k in e))
+        # the loop's arithmetic, same inputs: kind 98 against kind 83
+        assert e["98qs"].mean().item() <= 1.15 * e["83qs"].mean().item()
+        assert e["98qs"].max().item() <= 1.5 * e["83qs"].max().item() + 2.0 ** -7
+        if B * T * H >= 10000:  # the Q-scaled projection against the plain one (one rounding each)
+            assert e["98qs"].mean().item() <= 1.15 * e[83].mean().item()
+
+
+@pytest.mark.parametrize("hd,kind,ref", [(72, 99, 87), (80, 100, 87), (80, 101, 86)])
+@pytest.mark.parametrize("B,T,H,causal,lens", [(4, 730, 16, False, None), (8, 257, 16, False, None),
+                                                 (2, 520, 3, False, [520, 301]), (2, 200, 3, True, None),
+                                                 (2, 65, 2, False, None), (1, 32, 2, False, None),
+                                                 (3, 257, 5, False, [257, 100, 1])])
+def test_attention_m32_mfma_bias_vs_fp64(cuda, hd, kind, ref, B, T, H, causal, lens):
+    """Kinds 99-101 (round 6): attn_m32_kernel with attn_hyb_kernel's MFMA bias (Q^T row hd = -M against a
+    ones row of K; at hd 80 an extra k-step holds it), on the qs entry only. Same bounds as
+    test_attention_mfma_bias_vs_fp64 against the kernel they extend (87: 8-wave blocks, 86: 9-wave blocks
+    with the last-tile skip) run on the same pre-scaled Q at c = 1."""
+    g = torch.Generator(device="cuda").manual_seed(B * T + hd + kind)
+    sl = None if lens is None else torch.tensor(lens, dtype=torch.int32, device="cuda")
+    for amp in (1.5, 6.0):
+        q32, kb, vb, qkv, qkv_s = _qs_inputs(B, T, H, hd, amp, g)
+        refo = _attn_f64(q32, kb, vb, B, T, H, hd, sl, causal)
+        outs = {}
+        for k in (ref, kind):
+            with ops.kernel_forms(attention=30 + k):
+                outs[k] = ops.attention(qkv_s, B, T, H, hd, seq_lens=sl, causal=causal, q_prescaled=True).double()
+        torch.cuda.synchronize()
+        assert torch.isfinite(outs[kind]).all()
+        e = {k: (o - refo).abs() for k, o in outs.items()}
+        print(f"hd {hd} B {B} T {T} amp {amp}: mean err {e[ref].mean().item():.3g} ({ref}) / "
+              f"{e[kind].mean().item():.3g} ({kind}); max {e[ref].max().item():.3g} / {e[kind].max().item():.3g}")
+        assert e[kind].mean().item() <= 1.15 * e[ref].mean().item()
+        assert e[kind].max().item() <= 1.5 * e[ref].max().item() + 2.0 ** -7
+
+
+@pytest.mark.parametrize("B,T,H,hd,causal,lens", [(2, 729, 4, 72, False, None), (3, 64, 3, 72, False, [64, 1, 30]),
+                                                   (3, 77, 4, 64, True, [77, 9, 40]), (2, 577, 3, 64, False, None),
+                                                   (1, 730, 3, 80, False, None), (2, 257, 4, 80, False, [257, 100]),
+                                                   (2, 100, 2, 72, False, None), (2, 300, 2, 80, True, None)])
+def test_attention_qs_entry_every_kernel(cuda, B, T, H, hd, causal, lens):
+    """mme_attention_qs on every production kernel (short, attn_fwd, attn_m32, attn_hyb): with Q scaled by
+    attention_q_scale the outputs match the fp32 reference at test_attention's tolerance, like the plain
+    entry on the plain Q."""
+    g = torch.Generator(device="cuda").manual_seed(B * T + hd + 1)
+    sl = None if lens is None else torch.tensor(lens, dtype=torch.int32, device="cuda")
+    q32, kb, vb, qkv, qkv_s = _qs_inputs(B, T, H, hd, 1.5, g)
+    ref = _attn_f64(q32, kb, vb, B, T, H, hd, sl, causal)
+    out = ops.attention(qkv_s, B, T, H, hd, seq_lens=sl, causal=causal, q_prescaled=True)
+    plain = ops.attention(qkv, B, T, H, hd, seq_lens=sl, causal=causal)
+    torch.testing.assert_close(out.double(), ref, atol=2e-2, rtol=2e-2)
+    torch.testing.assert_close(plain.double(), ref, atol=2e-2, rtol=2e-2)
 
 
 @pytest.mark.dev

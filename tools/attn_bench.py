@@ -13,6 +13,9 @@ from mme import ops  # noqa: E402
 # --batch B overrides every case's batch (e.g. 417 = the SigLIP job's execution batch).
 VARIANTS = [int(v) for v in sys.argv[sys.argv.index("--variants") + 1].split(",")] if "--variants" in sys.argv else [0]
 BATCH = int(sys.argv[sys.argv.index("--batch") + 1]) if "--batch" in sys.argv else None
+# --qs: Q pre-scaled by ops.attention_q_scale(hd), every call through mme_attention_qs (round 6: kinds
+# 98-101 take their exp2 argument from the QK^T MFMA and exist on that entry only)
+QS = "--qs" in sys.argv
 
 CASES = [  # name, B, T, H, hd, causal
     ("siglip_vision", 256, 729, 16, 72, False),
@@ -30,13 +33,16 @@ if "--cases" in sys.argv:
     CASES = [c for c in CASES if c[0] in _want]
 def run(v, *args, **kw):
     with ops.kernel_forms(**({"attention": v} if v else {})):
-        return ops.attention(*args, **kw)
+        return ops.attention(*args, q_prescaled=QS, **kw)
 
 
 for (name, B, T, H, hd, causal), v in [(c, v) for c in CASES for v in VARIANTS]:
     B = BATCH or B
     torch.manual_seed(0)
-    qkv = torch.randn(B * T, 3 * H * hd, device="cuda").to(torch.bfloat16)
+    qkv = torch.randn(B * T, 3 * H * hd, device="cuda")
+    if QS:
+        qkv[:, : H * hd] *= ops.attention_q_scale(hd)
+    qkv = qkv.to(torch.bfloat16)
     out = torch.empty(B * T, H * hd, device="cuda", dtype=torch.bfloat16)
     ref = run(0, qkv, B, T, H, hd, causal=causal)
     run(v, qkv, B, T, H, hd, causal=causal, out=out)
