@@ -3767,7 +3767,10 @@ int attention_entry(int form, const void* qkv, int ld_qkv, void* out, int ld_out
 #endif
     // hd 72 with Q pre-scaled: kind 83's loop with the exp2 argument from the MFMA (kind 98, round 6: the
     // per-score FMA goes); a forced kind 83 keeps its own loop (c = 1), the A/B and accuracy reference
+    // (kinds 100 / 101 the same in attn_m32_kernel for hd 80: kinds 87 / 86 with an extra k-step for -M)
     if (qs && kind == 83) kind = 98;
+    if (qs && kind == 87) kind = 100;
+    if (qs && kind == 86) kind = 101;
     if (form >= 9 && form <= 16) kind = form - 9;  // dev: force a kernel
     if (form >= 30 && form <= 199) kind = form - 30;  // dev: force a kernel
     if ((kind == 16 || kind == 19 || kind == 66) && T > 64) kind = 0;  // the short kernels hold one 64-key tile

@@ -38,10 +38,15 @@ PRUNE_LAST = os.environ.get("MME_PRUNE_LAST", "1") != "0"
 # SigLIP's MAP head with the probe query absorbed into the key projection (mme_map_pool):
 # no [B*T, 2d] K / V projection; MME_MAP_ABSORB=0 runs the K / V GEMM + mme_probe_attention.
 MAP_ABSORB = os.environ.get("MME_MAP_ABSORB", "1") != "0"
-# Head dim 72 with T > 128 (SigLIP vision towers; round 6): the attention's scale * log2(e) folded into
-# the Q rows of the LayerNorm-folded QKV projection, attention through mme_attention_qs (kind 98: the
+# Head dims 72 / 80 with T > 128 (the vision towers; round 6): the attention's scale * log2(e) folded
+# into the Q rows of the QKV projection, attention through mme_attention_qs (kinds 98 / 100 / 101: the
 # softmax's exp2 argument straight out of the QK^T MFMA). MME_Q_PRESCALE=0 keeps the plain entry.
 Q_PRESCALE = os.environ.get("MME_Q_PRESCALE", "1") != "0"
+
+
+def q_prescale(cfg: TowerConfig, T: int) -> Optional[float]:
+    """The factor folded into a tower's Q projection (None: the plain attention entry)."""
+    return ops.attention_q_scale(cfg.head_dim) if Q_PRESCALE and cfg.head_dim in (72, 80) and T > 128 else None
 
 
 class _Bufs:
@@ -88,8 +93,9 @@ def encoder_layer(x: torch.Tensor, L: LayerW, cfg: TowerConfig, B: int, T: int, 
     act = ACTS[cfg.act]
     if L.mx is not None:  # fp8 mode: QKV / fc1 / fc2 on the block-scaled fp8 MFMA (mme/mx.py)
         hq = mx.layernorm(x, L.ln1_g, L.ln1_b, cfg.eps, out=bufs.hq)
-        qkv = mx.gemm(hq, L.mx.qkv, L.qkv_b, out=bufs.wide[:, : 3 * d])
-        a = ops.attention(qkv, B, T, H, hd, seq_lens=seq_lens, causal=causal, out=bufs.h)
+        qkv = mx.gemm(hq, L.mx.qkv, L.qkv_b if L.mx.qkv_b is None else L.mx.qkv_b, out=bufs.wide[:, : 3 * d])
+        a = ops.attention(qkv, B, T, H, hd, seq_lens=seq_lens, causal=causal, out=bufs.h,
+                          q_prescaled=L.mx.qkv_b is not None)
         a, x = _pooled(a, x, rows)
         n = x.shape[0]
         mlp_flops = 2.0 * n * d * cfg.intermediate
@@ -103,10 +109,10 @@ def encoder_layer(x: torch.Tensor, L: LayerW, cfg: TowerConfig, B: int, T: int, 
         return False, x
     if LN_FOLD:  # layer_norm1 -> qkv and layer_norm2 -> fc1 folded (mme.h mme_gemm_lnfold)
         if L.fold is None:
-            qs = None
-            if Q_PRESCALE and hd == 72 and T > 128:  # Q rows carry the attention's scale * log2(e)
+            qs, c = None, q_prescale(cfg, T)
+            if c is not None:  # Q rows carry the attention's scale * log2(e)
                 qs = torch.ones(3 * d, dtype=torch.float32)
-                qs[:d] = ops.attention_q_scale(hd)
+                qs[:d] = c
             L.fold = (ops.LNFolded(L.qkv_w, L.qkv_b, L.ln1_g, L.ln1_b, row_scale=qs),
                       ops.LNFolded(L.fc1_w, L.fc1_b, L.ln2_g, L.ln2_b))
             L.q_prescaled = qs is not None
@@ -376,10 +382,12 @@ class DualEncoder:
         """Opt-in fp8 precision mode (BASELINE configs[4]): quantise every encoder
         layer's QKV / fc1 / fc2 weights to mx8 once; forward passes then run those
         products on the block-scaled fp8 MFMA (mme/mx.py)."""
-        for tower in (self.weights.vision, self.weights.text):
+        vc = self.spec.vision
+        tv = vc.num_patches + (0 if self.spec.family == "siglip" else 1)
+        for tower, c in ((self.weights.vision, q_prescale(vc, tv)), (self.weights.text, None)):
             for L in tower.layers:
                 if L.mx is None:
-                    L.mx = mx.quantize_layer(L)
+                    L.mx = mx.quantize_layer(L, q_scale=c)
         self.precision = "fp8"
         return self
 

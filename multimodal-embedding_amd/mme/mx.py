@@ -127,11 +127,26 @@ class LayerMX:
     fc1: MXTensor
     fc2: MXTensor
     o: Optional[MXTensor] = None
+    qkv_b: Optional[torch.Tensor] = None  # q_scale: the QKV bias with its Q part scaled (bf16)
 
 
-def quantize_layer(L) -> LayerMX:
+def quantize_layer(L, q_scale: Optional[float] = None) -> LayerMX:
+    """q_scale (round 6): the attention's scale * log2(e) folded into the Q rows of the QKV weight before
+    quantisation and into the Q part of its bias (mme_attention_qs, models.q_prescale)."""
     o = quantize(L.o_w) if os.environ.get("MME_FP8_OPROJ") == "1" else None
-    return LayerMX(quantize(L.qkv_w), quantize(L.fc1_w), quantize(L.fc2_w), o)
+    w, qb = L.qkv_w, None
+    if q_scale is not None:
+        d = w.shape[0] // 3
+        wf = w.float()
+        wf[:d] *= q_scale
+        w = wf.to(ops.BF16)
+        if L.qkv_b is not None:
+            bf = L.qkv_b.float()
+            bf[:d] *= q_scale
+            qb = bf.to(ops.BF16)
+        else:
+            qb = torch.zeros(3 * d, dtype=ops.BF16, device=w.device)
+    return LayerMX(quantize(w), quantize(L.fc1_w), quantize(L.fc2_w), o, qb)
 
 
 # Whole-job fp8 drift bounds (BASELINE configs[4], DFN5B-H at 5 000 images x 25 000 captions): the same
