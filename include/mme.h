@@ -160,11 +160,13 @@ int mme_attention_qs(const void* qkv, int ld_qkv, void* out, int ld_out, int B, 
  *     47 = pipe6 (the bit-identity reference of pipe8 / pipe9), 48 = the per-row statistics
  *     combine (res_stats); other forms exist in the development build (libmme_dev.so) only;
  *   mme_attention_form: 0 = production, 30 + kind = kernel kind `kind` (production: 83 hd 72,
- *     86 / 87 hd 80, 89 hd 64; 94 = the persistent form of 86, measured and not dispatched);
+ *     86 / 87 hd 80, 89 hd 64; through mme_attention_qs(_form) 98 hd 72, 101 / 100 hd 80 -- 97 and 99 are
+ *     measured forms, 99-101 need Q pre-scaled; 94 = the persistent form of 86, measured and not dispatched);
  *   mme_gemm_mx_form (below): -1 = production (mx11 where its geometry holds -- with the bias loaded up
- *     front, the mx8 block absmax by DPP and quick_gelu in packed f32 where N % 4 == 0 (form 16) -- else
+ *     front, the mx8 block absmax by DPP and quick_gelu in packed f32 where N % 4 == 0 (form 17) -- else
  *     mx10), 11 = mx11 without those, 10 = mx10, 0 / 2 / 3 = earlier forms, 15 = mx11 with the
- *     bias loaded up front alone (N % 4 == 0, 8-B aligned bias), 16 = what production runs there;
+ *     bias loaded up front alone (N % 4 == 0, 8-B aligned bias), 16 = production there until round 6, 17 = 16 with
+ *     the mx8 output packed without the inactive clamp (what production runs there since round 6);
  *     12 / 14 = mx12 (persistent mx11 with / without the next tile's DMA under the epilogue; measured
  *     slower, not dispatched) exist in the development build only;
  *   two NON-dispatched GEMM forms stay in the production build on purpose, because production-suite

@@ -47,6 +47,24 @@ __device__ __forceinline__ uint2 mx_pack8(const float (&v)[8], int sb) {
     return make_uint2(lo, hi);
 }
 
+// mx_pack8 for the GEMM epilogue (round 6, FQ): no clamp and packed scaling. sb = mx_scale_byte(amax) makes
+// amax * 2^(127 - sb) <= 448 for every finite block: amax = (1 + m) 2^(E - 127) scales to (1 + m) 2^8 <= 448 for
+// m <= 0.75 and to (1 + m) 2^7 < 256 above (sb clamped at 1 only for amax < 2^-118, which scales below 1); so the
+// clamp never acts and the result is mx_pack8's, bit for bit. The epilogue's values are bf16-rounded, so sb <=
+// 247 and 2^(127 - sb) is a normal float, applied by one exact multiply (v_pk_mul_f32: two values per issue).
+__device__ __forceinline__ uint2 mx_pack8_fast(const float (&v)[8], int sb) {
+    const float m = __uint_as_float((unsigned)(254 - sb) << 23);
+    const f32x2 mm = {m, m};
+    const f32x2 s0 = f32x2{v[0], v[1]} * mm, s1 = f32x2{v[2], v[3]} * mm;
+    const f32x2 s2 = f32x2{v[4], v[5]} * mm, s3 = f32x2{v[6], v[7]} * mm;
+    unsigned lo = 0, hi = 0;
+    lo = __builtin_amdgcn_cvt_pk_fp8_f32(s0.x, s0.y, lo, false);
+    lo = __builtin_amdgcn_cvt_pk_fp8_f32(s1.x, s1.y, lo, true);
+    hi = __builtin_amdgcn_cvt_pk_fp8_f32(s2.x, s2.y, hi, false);
+    hi = __builtin_amdgcn_cvt_pk_fp8_f32(s3.x, s3.y, hi, true);
+    return make_uint2(lo, hi);
+}
+
 // Scale-plane row order (round 4): inside each 128-row group of a plane, row r is stored at
 // (r % 32) * 4 + (r % 128) / 32, so the 4 scale bytes a 32x32x64 MFMA lane needs for the rows
 // i * 32 + r (i = 0..3) of one block are one aligned dword (gemm_mx11: one 4-byte load per block).
@@ -142,7 +160,8 @@ __global__ __launch_bounds__(256) void layernorm_mx_kernel(const bf16* __restric
         }
         const int sb = mx_scale_byte(block_amax(a));
         if (ch < nch) {
-            *reinterpret_cast<uint2*>(q + (long)row * ldq + ch * 8) = mx_pack8(o, sb);
+            // the outputs are bf16-rounded: mx_pack8_fast is exact (round 6)
+            *reinterpret_cast<uint2*>(q + (long)row * ldq + ch * 8) = mx_pack8_fast(o, sb);
             if ((ch & 3) == 0) sc[(long)(ch >> 2) * rows_pad + mx_srow(row)] = (uint8_t)sb;
         }
     }
@@ -255,7 +274,8 @@ constexpr int MXW_PITCH = 144, MXW_LDS = 8 * 128 * MXW_PITCH;
 // BPRE (mx form 15, round 5): the wave's 32 bias values loaded up front as eight 8-B loads (one wait)
 // instead of four 2-B loads and a wait per column quad (needs N % 4 == 0 and an 8-B aligned bias:
 // a quad's columns are then all in range or all past N, so clamping the quad start is exact).
-template <int ACT, bool SWZ = true, bool SB = false, int PASSES = 1, bool BPRE = false, bool DPPA = false>
+// FQ (form 17, round 6): the mx8 output packed by mx_pack8_fast (bit-identical to mx_pack8).
+template <int ACT, bool SWZ = true, bool SB = false, int PASSES = 1, bool BPRE = false, bool DPPA = false, bool FQ = false>
 __device__ __forceinline__ void mx_epilogue_wave(const MxArgs& p, char* lds, f32x16 (&acc)[4][2], int m0, int n0,
                                                  int wave, int lane) {
     static_assert(PASSES == 1 || (PASSES == 2 && SWZ), "one or two staging passes");
@@ -362,7 +382,7 @@ __device__ __forceinline__ void mx_epilogue_wave(const MxArgs& p, char* lds, f32
             }
             const int sbyte = mx_scale_byte(DPPA ? block_amax_dpp(a) : block_amax(a));
             if (gr < p.M && gc < p.N) {
-                *reinterpret_cast<uint2*>(Cq + (size_t)gr * p.ldc + gc) = mx_pack8(f, sbyte);
+                *reinterpret_cast<uint2*>(Cq + (size_t)gr * p.ldc + gc) = FQ ? mx_pack8_fast(f, sbyte) : mx_pack8(f, sbyte);
                 if ((cc & 3) == 0) p.sc[(size_t)(gc >> 5) * p.sc_rows + mx_srow(gr)] = (uint8_t)sbyte;
             }
         }
@@ -804,7 +824,7 @@ __device__ __forceinline__ void mx11_mfma(f32x16& acc, const bf16x8 (&a)[2], con
     acc = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(bo, ao, acc, 0, 0, J, (int)sb, I, (int)sa);
 }
 
-template <int ACT, bool LATE, bool BPRE = false, bool DPPA = false>
+template <int ACT, bool LATE, bool BPRE = false, bool DPPA = false, bool FQ = false>
 __device__ __forceinline__ void mx11_tile(const MxArgs& p, char* lds, const int m0, const int n0, const int wave) {
     constexpr int UNIT = 32768;
     const int lane = threadIdx.x & 63;
@@ -976,10 +996,10 @@ __device__ __forceinline__ void mx11_tile(const MxArgs& p, char* lds, const int 
         for (int j = 0; j < 2; ++j) asm volatile("" : "+v"(acc[i][j]));
     // no LDS hazard: every wave's last fragment reads precede the barrier closing the late row's
     // last memory phase, which the early row passes before it writes its epilogue region
-    mx_epilogue_wave<ACT, true, true, 1, BPRE, DPPA>(p, lds, acc, m0, n0, wave, lane);
+    mx_epilogue_wave<ACT, true, true, 1, BPRE, DPPA, FQ>(p, lds, acc, m0, n0, wave, lane);
 }
 
-template <int GROUP_M, int ACT, bool BPRE = false, bool DPPA = false>
+template <int GROUP_M, int ACT, bool BPRE = false, bool DPPA = false, bool FQ = false>
 __global__ __launch_bounds__(512, 2) void gemm_mx11_kernel(MxArgs p) {
     __shared__ __attribute__((aligned(16))) char lds[5 * 32768];
     const int nbm = (p.M + 255) / 256, nbn = (p.N + 255) / 256;
@@ -988,26 +1008,26 @@ __global__ __launch_bounds__(512, 2) void gemm_mx11_kernel(MxArgs p) {
     tile_coords<GROUP_M>(tile, nbm, nbn, bm, bn);
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     if (wave >= 4)
-        mx11_tile<ACT, true, BPRE, DPPA>(p, lds, bm * 256, bn * 256, wave);
+        mx11_tile<ACT, true, BPRE, DPPA, FQ>(p, lds, bm * 256, bn * 256, wave);
     else
-        mx11_tile<ACT, false, BPRE, DPPA>(p, lds, bm * 256, bn * 256, wave);
+        mx11_tile<ACT, false, BPRE, DPPA, FQ>(p, lds, bm * 256, bn * 256, wave);
 }
 
-template <int GROUP_M, bool BPRE = false, bool DPPA = false>
+template <int GROUP_M, bool BPRE = false, bool DPPA = false, bool FQ = false>
 int launch_mx11(const MxArgs& a, hipStream_t s) {
     const dim3 grid(((a.M + 255) / 256) * ((a.N + 255) / 256)), block(512);
     switch (a.act) {
         case MME_ACT_GELU_TANH:
-            hipLaunchKernelGGL((gemm_mx11_kernel<GROUP_M, MME_ACT_GELU_TANH, BPRE, DPPA>), grid, block, 0, s, a);
+            hipLaunchKernelGGL((gemm_mx11_kernel<GROUP_M, MME_ACT_GELU_TANH, BPRE, DPPA, FQ>), grid, block, 0, s, a);
             break;
         case MME_ACT_QUICK_GELU:
-            hipLaunchKernelGGL((gemm_mx11_kernel<GROUP_M, MME_ACT_QUICK_GELU, BPRE, DPPA>), grid, block, 0, s, a);
+            hipLaunchKernelGGL((gemm_mx11_kernel<GROUP_M, MME_ACT_QUICK_GELU, BPRE, DPPA, FQ>), grid, block, 0, s, a);
             break;
         case MME_ACT_GELU_ERF:
-            hipLaunchKernelGGL((gemm_mx11_kernel<GROUP_M, MME_ACT_GELU_ERF, BPRE, DPPA>), grid, block, 0, s, a);
+            hipLaunchKernelGGL((gemm_mx11_kernel<GROUP_M, MME_ACT_GELU_ERF, BPRE, DPPA, FQ>), grid, block, 0, s, a);
             break;
         default:
-            hipLaunchKernelGGL((gemm_mx11_kernel<GROUP_M, MME_ACT_NONE, BPRE, DPPA>), grid, block, 0, s, a);
+            hipLaunchKernelGGL((gemm_mx11_kernel<GROUP_M, MME_ACT_NONE, BPRE, DPPA, FQ>), grid, block, 0, s, a);
             break;
     }
     return mme_check_launch("mme_gemm_mx");
@@ -1476,9 +1496,9 @@ inline int mx_default_form() { return -1; }
 #endif
 inline bool mx_form_ok(int v) {
 #ifdef MME_DEV
-    return v == -1 || v == 0 || v == 2 || v == 3 || v == 4 || v == 9 || v == 10 || v == 11 || v == 12 || v == 14 || v == 15 || v == 16;
+    return v == -1 || v == 0 || v == 2 || v == 3 || v == 4 || v == 9 || v == 10 || v == 11 || v == 12 || v == 14 || v == 15 || v == 16 || v == 17;
 #else
-    return v == -1 || v == 0 || v == 2 || v == 3 || v == 10 || v == 11 || v == 15 || v == 16;  // mx12: dev only
+    return v == -1 || v == 0 || v == 2 || v == 3 || v == 10 || v == 11 || v == 15 || v == 16 || v == 17;  // mx12: dev only
 #endif
 }
 
@@ -1625,8 +1645,11 @@ int gemm_mx_entry(int form, const void* A, int lda, const void* sa, int sa_rows,
     // bit-identical throughout; form 11 = mx11 without either, form 15 = the bias alone
     if (form == 15 && mx11_ok && N % 4 == 0 && ((uintptr_t)bias & 7) == 0)
         return launch_mx11<4, true>(a, as_stream(stream));
-    if (form != 10 && form != 11 && mx11_ok && N % 4 == 0 && ((uintptr_t)bias & 7) == 0)
+    // round 6, form 17 = form 16 with the mx8 output packed without the (inactive) clamp, scaled by packed multiplies
+    if (form == 16 && mx11_ok && N % 4 == 0 && ((uintptr_t)bias & 7) == 0)
         return launch_mx11<4, true, true>(a, as_stream(stream));
+    if (form != 10 && form != 11 && mx11_ok && N % 4 == 0 && ((uintptr_t)bias & 7) == 0)
+        return launch_mx11<4, true, true, true>(a, as_stream(stream));
     if (form != 10 && mx11_ok) return launch_mx11<4>(a, as_stream(stream));
     return launch_mx10<4>(a, as_stream(stream));
 }

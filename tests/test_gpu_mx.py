@@ -264,7 +264,8 @@ def test_gemm_mx12_bit_identical_to_mx11(cuda, M, N, K, kind):
     """Forms 12 / 14 (mx12: persistent mx11, the next tile's first DMA units under the epilogue or not,
     two-pass staging; measured slower, not dispatched; development build only), 15 (mx11 with the bias
     loaded up front) and 16
-    (+ the mx8 block absmax by DPP, quick_gelu in packed f32)
+    (+ the mx8 block absmax by DPP, quick_gelu in packed f32) and 17 (+ the mx8 output packed without the
+    inactive clamp, by packed multiplies; production since round 6)
     against form 11 (mx11) at DFN5B-H's execution batch (417 images x 730 tokens: many tiles per
     CU) for the three fp8 encoder GEMMs with their job epilogues, the minimum K and fewer tiles than CUs:
     bit-identical outputs and scales."""
@@ -275,7 +276,7 @@ def test_gemm_mx12_bit_identical_to_mx11(cuda, M, N, K, kind):
     res0 = rnd(M, N, gen=g)
     outs = []
     dev = (12, 14) if os.environ.get("MME_DEV") == "1" else ()   # mx12: development build only
-    for v in (11, 15, 16) + dev:
+    for v in (11, 15, 16, 17) + dev:
         with ops.kernel_forms(mx=v):
             if kind == "mx_out":
                 o = mx.MXTensor.empty(M, N, "cuda")
@@ -288,7 +289,7 @@ def test_gemm_mx12_bit_identical_to_mx11(cuda, M, N, K, kind):
         torch.cuda.synchronize()
     for o in outs[1:]:
         for p, q in zip(outs[0], o):
-            assert torch.equal(p, q), f"mx12 / form 15 differs from mx11 ({kind}, {M}x{N}x{K})"
+            assert torch.equal(p, q), f"mx12 / forms 15-17 differ from mx11 ({kind}, {M}x{N}x{K})"
 
 
 @pytest.mark.slow

@@ -33,7 +33,8 @@ def main():
     p.add_argument("--mx-variants", default="-1", help="mx GEMM forms to time with --mx (-1 = production, "
                    "10 = mx10, 0 = round-2 form, 2 = per-wave epilogue alone, 3 = + scale wave; dev: 4, 9)")
     p.add_argument("--mx-epi", default="none", help="mx8 epilogue: none | job (the fp8 job's: QKV bias, fc1 "
-                   "bias + quick_gelu to an mx8 output, fc2 bias + residual in place)")
+                   "bias + quick_gelu to an mx8 output, fc2 bias + residual in place) | bias | quick (bias + "
+                   "quick_gelu, bf16 out) | mx8 (bias, mx8 out): the parts of fc1's job epilogue")
     p.add_argument("--torch", action="store_true", help="also time torch F.linear (hipBLASLt) on each shape")
     p.add_argument("--epi", default="none", help="epilogue: none | bias | res (residual in place) | resstats (res + LayerNorm "
                    "statistics, mme_gemm_res_stats) | gelu (bias+gelu_tanh) | erf (bias+exact GELU) | quick (bias+quick_gelu)")
@@ -122,6 +123,13 @@ def main():
                     mkw.update(act=_lib.ACT_QUICK_GELU, out_mx=omx)
                 elif name.endswith("fc2"):
                     mkw.update(residual=C)
+            elif a.mx_epi in ("bias", "quick", "mx8"):
+                mkw = {"bias": bias}
+                if a.mx_epi == "quick":
+                    mkw.update(act=_lib.ACT_QUICK_GELU)
+                if a.mx_epi == "mx8":
+                    omx = mx.MXTensor.empty(M, N, "cuda")
+                    mkw.update(out_mx=omx)
             if "out_mx" not in mkw:
                 mkw["out"] = C
             first = None
