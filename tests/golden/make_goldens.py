@@ -259,7 +259,7 @@ def _fit_factors(F: np.ndarray, T: np.ndarray):
     return bf16_bits(torch.from_numpy(A.astype(np.float32))), B
 
 
-def make_e2e(main):
+def make_e2e(main, models=None, fname="e2e_fitted.npz"):
     """End-to-end parity fixture: the reference's own encode_data (main.py:386-438)
     -> compute_similarity_scores (main.py:440-475) -> compute_metrics_detailed (main.py:305-383, v28 I2T
     orientation) on inputs whose ranking is DECIDED beyond bf16 noise.
@@ -275,7 +275,9 @@ def make_e2e(main):
     mlp.fc2 (weight + bias, so image = r + fc2(h) hits the target) and text_model.head. They are
     stored as bf16 factors A [D, m], B [m, d] (weights_gen.factor_product rebuilds W = bf16(A B)
     bit-identically on any box; SHA-256 stored). The inputs are synthetic noise images and ragged
-    random-id captions (planted.e2e_inputs), encoded at the reference's --batch-size 32."""
+    random-id captions (planted.e2e_inputs), encoded at the reference's --batch-size 32.
+    `models` (default planted.E2E_MODELS) / `fname`: the ViT-H towers (planted.E2E_H_MODELS) are written to
+    e2e_fitted_h.npz by the same recipe ("e2e_h")."""
     from PIL import Image
     from transformers.models.siglip.image_processing_pil_siglip import SiglipImageProcessorPil
     from transformers.models.clip.image_processing_pil_clip import CLIPImageProcessorPil
@@ -284,9 +286,10 @@ def make_e2e(main):
     from planted import E2E_MODELS, e2e_inputs, graded_targets
     from weights_gen import factor_product
     caps, bs = 5, 32
-    out = {"models": np.array([m[0] for m in E2E_MODELS]), "caps": np.int64(caps), "batch_size": np.int64(bs)}
+    models = E2E_MODELS if models is None else models
+    out = {"models": np.array([m[0] for m in models]), "caps": np.int64(caps), "batch_size": np.int64(bs)}
     torch.set_num_threads(os.cpu_count() or 8)
-    for name, n, H in E2E_MODELS:
+    for name, n, H in models:
         spec = get_spec(name)
         key = name.replace("-", "_")
         imgs, rows = e2e_inputs(spec, n, H, caps)
@@ -386,8 +389,8 @@ def make_e2e(main):
         for k in ("img", "all", "t2i"):
             c = (e16[k] * out[f"{key}_{k}_f32"]).sum(1) / np.linalg.norm(e16[k], axis=1)
             print(f"e2e {name} {k}: bf16 vs fp32 reference cos min {c.min():.5f}", flush=True)
-    np.savez_compressed(os.path.join(HERE, "e2e_fitted.npz"), **out)
-    print("e2e_fitted.npz:", sum(v.nbytes for v in out.values()) / 1e6, "MB raw")
+    np.savez_compressed(os.path.join(HERE, fname), **out)
+    print(f"{fname}:", sum(v.nbytes for v in out.values()) / 1e6, "MB raw")
 
 
 def bits_f32(b):
@@ -990,7 +993,8 @@ if __name__ == "__main__":
              "config0": lambda: make_config0(main), "edge": lambda: make_edge(main),
              "winoground": make_winoground, "bootstrap": lambda: make_bootstrap(main),
              "colpali_full": lambda: make_colpali_full(main), "torch_topk": make_torch_topk,
-             "dense_ties": lambda: make_dense_ties(main), "e2e": lambda: make_e2e(main)}
+             "dense_ties": lambda: make_dense_ties(main), "e2e": lambda: make_e2e(main),
+             "e2e_h": lambda: make_e2e(main, __import__("planted").E2E_H_MODELS, "e2e_fitted_h.npz")}
     for name, fn in steps.items():
         if not only or name in only:
             fn()

@@ -125,6 +125,10 @@ def config0_inputs(spec, n_img: int = 64, caps: int = 5, seed: int = 21):
 
 
 E2E_MODELS = (("tiny-clip", 32, 112), ("tiny-siglip", 64, 112), ("OpenAI-CLIP-L", 64, 224), ("SigLIP-400M", 64, 224))
+# the ViT-H towers of BASELINE configs[2] (LAION-CLIP-H), configs[3] / [4] (Apple-DFN5B-H, bf16 and fp8) and
+# SURVEY §8 f4 (MetaCLIP-H14):
+# their own fixture file (e2e_fitted_h.npz), so e2e_fitted.npz stays as generated
+E2E_H_MODELS = (("LAION-CLIP-H", 64, 224), ("Apple-DFN5B-H", 64, 224), ("MetaCLIP-H14", 64, 224))
 
 
 def e2e_inputs(spec, n: int, H: int, caps: int = 5, seed: int = 41):
