@@ -1013,6 +1013,12 @@ __global__ __launch_bounds__(256, 3) void attn_short_kernel(AttnArgs a, int unit
     const int Tk = a.seq_lens ? a.seq_lens[b] : T;
     const float c = a.scale_log2;
 
+    // Q fragments, loaded unconditionally and zeroed past HD by a mask: the padding columns HD..HDP of
+    // the reduction read the next head's (or K's) columns of the same row, in bounds since
+    // h * HD + HDP <= 3 * H * HD <= ld. Round 6: the per-lane `if (col < HD)` load this replaces made
+    // hipcc copy the loaded value inside the branch, i.e. wait for it (s_waitcnt vmcnt(0)) before the
+    // first K / V load below was issued -- one HBM round trip in series per block.
+    typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));
     bf16x8 qf[2][NKS];
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
@@ -1020,27 +1026,41 @@ __global__ __launch_bounds__(256, 3) void attn_short_kernel(AttnArgs a, int unit
 #pragma unroll
         for (int ks = 0; ks < NKS; ++ks) {
             const int col = ks * 32 + 8 * g;
-            if (col < HD)
-                qf[u][ks] = *reinterpret_cast<const bf16x8*>(qrow + col);
-            else
-                qf[u][ks] = bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
+            const unsigned keep = col < HD ? 0xffffffffu : 0u;
+            const u32x4_t v = *reinterpret_cast<const u32x4_t*>(qrow + col);
+            qf[u][ks] = __builtin_bit_cast(bf16x8, v & u32x4_t{keep, keep, keep, keep});
         }
     }
-    // stage K and V of both units (rows past T clamped: finite, masked below)
+    // stage K and V of both units (rows past T clamped: finite, masked below): every load issued before the
+    // first LDS write, the units' K bases computed once (the per-chunk run-time division by H cost ~40
+    // instructions in front of each load)
+    constexpr int NLD = 4 * NCH / 256;
+    long kb[2];  // element offsets (not pointers: a pointer array indexed per lane became flat loads)
 #pragma unroll
-    for (int i = 0; i < 4 * NCH / 256; ++i) {
+    for (int s = 0; s < 2; ++s) {
+        const int un = min(pair * 2 + s, units - 1);
+        kb[s] = (long)(un / a.H) * T * a.ld + D + (un % a.H) * HD;
+    }
+    u16x8 kv[NLD];
+#pragma unroll
+    for (int i = 0; i < NLD; ++i) {
         const int ci = tid + i * 256;
         const int s = ci / (2 * NCH), r = ci % (2 * NCH);
         const bool isV = r >= NCH;
         const int row = (r % NCH) / NCHL, ch = (r % NCH) % NCHL;
-        const int un = min(pair * 2 + s, units - 1);
-        const int ub = un / a.H, uh = un % a.H;
-        const bf16* src = a.qkv + ((long)ub * T + min(row, T - 1)) * a.ld + (isV ? 2 : 1) * D + uh * HD + ch * 8;
-        const u16x8 v = *reinterpret_cast<const u16x8*>(src);
+        kv[i] = *reinterpret_cast<const u16x8*>(a.qkv + (s ? kb[1] : kb[0]) + (long)min(row, T - 1) * a.ld +
+                                                (isV ? D : 0) + ch * 8);
+    }
+#pragma unroll
+    for (int i = 0; i < NLD; ++i) {
+        const int ci = tid + i * 256;
+        const int s = ci / (2 * NCH), r = ci % (2 * NCH);
+        const bool isV = r >= NCH;
+        const int row = (r % NCH) / NCHL, ch = (r % NCH) % NCHL;
         if (isV)
-            *reinterpret_cast<u16x8*>(&Vs[s][row * VS + ch * 8]) = v;
+            *reinterpret_cast<u16x8*>(&Vs[s][row * VS + ch * 8]) = kv[i];
         else
-            *reinterpret_cast<u16x8*>(&Ks[s][row * KS + ch * 8]) = v;
+            *reinterpret_cast<u16x8*>(&Ks[s][row * KS + ch * 8]) = kv[i];
     }
     if (KZ > HD || VS > HD) {  // zero the padding columns (disjoint from the tile bytes)
         for (int i = tid; i < 2 * 64; i += 256) {
@@ -1144,6 +1164,162 @@ __global__ __launch_bounds__(256, 3) void attn_short_kernel(AttnArgs a, int unit
                     for (int r = 0; r < 4; ++r) v[r] = f2bf(o[u][dt][r] * inv);
                     *reinterpret_cast<bf16x4*>(orow + d0) = v;
                 }
+            }
+        }
+    }
+}
+
+// attn_short2_kernel (round 6, kind 102): sequences of 65..128 tokens at head dim 64 -- the CLIP
+// causal text towers (T 77: OpenAI-CLIP-L, LAION-CLIP-H, MetaCLIP, DFN5B-H). attn_fwd_kernel (kind 89)
+// runs them as a two-tile flash loop: Q and key tile 0 loaded, then tile 1 loaded while tile 0
+// computes -- two HBM round trips in series per block for a kernel that is HBM-bound (3.9 TB/s).
+// Here a block = one (batch, head) unit and 4 waves of 32 queries; Q, and K / V of all 128 key rows
+// (rows past T clamped: finite, masked), are loaded in one burst (8 + 4 loads per lane) before the
+// first LDS write; the scores of all 128 keys stay in registers, so the softmax is one pass (no
+// running max, no rescale). Waves whose 32 queries all lie past T only help load. Per-wave math is
+// attn_short_kernel's (S^T = K.Q^T, P in registers as the B operand of O^T = V^T.P^T, V^T by
+// ds_read_b64_tr_b16), over 8 key sub-tiles instead of 4.
+template <int HD>
+__global__ __launch_bounds__(256, 4) void attn_short2_kernel(AttnArgs a, int units) {
+    static_assert(HD == 64, "attn_short2_kernel: head dim 64 (the CLIP text towers)");
+    constexpr int NKS = HD / 32;
+    constexpr int KS = HD + 8;   // K LDS row stride (elements)
+    constexpr int VS = 80;       // V LDS row stride: conflict-free tr reads
+    constexpr int NCHL = HD / 8;
+    constexpr int NDT = HD / 16;
+    constexpr int NCH = 128 * NCHL;          // 16-B chunks per K (or V) image
+    constexpr int NLD = 2 * NCH / 256;       // K + V chunks per thread
+    __shared__ __attribute__((aligned(16))) bf16 Ks[128 * KS];
+    __shared__ __attribute__((aligned(16))) bf16 Vs[128 * VS];
+
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int g = lane >> 4, li = lane & 15;
+    const int T = a.T, D = a.H * HD;
+    int unit;  // XCD-aware: consecutive units (neighbouring heads of one sequence) on one XCD / L2
+    {
+        const int bid = blockIdx.x, nwg = gridDim.x;
+        const int xcd = bid & 7, loc = bid >> 3, q8 = nwg >> 3, r8 = nwg & 7;
+        unit = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + loc;
+    }
+    if (unit >= units) return;  // uniform over the block
+    const int b = unit / a.H, h = unit % a.H;
+    const bf16* base = a.qkv + (long)b * T * a.ld + h * HD;
+    const int qw0 = wave * 32;
+    const int Tk = a.seq_lens ? a.seq_lens[b] : T;
+    const float c = a.scale_log2;
+
+    bf16x8 qf[2][NKS];
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+        const bf16* qrow = base + (long)min(qw0 + u * 16 + li, T - 1) * a.ld;
+#pragma unroll
+        for (int ks = 0; ks < NKS; ++ks) qf[u][ks] = *reinterpret_cast<const bf16x8*>(qrow + ks * 32 + 8 * g);
+    }
+    u16x8 kv[NLD];
+#pragma unroll
+    for (int i = 0; i < NLD; ++i) {
+        const int ci = tid + i * 256;
+        const bool isV = ci >= NCH;
+        const int r = ci % NCH, row = r / NCHL, ch = r % NCHL;
+        kv[i] = *reinterpret_cast<const u16x8*>(base + (long)min(row, T - 1) * a.ld + (isV ? 2 * D : D) + ch * 8);
+    }
+#pragma unroll
+    for (int i = 0; i < NLD; ++i) {
+        const int ci = tid + i * 256;
+        const bool isV = ci >= NCH;
+        const int r = ci % NCH, row = r / NCHL, ch = r % NCHL;
+        if (isV)
+            *reinterpret_cast<u16x8*>(&Vs[row * VS + ch * 8]) = kv[i];
+        else
+            *reinterpret_cast<u16x8*>(&Ks[row * KS + ch * 8]) = kv[i];
+    }
+    __syncthreads();
+    if (qw0 >= T) return;  // wave-uniform; no barrier follows
+
+    f32x4 sc[2][8];
+#pragma unroll
+    for (int kt = 0; kt < 8; ++kt) {
+        const bf16* krow = Ks + (kt * 16 + li) * KS;
+        bf16x8 kf[NKS];
+#pragma unroll
+        for (int ks = 0; ks < NKS; ++ks) kf[ks] = *reinterpret_cast<const bf16x8*>(krow + ks * 32 + 8 * g);
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+            f32x4 z = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int ks = 0; ks < NKS; ++ks) z = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf[ks], qf[u][ks], z, 0, 0, 0);
+            sc[u][kt] = z;
+        }
+    }
+    // keys past the sequence (T < 128: clamped duplicate rows), past its length or the causal diagonal
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+        const int q = qw0 + u * 16 + li;
+        const int lim = a.causal ? min(Tk, q + 1) : Tk;  // valid keys: key < lim (<= T)
+#pragma unroll
+        for (int kt = 0; kt < 8; ++kt)
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+                if (kt * 16 + 4 * g + r >= lim) sc[u][kt][r] = -INFINITY;
+    }
+
+    float lsum[2];
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+        float mloc = -1e30f;
+#pragma unroll
+        for (int kt = 0; kt < 8; ++kt)
+            mloc = fmaxf(mloc, fmaxf(fmaxf(sc[u][kt][0], sc[u][kt][1]), fmaxf(sc[u][kt][2], sc[u][kt][3])));
+        mloc = xmax32(xmax16(mloc));
+        const float mc = mloc * c;
+        float psum = 0.f;
+#pragma unroll
+        for (int kt = 0; kt < 8; ++kt)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const float pv = __builtin_amdgcn_exp2f(__builtin_fmaf(sc[u][kt][r], c, -mc));
+                sc[u][kt][r] = pv;
+                psum += pv;
+            }
+        lsum[u] = xsum32(xsum16(psum));
+    }
+
+    f32x4 o[2][NDT];
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+#pragma unroll
+        for (int i = 0; i < NDT; ++i) o[u][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int hh = 0; hh < 4; ++hh) {
+        bf16x8 pb[2];
+#pragma unroll
+        for (int u = 0; u < 2; ++u)
+            pb[u] = __builtin_convertvector(__builtin_shufflevector(sc[u][2 * hh], sc[u][2 * hh + 1], 0, 1, 2, 3, 4, 5,
+                                                                    6, 7), bf16x8);
+        const int r1 = 32 * hh + 4 * g + (li >> 2);
+#pragma unroll
+        for (int dt = 0; dt < NDT; ++dt) {
+            const int col = dt * 16 + 4 * (li & 3);
+            const s16x4 v0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS_AS s16x4*)(Vs + r1 * VS + col));
+            const s16x4 v1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS_AS s16x4*)(Vs + (r1 + 16) * VS + col));
+            const bf16x8 vv = __builtin_bit_cast(bf16x8, __builtin_shufflevector(v0, v1, 0, 1, 2, 3, 4, 5, 6, 7));
+#pragma unroll
+            for (int u = 0; u < 2; ++u) o[u][dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vv, pb[u], o[u][dt], 0, 0, 0);
+        }
+    }
+
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+        const float inv = 1.0f / lsum[u];
+        const int q = qw0 + u * 16 + li;
+        if (q < T) {
+            bf16* orow = a.out + ((long)b * T + q) * a.ldo + h * HD;
+#pragma unroll
+            for (int dt = 0; dt < NDT; ++dt) {
+                bf16x4 v;
+#pragma unroll
+                for (int r = 0; r < 4; ++r) v[r] = f2bf(o[u][dt][r] * inv);
+                *reinterpret_cast<bf16x4*>(orow + dt * 16 + 4 * g) = v;
             }
         }
     }
@@ -3417,6 +3593,11 @@ bool launch_attn(int kind, const AttnArgs& a, int B, int T, int H, hipStream_t s
         else
             hipLaunchKernelGGL((attn_hyb_kernel<HD, 8, 4, true, 2, false, 2, 14>), dim3(cdiv(T, 256) * H * B),
                                dim3(512), 0, st, a);
+    } else if (kind == 102) {  // T <= 128 at head dim 64 (CLIP causal text): one burst of loads per unit
+        if constexpr (HD != 64)
+            return false;
+        else
+            hipLaunchKernelGGL((attn_short2_kernel<HD>), dim3(B * H), dim3(256), 0, st, a, B * H);
     } else
         return launch_attn_dev<HD>(kind, a, B, T, H, st);
     return true;
@@ -3746,7 +3927,10 @@ int attention_entry(int form, const void* qkv, int ld_qkv, void* out, int ld_out
     // Round 6: kind 98 = kind 83 with the exp2 argument c s - M out of the QK^T MFMA (mme_attention_qs: Q
     // pre-scaled by c in the projection, Q^T row 72 = -M against a ones row of K): 1.48 -> 1.40 ms per
     // 417-image launch, SigLIP job +0.8 % (profiles/r06_v5_*); chosen below when qs.
+    // Round 6: kind 102 (attn_short2_kernel) for 64 < T <= 128 at head dim 64 (the CLIP causal text towers, T 77):
+    // every load of a unit in one burst instead of kind 89's two-tile flash loop.
     int kind = T <= 64 ? 16
+               : (T <= 128 && hd == 64) ? 102
                : (T <= 128 || hd == 64) ? 89
                : (hd == 80 && pad9 * 10 < min(pad8, pad4) * 9) ? 86
                : hd == 80 && pad8 * 10 <= pad4 * 11 ? 87
@@ -3774,6 +3958,7 @@ int attention_entry(int form, const void* qkv, int ld_qkv, void* out, int ld_out
     if (form >= 9 && form <= 16) kind = form - 9;  // dev: force a kernel
     if (form >= 30 && form <= 199) kind = form - 30;  // dev: force a kernel
     if ((kind == 16 || kind == 19 || kind == 66) && T > 64) kind = 0;  // the short kernels hold one 64-key tile
+    if (kind == 102 && (T > 128 || hd != 64)) kind = 0;                 // attn_short2_kernel: 128 keys, hd 64
     // kinds 97 / 98 are one kernel scaling Q itself / taking it pre-scaled
     if (qs && kind == 97) kind = 98;
     if (!qs && kind == 98) kind = 97;

@@ -73,19 +73,36 @@ __device__ __forceinline__ float half_sum(float v) {
     return v;
 }
 
+// 16-B chunk ch of a row (8 bf16 as bits), or zeros when ch >= nch. The load itself is unconditional
+// (clamped to chunk nch - 1, nch >= 1) and masked afterwards, so every chunk of a row is in flight before
+// the first wait. Round 6: with the load inside a per-lane `if (ch < nch)`, hipcc waited for each chunk in
+// its branch (s_waitcnt vmcnt(0) after every load): one memory round trip per chunk in series.
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ u16x8 load_chunk_or_zero(const bf16* __restrict__ xr, int ch, int nch) {
+    const u32x4 u = *reinterpret_cast<const u32x4*>(xr + min(ch, nch - 1) * 8);
+    const unsigned m = ch < nch ? 0xffffffffu : 0u;
+    return __builtin_bit_cast(u16x8, u & u32x4{m, m, m, m});
+}
+
 template <int MAXC>
 __device__ __forceinline__ void ln_load_half(const bf16* __restrict__ xr, int nch, int hl, float (&v)[MAXC][8]) {
+    u16x8 u[MAXC];
+#pragma unroll
+    for (int c = 0; c < MAXC; ++c) u[c] = load_chunk_or_zero(xr, hl + 32 * c, nch);
+#pragma unroll
+    for (int c = 0; c < MAXC; ++c)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[c][e] = bits2f(u[c][e]);
+}
+
+// gamma / beta chunks of a half-wave row's lane (zeros past the row), issued with the row's own loads
+template <int MAXC>
+__device__ __forceinline__ void ln_load_affine_half(const bf16* __restrict__ g, const bf16* __restrict__ b, int nch,
+                                                    int hl, u16x8 (&gu)[MAXC], u16x8 (&bu)[MAXC]) {
 #pragma unroll
     for (int c = 0; c < MAXC; ++c) {
-        const int ch = hl + 32 * c;
-        if (ch < nch) {
-            const u16x8 u = *reinterpret_cast<const u16x8*>(xr + ch * 8);
-#pragma unroll
-            for (int e = 0; e < 8; ++e) v[c][e] = bits2f(u[e]);
-        } else {
-#pragma unroll
-            for (int e = 0; e < 8; ++e) v[c][e] = 0.f;
-        }
+        gu[c] = load_chunk_or_zero(g, hl + 32 * c, nch);
+        bu[c] = load_chunk_or_zero(b, hl + 32 * c, nch);
     }
 }
 

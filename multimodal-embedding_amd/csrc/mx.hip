@@ -137,26 +137,23 @@ __global__ __launch_bounds__(256) void layernorm_mx_kernel(const bf16* __restric
     const long src = idx ? idx[row] : row;
     const int nch = d >> 3;
     float v[MAXC][8];
+    u16x8 gu[MAXC], bu[MAXC];
     ln_load_half(x + src * ldx, nch, hl, v);
+    ln_load_affine_half(g, b, nch, hl, gu, bu);  // in flight with the row (round 6)
     float mean, rstd;
     ln_stats_half(v, nch, hl, d, eps, mean, rstd);
+    // every chunk computed without a branch (chunks past the row: x = gamma = beta = 0 give o = +0 exactly,
+    // as the explicit zeros did), so hipcc keeps the gamma / beta loads up with the row's instead of sinking
+    // them into per-chunk branches; only the stores are conditional
 #pragma unroll
     for (int c = 0; c < MAXC; ++c) {
         const int ch = hl + 32 * c;
-        if (c * 32 >= nch) break;  // uniform over the half wave
         float o[8];
         float a = 0.f;
-        if (ch < nch) {
-            const u16x8 gu = *reinterpret_cast<const u16x8*>(g + ch * 8);
-            const u16x8 bu = *reinterpret_cast<const u16x8*>(b + ch * 8);
 #pragma unroll
-            for (int e = 0; e < 8; ++e) {
-                o[e] = bf2f(f2bf((v[c][e] - mean) * rstd * bits2f(gu[e]) + bits2f(bu[e])));
-                a = fmaxf(a, fabsf(o[e]));
-            }
-        } else {
-#pragma unroll
-            for (int e = 0; e < 8; ++e) o[e] = 0.f;
+        for (int e = 0; e < 8; ++e) {
+            o[e] = bf2f(f2bf((v[c][e] - mean) * rstd * bits2f(gu[c][e]) + bits2f(bu[c][e])));
+            a = fmaxf(a, fabsf(o[e]));
         }
         const int sb = mx_scale_byte(block_amax(a));
         if (ch < nch) {

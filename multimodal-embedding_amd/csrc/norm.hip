@@ -9,18 +9,13 @@ constexpr int ROWS_PER_BLOCK = 4;  // 4 waves, one row each
 constexpr int MAXC = 4;            // 16-B chunks per lane: d <= 8*64*4 = 2048
 
 __device__ __forceinline__ void load_row(const bf16* xr, int nch, int lane, float (&v)[MAXC][8]) {
+    u16x8 u[MAXC];  // every chunk in flight before the first wait (common.h load_chunk_or_zero)
 #pragma unroll
-    for (int c = 0; c < MAXC; ++c) {
-        const int ch = lane + c * 64;
-        if (ch < nch) {
-            const u16x8 u = *reinterpret_cast<const u16x8*>(xr + ch * 8);
+    for (int c = 0; c < MAXC; ++c) u[c] = load_chunk_or_zero(xr, lane + c * 64, nch);
 #pragma unroll
-            for (int e = 0; e < 8; ++e) v[c][e] = bits2f(u[e]);
-        } else {
+    for (int c = 0; c < MAXC; ++c)
 #pragma unroll
-            for (int e = 0; e < 8; ++e) v[c][e] = 0.f;
-        }
-    }
+        for (int e = 0; e < 8; ++e) v[c][e] = bits2f(u[c][e]);
 }
 
 // nn.LayerNorm on a bf16 row (TF:models/siglip/modeling_siglip.py:329-331):
@@ -38,21 +33,19 @@ __global__ __launch_bounds__(256) void layernorm_kernel(const bf16* __restrict__
     const long src = idx ? idx[row] : row;
     const int nch = d >> 3;
     float v[MAXC][8];
+    u16x8 gu[MAXC], bu[MAXC];
     ln_load_half(x + src * ldx, nch, hl, v);
+    ln_load_affine_half(g, b, nch, hl, gu, bu);  // in flight with the row (round 6)
     float mean, rstd;
     ln_stats_half(v, nch, hl, d, eps, mean, rstd);
     bf16* yr = y + (long)row * ldy;
 #pragma unroll
-    for (int c = 0; c < MAXC; ++c) {
+    for (int c = 0; c < MAXC; ++c) {  // computed without a branch, stored where the chunk is in the row
         const int ch = hl + 32 * c;
-        if (ch < nch) {
-            const u16x8 gu = *reinterpret_cast<const u16x8*>(g + ch * 8);
-            const u16x8 bu = *reinterpret_cast<const u16x8*>(b + ch * 8);
-            bf16x8 o;
+        bf16x8 o;
 #pragma unroll
-            for (int e = 0; e < 8; ++e) o[e] = f2bf((v[c][e] - mean) * rstd * bits2f(gu[e]) + bits2f(bu[e]));
-            *reinterpret_cast<bf16x8*>(yr + ch * 8) = o;
-        }
+        for (int e = 0; e < 8; ++e) o[e] = f2bf((v[c][e] - mean) * rstd * bits2f(gu[c][e]) + bits2f(bu[c][e]));
+        if (ch < nch) *reinterpret_cast<bf16x8*>(yr + ch * 8) = o;
     }
 }
 

@@ -129,7 +129,7 @@ def test_attention(cuda, B, T, H, hd, causal, lens):
     torch.testing.assert_close(out.float(), ref, atol=2e-2, rtol=2e-2)
 
 
-PROD_ATTN_KINDS = (38, 41, 58, 62, 65, 83, 84, 86, 87, 88, 89, 94, 97)  # in the production library; the rest are development forms (libmme_dev.so)
+PROD_ATTN_KINDS = (38, 41, 58, 62, 65, 83, 84, 86, 87, 88, 89, 94, 97, 102)  # in the production library; the rest are development forms (libmme_dev.so)
 
 
 @pytest.mark.parametrize("kind", [k if k in PROD_ATTN_KINDS else pytest.param(k, marks=pytest.mark.dev)
@@ -445,6 +445,39 @@ def test_attention_m32_mfma_bias_vs_fp64(cuda, hd, kind, ref, B, T, H, causal, l
               f"{e[kind].mean().item():.3g} ({kind}); max {e[ref].max().item():.3g} / {e[kind].max().item():.3g}")
         assert e[kind].mean().item() <= 1.15 * e[ref].mean().item()
         assert e[kind].max().item() <= 1.5 * e[ref].max().item() + 2.0 ** -7
+
+
+@pytest.mark.parametrize("B,T,H,causal,lens", [(6, 77, 16, True, None), (5, 77, 16, True, [77, 9, 40, 1, 76]),
+                                                 (3, 65, 3, True, [65, 64, 2]), (2, 128, 5, False, None),
+                                                 (3, 100, 4, False, [100, 37, 99]), (4, 128, 3, True, [128, 127, 64, 65]),
+                                                 (2, 40, 2, True, None)])
+def test_attention_short2_vs_fp64(cuda, B, T, H, causal, lens):
+    """attn_short2_kernel (kind 102, round 6: production for 64 < T <= 128 at head dim 64, the CLIP causal text
+    towers) against the fp64 softmax attention, beside kind 89 (attn_fwd_kernel with the rescale threshold,
+    production before): mean / max error within 1.15x / 1.5x of kind 89's on the same inputs (one softmax pass
+    over all 128 keys instead of two online tiles), all outputs finite; T = 40 exercises the clamped rows."""
+    g = torch.Generator(device="cuda").manual_seed(B * T + H)
+    sl = None if lens is None else torch.tensor(lens, dtype=torch.int32, device="cuda")
+    hd = 64
+    for amp in (1.5, 4.0):
+        q32, kb, vb, qkv, _ = _qs_inputs(B, T, H, hd, amp, g)
+        refo = _attn_f64(q32, kb, vb, B, T, H, hd, sl, causal)
+        outs = {}
+        for kind in (89, 102):
+            with ops.kernel_forms(attention=30 + kind):
+                outs[kind] = ops.attention(qkv, B, T, H, hd, seq_lens=sl, causal=causal).double()
+        torch.cuda.synchronize()
+        assert torch.isfinite(outs[102]).all()
+        e = {k: (o - refo).abs() for k, o in outs.items()}
+        print(f"short2 B {B} T {T} H {H} causal {causal} amp {amp}: mean err {e[89].mean().item():.3g} (89) / "
+              f"{e[102].mean().item():.3g} (102); max {e[89].max().item():.3g} / {e[102].max().item():.3g}")
+        assert e[102].mean().item() <= 1.15 * e[89].mean().item()
+        assert e[102].max().item() <= 1.5 * e[89].max().item() + 2.0 ** -7
+    if T > 64:  # the production dispatch picks it
+        plain = ops.attention(qkv, B, T, H, hd, seq_lens=sl, causal=causal)
+        with ops.kernel_forms(attention=30 + 102):
+            forced = ops.attention(qkv, B, T, H, hd, seq_lens=sl, causal=causal)
+        assert torch.equal(plain, forced)
 
 
 @pytest.mark.parametrize("B,T,H,hd,causal,lens", [(2, 729, 4, 72, False, None), (3, 64, 3, 72, False, [64, 1, 30]),
