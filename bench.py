@@ -242,10 +242,10 @@ def fp8_drift(model_name, dev, imgs, t2i_ids, cap_ids, fp8_tables, img_batch, tx
     """fp8 against bf16 over the WHOLE job (checker; after the timed region, --fp8 only): the same
     weights (seed 0) loaded without the mx8 GEMMs encode the job's images and captions, and the
     job's fp8 tables are compared with them (mme.mx.job_drift: per-row cosine of the embeddings; the
-    I2T ranking -- every image against all 5n captions, mme_sim_topk -- as top-1 agreement on the rows
-    decided beyond the measured fp8 score perturbation (gated, with the decided count), and over all rows
-    plus top-10 overlap (reported); `drift_ok` against mme.mx.JOB_DRIFT_BOUNDS, which tests/test_gpu_mx.py
-    asserts on the same job)."""
+    T2I, I2T (every image against all 5n captions) and I2T_Sym rankings, mme_sim_topk, as top-1 agreement on
+    the rows decided beyond the measured fp8 score perturbation (gated, with the decided counts), and the I2T
+    agreement over all rows plus top-10 overlap (reported); `drift_ok` against mme.mx.JOB_DRIFT_BOUNDS, which
+    tests/test_gpu_mx.py asserts on the same job)."""
     from mme import mx
     from mme.models import load_model
     t0 = time.time()

@@ -948,6 +948,22 @@ __device__ __forceinline__ void gemm_epilogue_wave(const GemmArgs& p, char* lds,
             }
         }
     };
+    // FOLD 2 / 3 (bias; residual): the bias of the wave's FN column blocks, loaded ahead of the residual rows as
+    // raw bf16 bits (round 6). Loaded per column block inside the staging loop, each block's loads were
+    // followed by s_waitcnt vmcnt(0), which drained the residual rows issued just above (their latency no
+    // longer overlapped the staging) and put FN bias round trips in series. Used unconditionally below (zeros
+    // without a bias), so hipcc does not sink the loads back into the loop. FOLD 0 (form 93) keeps the loads
+    // in the loop: hoisted, its run-time-branched epilogue spills.
+    constexpr bool HOIST_BIAS = FOLD == 2 || FOLD == 3;
+    u16x4 bias4[C::FN];
+#pragma unroll
+    for (int j = 0; j < C::FN; ++j) bias4[j] = u16x4{0, 0, 0, 0};
+    if (HOIST_BIAS && p.bias) {  // one 8-B load per block: 4 columns from a multiple of 4 (N % 8 == 0; the
+                                 // launch takes FOLD 2 / 3 only for an 8-B aligned bias, bias_aligned)
+#pragma unroll
+        for (int j = 0; j < C::FN; ++j)
+            bias4[j] = *reinterpret_cast<const u16x4*>(p.bias + min(cn0 + j * 16 + 4 * g, p.N - 4));
+    }
     if constexpr (PASSES == 1) {
         if (!GLU && hres) {  // residual rows first: their latency overlaps the staging below
 #pragma unroll
@@ -980,6 +996,9 @@ __device__ __forceinline__ void gemm_epilogue_wave(const GemmArgs& p, char* lds,
             const float4 s4 = *reinterpret_cast<const float4*>(p.ln_cs + c4);
             bv[0] = b4.x, bv[1] = b4.y, bv[2] = b4.z, bv[3] = b4.w;
             cs[0] = s4.x, cs[1] = s4.y, cs[2] = s4.z, cs[3] = s4.w;
+        } else if (HOIST_BIAS) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) bv[r] = bits2f(bias4[j][r]);
         } else if (p.bias) {
 #pragma unroll
             for (int r = 0; r < 4; ++r) bv[r] = bf2f(p.bias[min(cn0 + j * 16 + 4 * g + r, p.N - 1)]);
@@ -1625,6 +1644,10 @@ int persistent_grid(int ntiles) {
     return std::min(ntiles, cus[dev]);
 }
 
+// FOLD 2 / 3 epilogues read the bias as 8-B groups of 4 columns (gemm_epilogue_wave, round 6); an unaligned
+// bias takes the run-time-branched FOLD 0 form (same arithmetic, bit-identical)
+inline bool bias_aligned(const GemmArgs& a) { return ((uintptr_t)a.bias & 7) == 0; }
+
 template <class C, int GROUP_M, bool SPLIT, bool SPEC = true>
 int launch_pipe10(const GemmArgs& a, hipStream_t s) {
     const int nbm = (a.M + C::BM - 1) / C::BM, nbn = (a.N + C::BN - 1) / C::BN;
@@ -1632,7 +1655,8 @@ int launch_pipe10(const GemmArgs& a, hipStream_t s) {
     const dim3 grid(persistent_grid(ntiles)), block(C::NT);
     // SPEC: the epilogue compiled for its operands (FOLD 1: LayerNorm fold; FOLD 2: bias; FOLD 3: residual,
     // activation-free only)
-    const int fold = !SPEC ? 0 : a.res ? (a.ln_stats || a.act != MME_ACT_NONE ? 0 : 3) : a.ln_stats ? 1 : 2;
+    const int fold = !SPEC ? 0 : a.res ? (a.ln_stats || a.act != MME_ACT_NONE || !bias_aligned(a) ? 0 : 3)
+                                : a.ln_stats ? 1 : bias_aligned(a) ? 2 : 0;
 #define MME_P10(ACT_)                                                                                          \
     if (fold == 1)                                                                                            \
         hipLaunchKernelGGL((gemm_pipe10_kernel<C, GROUP_M, ACT_, SPLIT, SPEC ? 1 : 0>), grid, block, 0, s, a); \
@@ -1747,7 +1771,7 @@ int launch_pipe9(const GemmArgs& a, hipStream_t s) {
     const int nbm = (a.M + C::BM - 1) / C::BM, nbn = (a.N + C::BN - 1) / C::BN;
     const dim3 grid(SPLIT ? split_tiles(nbm, a.N / C::BN) : nbm * nbn), block(C::NT);
     if constexpr (SPEC) {  // the activation-free epilogues compiled for their operands (gemm_epilogue_wave FOLD)
-        if (a.act == MME_ACT_NONE && !(a.res && a.ln_stats)) {
+        if (a.act == MME_ACT_NONE && !(a.res && a.ln_stats) && (a.ln_stats || bias_aligned(a))) {
             if (a.ln_stats)
                 hipLaunchKernelGGL((gemm_pipe9_kernel<C, GROUP_M, MME_ACT_NONE, SPLIT, PRIO, ESWZ, 1>), grid, block, 0, s, a);
             else if (a.res)
@@ -1756,7 +1780,7 @@ int launch_pipe9(const GemmArgs& a, hipStream_t s) {
                 hipLaunchKernelGGL((gemm_pipe9_kernel<C, GROUP_M, MME_ACT_NONE, SPLIT, PRIO, ESWZ, 2>), grid, block, 0, s, a);
             return mme_check_launch("mme_gemm");
         }
-        if (a.act == MME_ACT_GEGLU_TANH && !a.res && !a.ln_stats) {  // ColPali's gate / up GEMM: bias only
+        if (a.act == MME_ACT_GEGLU_TANH && !a.res && !a.ln_stats && bias_aligned(a)) {  // ColPali's gate / up: bias only
             hipLaunchKernelGGL((gemm_pipe9_kernel<C, GROUP_M, MME_ACT_GEGLU_TANH, SPLIT, PRIO, ESWZ, 2>), grid, block, 0, s,
                                a);
             return mme_check_launch("mme_gemm");

@@ -297,9 +297,10 @@ def test_fp8_dfn5b_whole_job_drift():
     """BASELINE configs[4] at its whole-job size: DFN5B-H, 5 000 synthetic images x 25 000 captions (+ the
     5 000 T2I captions), exactly bench.py --model Apple-DFN5B-H --fp8's inputs, execution batches and
     weights, encoded with the mx8 encoder GEMMs and in bf16. The job-level drift (mme.mx.job_drift: per-row
-    cosine; I2T top-1 agreement over all 5 000 x 25 000 on the rows whose bf16 top-1 / top-2 gap exceeds twice
-    the fp8 score perturbation measured on that row) must stay within mme.mx.JOB_DRIFT_BOUNDS with at least
-    JOB_DRIFT_MIN_DECIDED decided rows, the bounds the bench line's `drift_ok` reports against."""
+    cosine; top-1 agreement in T2I, I2T (5 000 x 25 000) and I2T_Sym on the rows whose bf16 top-1 / top-2 gap
+    exceeds twice the fp8 score perturbation measured on that row) must stay within mme.mx.JOB_DRIFT_BOUNDS
+    with at least JOB_DRIFT_MIN_DECIDED decided rows over the three protocols, the bounds the bench line's
+    `drift_ok` reports against."""
     import bench
     from mme import get_spec
     from mme.config import exec_batches
@@ -317,8 +318,10 @@ def test_fp8_dfn5b_whole_job_drift():
     d = mx.job_drift(tables[True], tables[False])
     print(f"fp8 vs bf16 over the whole job: {d}")
     import warnings
-    warnings.warn(f"fp8 whole-job drift: {d['i2t_decided_rows']} decided I2T rows, top-1 agreement there "
-                  f"{d['i2t_top1_agreement_decided']} (all rows {d['i2t_top1_agreement_all_rows']}); cos min img "
+    warnings.warn(f"fp8 whole-job drift: decided rows T2I {d['t2i_decided_rows']} / I2T {d['i2t_decided_rows']} / "
+                  f"Sym {d['sym_decided_rows']} (total {d['decided_rows_total']}), top-1 agreement there "
+                  f"{d['t2i_top1_agreement_decided']} / {d['i2t_top1_agreement_decided']} / "
+                  f"{d['sym_top1_agreement_decided']} (I2T all rows {d['i2t_top1_agreement_all_rows']}); cos min img "
                   f"{d['cos_img_min']} txt {d['cos_txt_min']}; drift_ok {d['drift_ok']}")
     assert d["drift_ok"], f"fp8 whole-job drift out of bounds: {d}"
 
