@@ -984,16 +984,27 @@ __device__ __forceinline__ void gemm_epilogue_wave(const GemmArgs& p, char* lds,
             lm[i] = -st.y * st.x;
         }
     }
+    // two passes (pipe10): the second walks the column blocks in reverse, so its first block's LayerNorm-fold
+    // constants are the ones the first pass loaded last (kept in registers over its stores) instead of a
+    // reload it would wait for at once (round 6)
+    float4 keep_b = {0.f, 0.f, 0.f, 0.f}, keep_s = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int ps = 0; ps < PASSES; ++ps) {
     if constexpr (PASSES > 1) load_res(ps);
 #pragma unroll
-    for (int j = 0; j < C::FN; ++j) {
+    for (int jx = 0; jx < C::FN; ++jx) {
+        const int j = PASSES == 2 && ps == 1 ? C::FN - 1 - jx : jx;
         float bv[4] = {0.f, 0.f, 0.f, 0.f}, cs[4] = {0.f, 0.f, 0.f, 0.f};
         if (lnf) {
             const int c4 = min(cn0 + j * 16 + 4 * g, p.N - 4);
-            const float4 b4 = *reinterpret_cast<const float4*>(p.ln_b + c4);
-            const float4 s4 = *reinterpret_cast<const float4*>(p.ln_cs + c4);
+            float4 b4, s4;
+            if (PASSES == 2 && ps == 1 && jx == 0) {
+                b4 = keep_b, s4 = keep_s;
+            } else {
+                b4 = *reinterpret_cast<const float4*>(p.ln_b + c4);
+                s4 = *reinterpret_cast<const float4*>(p.ln_cs + c4);
+            }
+            if (PASSES == 2 && ps == 0 && jx == C::FN - 1) keep_b = b4, keep_s = s4;
             bv[0] = b4.x, bv[1] = b4.y, bv[2] = b4.z, bv[3] = b4.w;
             cs[0] = s4.x, cs[1] = s4.y, cs[2] = s4.z, cs[3] = s4.w;
         } else if (HOIST_BIAS) {
