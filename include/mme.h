@@ -159,8 +159,8 @@ int mme_attention_qs(const void* qkv, int ld_qkv, void* out, int ld_out, int B, 
  *   mme_gemm_form / mme_gemm_lnfold_form / mme_gemm_res_stats_form: -1 = production,
  *     47 = pipe6 (the bit-identity reference of pipe8 / pipe9), 48 = the per-row statistics
  *     combine (res_stats); other forms exist in the development build (libmme_dev.so) only;
- *   mme_attention_form: 0 = production, 30 + kind = kernel kind `kind` (production: 83 hd 72,
- *     86 / 87 hd 80, 89 hd 64; through mme_attention_qs(_form) 98 hd 72, 101 / 100 hd 80 -- 97 and 99 are
+ *   mme_attention_form: 0 = production, 30 + kind = kernel kind `kind` (production: 16 T <= 64, 102 hd 64 with
+ *     64 < T <= 128 (round 6: the CLIP causal text towers), 83 hd 72, 86 / 87 hd 80, 89 hd 64; through mme_attention_qs(_form) 98 hd 72, 101 / 100 hd 80 -- 97 and 99 are
  *     measured forms, 99-101 need Q pre-scaled; 94 = the persistent form of 86, measured and not dispatched);
  *   mme_gemm_mx_form (below): -1 = production (mx11 where its geometry holds -- with the bias loaded up
  *     front, the mx8 block absmax by DPP and quick_gelu in packed f32 where N % 4 == 0 (form 17) -- else
