@@ -108,7 +108,7 @@ def synth_inputs(spec, n, caps, device):
 
 HBM_FAMILIES = {  # KernelTimer family -> the kernel(s) behind it (rocprof names)
     "preprocess": "resample_patch_p_kernel", "rowstats": "rowstats_kernel", "layernorm": "layernorm_kernel",
-    "l2norm": "l2norm_kernel", "attention_short": "attn_short_kernel"}
+    "l2norm": "l2norm_kernel", "attention_short": "attn_short_kernel", "attention_short2": "attn_short2_kernel"}
 
 
 def load_traffic(model, n, img_batch, txt_batch, fp8):

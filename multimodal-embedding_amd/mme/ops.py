@@ -343,9 +343,10 @@ def attention(qkv: torch.Tensor, B: int, T: int, H: int, hd: int, *, seq_lens: O
         call(entry + "_form", int(fl), *args)
     else:
         _call_form(entry, "attention", *args)
-    # T <= 64 (SigLIP text) runs attn_short_kernel: one key tile per (batch, head), HBM-bound (Q, K, V in, O out)
-    KernelTimer.end(ev, "attention_short" if T <= 64 else "attention",
-                    4.0 * B * H * T * T * hd * (0.5 if causal else 1.0), 8.0 * B * T * H * hd)
+    # T <= 64 (SigLIP text) runs attn_short_kernel: one key tile per (batch, head), HBM-bound (Q, K, V in, O out);
+    # 64 < T <= 128 at head dim 64 (the CLIP causal text towers, round 6) attn_short2_kernel, HBM-bound as well
+    fam = "attention_short" if T <= 64 else "attention_short2" if (T <= 128 and hd == 64) else "attention"
+    KernelTimer.end(ev, fam, 4.0 * B * H * T * T * hd * (0.5 if causal else 1.0), 8.0 * B * T * H * hd)
     return out
 
 

@@ -19,6 +19,7 @@ import json
 import os
 
 NAMED = ("resample_patch_p_kernel", "rowstats_kernel", "layernorm_kernel", "l2norm_kernel", "attn_short_kernel",
+         "attn_short2_kernel",
          "attn_hyb_kernel", "attn_m32_kernel", "attn_fwd_kernel", "sim_topk_kernel", "map_pool_kernel",
          "row_part_combine_lds_kernel", "layernorm_mx_kernel", "token_embed_kernel", "clip_embed_ln_kernel")
 
