@@ -985,6 +985,7 @@ def make_bootstrap(main):
 if __name__ == "__main__":
     torch.manual_seed(0)
     main = import_reference()
+    from planted import E2E_H_MODELS
     only = sys.argv[1:]
     steps = {"preprocess": make_preprocess, "l2norm": lambda: make_l2norm(main),
              "retrieval": lambda: make_retrieval(main), "full_retrieval": lambda: make_full_retrieval(main),
@@ -994,7 +995,7 @@ if __name__ == "__main__":
              "winoground": make_winoground, "bootstrap": lambda: make_bootstrap(main),
              "colpali_full": lambda: make_colpali_full(main), "torch_topk": make_torch_topk,
              "dense_ties": lambda: make_dense_ties(main), "e2e": lambda: make_e2e(main),
-             "e2e_h": lambda: make_e2e(main, __import__("planted").E2E_H_MODELS, "e2e_fitted_h.npz")}
+             "e2e_h": lambda: make_e2e(main, E2E_H_MODELS, "e2e_fitted_h.npz")}
     for name, fn in steps.items():
         if not only or name in only:
             fn()
