@@ -2439,7 +2439,16 @@ __global__ __launch_bounds__(256) void row_part_combine_lds_kernel(const float* 
     const int n4 = nr * nparts / 2;  // float4s of this block's rows (nparts even: the dispatcher's np % 2 check)
     const float4* src = reinterpret_cast<const float4*>(part + 2 * (size_t)r0 * nparts);
     float4* dst = reinterpret_cast<float4*>(sp);
-    for (int i = threadIdx.x; i < n4; i += 256) dst[i] = src[i];
+    // every load issued before the first LDS write (unconditional, clamped to the block's last float4;
+    // round 6): the strided `for (i = tid; i < n4; i += 256) dst[i] = src[i]` waited for each load in turn,
+    // up to COMBINE_MAXP / 2 memory round trips in series per block
+    constexpr int MAXL = COMBINE_MAXP / 2;
+    float4 v[MAXL];
+#pragma unroll
+    for (int k = 0; k < MAXL; ++k) v[k] = src[min((int)threadIdx.x + k * 256, n4 - 1)];
+#pragma unroll
+    for (int k = 0; k < MAXL; ++k)
+        if ((int)threadIdx.x + k * 256 < n4) dst[threadIdx.x + k * 256] = v[k];
     __syncthreads();
     const int rl = threadIdx.x;
     if (rl >= nr) return;
